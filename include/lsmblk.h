@@ -1,0 +1,167 @@
+/*
+ * lsmblk.h -- C ABI of the MI355X-native SSTable block codec (liblsmblk.so).
+ *
+ * Drop-in boundary for the CrystalAnalyst/Lsm block path (paths relative to the reference
+ * repository root).  Two halves:
+ *
+ *  1. Per-entry API, host-synchronous, mirroring the reference's Rust API one-to-one so that
+ *     SsTableBuilder / SsTable / SsTableIterator keep their call shape:
+ *       lsmblk_builder_*  <-  BlockBuilder          src/block/builder.rs:37-89
+ *       lsmblk_block_*    <-  Block::encode/decode  src/block.rs:14-34
+ *       lsmblk_iter_*     <-  BlockIterator         src/block/iterator.rs:37-139
+ *     (the reference calls these at src/table/builder.rs:34,55,62,113-114, src/table.rs:232,
+ *      src/table/iterator.rs:35,59,64,75-92).  `add` must answer "accepted?" synchronously,
+ *     so this half runs on the host CPU inside liblsmblk.so; it is product code, not a
+ *     fallback for the batch half.
+ *
+ *  2. Batch / device API (the HIP kernels, gfx950): whole flush / compaction batches.
+ *       lsmblk_decode_batch  replaces the per-block loop  SsTable::read_block -> Block::decode
+ *                            -> BlockIterator::next        (src/table.rs:213-233,
+ *                                                           src/table/iterator.rs:86-97)
+ *       lsmblk_encode_batch  replaces the per-entry loop  SsTableBuilder::add ->
+ *                            BlockBuilder::add / finish_block  (src/table/builder.rs:48-65,
+ *                                                           112-123), one segment per SST
+ *     All pointers are DEVICE pointers; calls are asynchronous on `stream` (a hipStream_t
+ *     passed as void*; NULL = the default stream).  Thread-safe per distinct context.
+ *
+ * Errors: every function returns 0 (LSMBLK_OK) or a negative LSMBLK_E_* code.  Where the
+ * reference panics (empty key builder.rs:55, empty build :82-83, malformed decode
+ * block.rs:25-27) the ABI returns an error code instead.
+ *
+ * Block format (bit-exact with the reference builder):
+ *   entry  = u16 prefix | u16 suffix_len | key[prefix..] | u64 ts | u16 value_len | value
+ *   block  = entry* | u16 offset* | u16 num_entries          (all integers big-endian)
+ *   prefix = LCP(key, first key of the block); fields use the reference's `as u16` wrap.
+ */
+#ifndef LSMBLK_H
+#define LSMBLK_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSMBLK_ABI_VERSION 1
+
+enum {
+  LSMBLK_OK = 0,
+  LSMBLK_E_INVAL = -1,     /* bad argument: empty key, empty build, bad segment table, misaligned output */
+  LSMBLK_E_MALFORMED = -2, /* a block does not parse (the reference would panic) */
+  LSMBLK_E_CAPACITY = -3,  /* an output buffer is too small; the stats hold the required sizes */
+  LSMBLK_E_NOMEM = -4,     /* host or device allocation failed */
+  LSMBLK_E_HIP = -5,       /* a HIP runtime call failed */
+  LSMBLK_E_TIMEOUT = -6,   /* a device-side look-back wait exceeded its bound (must not happen) */
+  LSMBLK_E_OVERFLOW = -7,  /* a batch total does not fit the u32 KV-stream offsets */
+  LSMBLK_E_INTERNAL = -8,  /* device self-check failed */
+};
+
+int lsmblk_abi_version(void);
+const char* lsmblk_strerror(int status);
+
+/* ------------------------------------------------------------------ per-entry (host) */
+typedef struct lsmblk_builder lsmblk_builder;
+typedef struct lsmblk_block lsmblk_block;
+typedef struct lsmblk_iter lsmblk_iter;
+
+/* BlockBuilder::new (builder.rs:37-44). NULL on allocation failure. */
+lsmblk_builder* lsmblk_builder_new(size_t block_size);
+void lsmblk_builder_free(lsmblk_builder* b);
+/* BlockBuilder::add (builder.rs:54-73). *accepted = 0 means "block full" (the reference's
+ * `false`); LSMBLK_E_INVAL for an empty key (the reference's assert!). */
+int lsmblk_builder_add(lsmblk_builder* b, const uint8_t* key, size_t klen, uint64_t ts,
+                       const uint8_t* val, size_t vlen, int* accepted);
+/* BlockBuilder::is_empty (builder.rs:76-78). */
+int lsmblk_builder_is_empty(const lsmblk_builder* b);
+/* estimated_size (builder.rs:48-50) == the encoded length finish() will produce. */
+size_t lsmblk_builder_estimated_size(const lsmblk_builder* b);
+/* build() + Block::encode() (builder.rs:81-89 + block.rs:14-22); the builder is reset to
+ * empty as SsTableBuilder::finish_block does (src/table/builder.rs:113). */
+int lsmblk_builder_finish(lsmblk_builder* b, uint8_t* out, size_t cap, size_t* len);
+/* build() without encode: hands the Block to the caller (refcount 1). */
+int lsmblk_builder_build(lsmblk_builder* b, lsmblk_block** out);
+
+/* Block::decode (block.rs:24-34). The returned block is reference counted (the reference
+ * shares it as Arc<Block>); iterators hold a reference. */
+int lsmblk_block_decode(const uint8_t* buf, size_t len, lsmblk_block** out);
+/* Block::encode (block.rs:14-22). */
+int lsmblk_block_encode(const lsmblk_block* blk, uint8_t* out, size_t cap, size_t* len);
+size_t lsmblk_block_encoded_len(const lsmblk_block* blk);
+/* Block { data, offsets } fields (block.rs:7-10). */
+int lsmblk_block_data(const lsmblk_block* blk, const uint8_t** data, size_t* len);
+int lsmblk_block_offsets(const lsmblk_block* blk, const uint16_t** offsets, size_t* n);
+void lsmblk_block_free(lsmblk_block* blk); /* drops one reference */
+
+/* BlockIterator (iterator.rs). seek_to_offset is the CORRECTED inverse of the builder: the
+ * 8-byte ts after the key suffix is skipped and returned as the key's ts (the reference
+ * reads value_len from the ts bytes, iterator.rs:133-134). */
+int lsmblk_iter_create_and_seek_to_first(lsmblk_block* blk, lsmblk_iter** out); /* :66-70 */
+int lsmblk_iter_create_and_seek_to_key(lsmblk_block* blk, const uint8_t* key, size_t klen,
+                                       lsmblk_iter** out);                         /* :73-77 */
+int lsmblk_iter_seek_to_first(lsmblk_iter* it);                                     /* :99-101 */
+int lsmblk_iter_seek_to_key(lsmblk_iter* it, const uint8_t* key, size_t klen);      /* :80-94 */
+int lsmblk_iter_next(lsmblk_iter* it);                                              /* :104-107 */
+int lsmblk_iter_is_valid(const lsmblk_iter* it);                                    /* :59-61 */
+/* key() (:51-53): pointer valid until the next seek/next; ts is the entry's timestamp. */
+int lsmblk_iter_key(const lsmblk_iter* it, const uint8_t** key, size_t* klen, uint64_t* ts);
+int lsmblk_iter_value(const lsmblk_iter* it, const uint8_t** val, size_t* vlen);    /* :55-57 */
+void lsmblk_iter_free(lsmblk_iter* it);
+
+/* ------------------------------------------------------------------ batch (device) */
+/* SoA KV stream in device memory (the decoded form of a batch of blocks):
+ *   keys[key_off[i] .. key_off[i+1]), vals[val_off[i] .. val_off[i+1]), ts[i],  i < n.
+ * key_off / val_off hold n+1 entries; arenas are limited to 4 GiB each per batch. */
+typedef struct {
+  uint8_t* keys;
+  uint32_t* key_off;
+  uint8_t* vals;
+  uint32_t* val_off;
+  uint64_t* ts;
+  uint64_t n;          /* encode input: number of entries. decode output: ignored */
+  uint64_t entry_cap;  /* decode output capacities: entries (key_off/val_off hold cap+1) */
+  uint64_t key_cap;    /*   bytes */
+  uint64_t val_cap;    /*   bytes */
+} lsmblk_kv_stream;
+
+/* Device-side result words (u64[LSMBLK_STATS_WORDS], device memory, written by the call):
+ *   decode: [0] entries  [1] key bytes  [2] value bytes  [3] error flags
+ *   encode: [0] blocks   [1] out bytes  [2] 0            [3] error flags             */
+#define LSMBLK_STATS_WORDS 4
+#define LSMBLK_ERR_MALFORMED 1u
+#define LSMBLK_ERR_CAPACITY 2u
+#define LSMBLK_ERR_OVERFLOW 4u
+#define LSMBLK_ERR_TIMEOUT 8u
+#define LSMBLK_ERR_SEGMENTS 16u
+#define LSMBLK_ERR_INTERNAL 32u
+#define LSMBLK_ERR_EMPTY_KEY 64u
+/* Map a stats[3] error-flag word (copied to the host) to an LSMBLK_E_* status. */
+int lsmblk_stats_status(uint64_t error_flags);
+
+typedef struct lsmblk_ctx lsmblk_ctx;
+/* One context per (device, stream user). Holds the look-back / plan workspace. */
+int lsmblk_ctx_create(int device, lsmblk_ctx** out);
+void lsmblk_ctx_destroy(lsmblk_ctx* ctx);
+/* Pre-size the workspace (optional; calls grow it on demand, which synchronizes). */
+int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entries,
+                       uint64_t max_segments);
+
+/* Decode nblk blocks (block b = blocks[blk_off[b] .. blk_off[b+1]), blk_off u64[nblk+1])
+ * into the SoA stream `out` (outputs must be 16-byte aligned).  Asynchronous: completion
+ * and error flags are in `stats` once the stream reaches this point. */
+int lsmblk_decode_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off,
+                        uint64_t nblk, const lsmblk_kv_stream* out, uint64_t* stats,
+                        void* stream);
+
+/* Encode the SoA stream `in` greedily into blocks of `block_size`, restarting the block
+ * packing at every segment start (seg_start u32[nseg+1], seg_start[0] = 0, seg_start[nseg]
+ * = in->n, non-decreasing), exactly as one SsTableBuilder per segment would.  Blocks are
+ * written tightly packed to `out` (16-byte aligned, out_cap bytes); blk_off (u64, room for
+ * blk_cap values) receives nblk+1 offsets. */
+int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* seg_start,
+                        uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
+                        uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,93 @@
+"""ctypes binding of liblsmblk.so (include/lsmblk.h).
+
+The library is built in-tree by lsm_amd/_build.py (``__graft_entry__.build()``).  There is
+no fallback: if the library is missing or fails to load, every call raises.
+"""
+import ctypes
+import os
+
+from . import _build
+
+_lib = None
+
+P, S, U32, U64, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+PP = ctypes.POINTER(ctypes.c_void_p)
+
+LSMBLK_OK = 0
+LSMBLK_E_INVAL = -1
+LSMBLK_E_MALFORMED = -2
+LSMBLK_E_CAPACITY = -3
+LSMBLK_E_NOMEM = -4
+LSMBLK_E_HIP = -5
+LSMBLK_E_TIMEOUT = -6
+LSMBLK_E_OVERFLOW = -7
+LSMBLK_E_INTERNAL = -8
+
+
+class LsmBlkError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        msg = lib().lsmblk_strerror(status).decode() if _lib is not None else str(status)
+        super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
+
+
+class KVStreamC(ctypes.Structure):
+    _fields_ = [("keys", P), ("key_off", P), ("vals", P), ("val_off", P), ("ts", P),
+                ("n", U64), ("entry_cap", U64), ("key_cap", U64), ("val_cap", U64)]
+
+
+# (name, restype, argtypes) for every symbol of include/lsmblk.h
+SIGNATURES = [
+    ("lsmblk_abi_version", I, []),
+    ("lsmblk_strerror", ctypes.c_char_p, [I]),
+    ("lsmblk_stats_status", I, [U64]),
+    ("lsmblk_builder_new", P, [S]),
+    ("lsmblk_builder_free", None, [P]),
+    ("lsmblk_builder_add", I, [P, P, S, U64, P, S, ctypes.POINTER(I)]),
+    ("lsmblk_builder_is_empty", I, [P]),
+    ("lsmblk_builder_estimated_size", S, [P]),
+    ("lsmblk_builder_finish", I, [P, P, S, ctypes.POINTER(S)]),
+    ("lsmblk_builder_build", I, [P, PP]),
+    ("lsmblk_block_decode", I, [P, S, PP]),
+    ("lsmblk_block_encode", I, [P, P, S, ctypes.POINTER(S)]),
+    ("lsmblk_block_encoded_len", S, [P]),
+    ("lsmblk_block_data", I, [P, PP, ctypes.POINTER(S)]),
+    ("lsmblk_block_offsets", I, [P, PP, ctypes.POINTER(S)]),
+    ("lsmblk_block_free", None, [P]),
+    ("lsmblk_iter_create_and_seek_to_first", I, [P, PP]),
+    ("lsmblk_iter_create_and_seek_to_key", I, [P, P, S, PP]),
+    ("lsmblk_iter_seek_to_first", I, [P]),
+    ("lsmblk_iter_seek_to_key", I, [P, P, S]),
+    ("lsmblk_iter_next", I, [P]),
+    ("lsmblk_iter_is_valid", I, [P]),
+    ("lsmblk_iter_key", I, [P, PP, ctypes.POINTER(S), ctypes.POINTER(U64)]),
+    ("lsmblk_iter_value", I, [P, PP, ctypes.POINTER(S)]),
+    ("lsmblk_iter_free", None, [P]),
+    ("lsmblk_ctx_create", I, [I, PP]),
+    ("lsmblk_ctx_destroy", None, [P]),
+    ("lsmblk_ctx_reserve", I, [P, U64, U64, U64]),
+    ("lsmblk_decode_batch", I, [P, P, P, U64, ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, P, U64, P, U64, P, P]),
+]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_build.SO):
+            raise RuntimeError(f"liblsmblk.so not built ({_build.SO}); run __graft_entry__.build()")
+        L = ctypes.CDLL(_build.SO)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.lsmblk_abi_version() != 1:
+            raise RuntimeError("liblsmblk.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(status, what=""):
+    if status != LSMBLK_OK:
+        raise LsmBlkError(status, what)
+    return status

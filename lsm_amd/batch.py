@@ -1,0 +1,173 @@
+"""Batch (device) API: whole flush / compaction batches through the HIP kernels.
+
+  decode_blocks  replaces SsTable::read_block -> Block::decode -> BlockIterator::next over a
+                 batch of blocks (reference src/table.rs:213-233, src/table/iterator.rs:86-97)
+  encode_kv      replaces SsTableBuilder::add -> BlockBuilder::add / finish_block over a batch
+                 of segments (reference src/table/builder.rs:48-65,112-123)
+
+Tensors live on a ROCm device (torch is only the allocator / stream provider).  The work
+is done by liblsmblk.so; there is no CPU path here.
+"""
+import ctypes
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ._lib import KVStreamC, LSMBLK_E_CAPACITY, LsmBlkError, check, lib
+
+STATS_WORDS = 4
+_ctx_lock = threading.Lock()
+_ctxs = {}
+
+
+def _ctx(device: int):
+    with _ctx_lock:
+        c = _ctxs.get(device)
+        if c is None:
+            h = ctypes.c_void_p()
+            check(lib().lsmblk_ctx_create(device, ctypes.byref(h)), "lsmblk_ctx_create")
+            c = _ctxs[device] = h.value
+        return c
+
+
+def _stream_ptr(stream, device):
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return s.cuda_stream
+
+
+def _dev_index(t: torch.Tensor) -> int:
+    if t.device.type != "cuda":
+        raise ValueError("batch API needs device tensors (ROCm); got " + str(t.device))
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None and t.numel() else None
+
+
+def _aligned_empty(nbytes: int, device) -> torch.Tensor:
+    # torch's caching allocator returns >=512-B aligned blocks; the kernels need 16 B.
+    t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+    assert t.data_ptr() % 16 == 0
+    return t
+
+
+@dataclass
+class KVStream:
+    """SoA KV stream on device: keys[key_off[i]:key_off[i+1]], vals[...], ts[i].
+
+    key_off / val_off are u32 stored in int32 tensors (n+1 entries); ts is u64 in int64.
+    """
+    keys: torch.Tensor
+    key_off: torch.Tensor
+    vals: torch.Tensor
+    val_off: torch.Tensor
+    ts: torch.Tensor
+    n: int
+
+    def _c(self, entry_cap=None, key_cap=None, val_cap=None):
+        return KVStreamC(_ptr(self.keys), _ptr(self.key_off), _ptr(self.vals), _ptr(self.val_off),
+                         _ptr(self.ts), self.n,
+                         self.n if entry_cap is None else entry_cap,
+                         self.keys.numel() if key_cap is None else key_cap,
+                         self.vals.numel() if val_cap is None else val_cap)
+
+    @staticmethod
+    def from_numpy(keys, key_off, vals, val_off, ts, device="cuda"):
+        dev = torch.device(device)
+        n = len(ts)
+        k = _aligned_empty(len(keys), dev)
+        v = _aligned_empty(len(vals), dev)
+        if len(keys):
+            k[:len(keys)].copy_(torch.from_numpy(np.ascontiguousarray(keys, np.uint8)))
+        if len(vals):
+            v[:len(vals)].copy_(torch.from_numpy(np.ascontiguousarray(vals, np.uint8)))
+        ko = torch.from_numpy(np.ascontiguousarray(key_off, np.uint32).view(np.int32)).to(dev)
+        vo = torch.from_numpy(np.ascontiguousarray(val_off, np.uint32).view(np.int32)).to(dev)
+        t = torch.from_numpy(np.ascontiguousarray(ts, np.uint64).view(np.int64)).to(dev)
+        return KVStream(k, ko, v, vo, t, n)
+
+    def to_numpy(self):
+        """-> (keys u8, key_off u32, vals u8, val_off u32, ts u64) trimmed to the stream."""
+        ko = self.key_off[:self.n + 1].cpu().numpy().view(np.uint32)
+        vo = self.val_off[:self.n + 1].cpu().numpy().view(np.uint32)
+        kb, vb = int(ko[-1]) if len(ko) else 0, int(vo[-1]) if len(vo) else 0
+        return (self.keys[:kb].cpu().numpy(), ko, self.vals[:vb].cpu().numpy(), vo,
+                self.ts[:self.n].cpu().numpy().view(np.uint64))
+
+
+def _status(stats: torch.Tensor) -> int:
+    return lib().lsmblk_stats_status(int(stats[3].item()) & 0xFFFFFFFFFFFFFFFF)
+
+
+def decode_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_cap, val_cap, stream=None):
+    """Asynchronous decode into preallocated buffers (no host sync). stats: int64[4] device."""
+    dev = _dev_index(blk_off)
+    c = out._c(entry_cap, key_cap, val_cap)
+    check(lib().lsmblk_decode_batch(_ctx(dev), _ptr(blocks), _ptr(blk_off), nblk, ctypes.byref(c),
+                                    stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_decode_batch")
+
+
+def decode_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None) -> KVStream:
+    """Decode blocks[blk_off[b]:blk_off[b+1]] for every b into a KVStream (synchronizes)."""
+    dev = torch.device("cuda", _dev_index(blk_off))
+    nblk = blk_off.numel() - 1
+    total = int(blocks.numel())
+    entry_cap = total // 16 + 1
+    key_cap, val_cap = total + 16, total + 16
+    for _ in range(2):
+        out = KVStream(_aligned_empty(key_cap, dev), torch.empty(entry_cap + 1, dtype=torch.int32, device=dev),
+                       _aligned_empty(val_cap, dev), torch.empty(entry_cap + 1, dtype=torch.int32, device=dev),
+                       torch.empty(max(entry_cap, 1), dtype=torch.int64, device=dev), 0)
+        stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+        decode_into(blocks, blk_off, nblk, out, stats, entry_cap, key_cap, val_cap, stream)
+        torch.cuda.synchronize(dev)
+        st = _status(stats)
+        s = stats.cpu().tolist()
+        if st == LSMBLK_E_CAPACITY:
+            entry_cap, key_cap, val_cap = max(s[0], 1), max(s[1], 16), max(s[2], 16)
+            continue
+        if st:
+            raise LsmBlkError(st, "decode_blocks")
+        out.n = s[0]
+        return out
+    raise LsmBlkError(LSMBLK_E_CAPACITY, "decode_blocks")
+
+
+def encode_bound(kv: KVStream, key_bytes: int, val_bytes: int):
+    """Exact worst-case output sizes: (bytes, blk_off entries)."""
+    return key_bytes + val_bytes + 18 * kv.n + 16, kv.n + 2
+
+
+def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: int, out, out_cap,
+                blk_off, blk_cap, stats, stream=None):
+    """Asynchronous encode into preallocated buffers (no host sync)."""
+    dev = _dev_index(seg_start)
+    c = kv._c()
+    check(lib().lsmblk_encode_batch(_ctx(dev), ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
+                                    _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
+                                    _stream_ptr(stream, dev)), "lsmblk_encode_batch")
+
+
+def encode_kv(kv: KVStream, seg_start, block_size: int, stream=None):
+    """Greedy block packing per segment -> (blocks u8 tensor, blk_off int64 tensor[nblk+1])."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    if not isinstance(seg_start, torch.Tensor):
+        seg_start = torch.from_numpy(np.ascontiguousarray(seg_start, np.uint32).view(np.int32))
+    seg_start = seg_start.to(dev)
+    nseg = seg_start.numel() - 1
+    kb = int(kv.key_off[kv.n].item()) if kv.n else 0
+    vb = int(kv.val_off[kv.n].item()) if kv.n else 0
+    out_cap, blk_cap = encode_bound(kv, kb & 0xFFFFFFFF, vb & 0xFFFFFFFF)
+    out = _aligned_empty(out_cap, dev)
+    blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    encode_into(kv, seg_start, nseg, block_size, out, out_cap, blk_off, blk_cap, stats, stream)
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "encode_kv")
+    nblk, nbytes = stats[0].item(), stats[1].item()
+    return out[:nbytes], blk_off[:nblk + 1]

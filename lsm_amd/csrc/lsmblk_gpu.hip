@@ -1,0 +1,1243 @@
+// lsmblk_gpu.hip -- batch half of the C ABI (include/lsmblk.h): SSTable block decode and
+// encode as hand-written HIP kernels for gfx950 (MI355X, CDNA4, wave64).
+//
+// Reference semantics (paths relative to the reference repository):
+//   encode: BlockBuilder::add / build / Block::encode  src/block/builder.rs:54-89,
+//           src/block.rs:14-22, driven per segment like SsTableBuilder::add
+//           src/table/builder.rs:48-65, 112-123
+//   decode: Block::decode src/block.rs:24-34 + the corrected BlockIterator walk
+//           src/block/iterator.rs:23-34, 99-139
+//
+// Kernels (DESIGN.md has the data layout and the roofline of each):
+//   decode_kernel   one wave per block (4 blocks per 256-thread workgroup).  The block is
+//                   staged into LDS with 16-B buffer loads, entries are parsed one per lane,
+//                   the block's (entries, key bytes, value bytes) are published and the
+//                   output bases found by a wave-parallel decoupled look-back over
+//                   data-tagged 8-byte granules; keys, values and per-entry metadata are
+//                   then written with coalesced, aligned stores.
+//   plan_kernel     one wave per segment: the greedy block-boundary walk (the only serial
+//                   dependency of the format) 64 candidate entries per step with a wave
+//                   prefix sum + ballot; segment totals via the same look-back.
+//   emit_kernel     one wave per output block: keys/values staged into LDS, headers written
+//                   by entry lanes, value bytes moved as aligned dwords, the block image
+//                   flushed with 16-B stores.
+// Blocks or batches that exceed the LDS fast paths take per-entry-lane "simple" paths
+// that read/write global memory directly (same results, slower).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "lsmblk.h"
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr uint32_t kSpinLimit = 1u << 22;  // look-back bound (~seconds); never reached when correct
+
+// ---------------------------------------------------------------- wave primitives
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return (uint64_t(uni(uint32_t(x >> 32))) << 32) | uni(uint32_t(x));
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    T t = __shfl_up(v, d, 64);
+    if (l >= d) v += t;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)nbytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF); }
+
+// ---------------------------------------------------------------- look-back granules
+// 8-byte granule = value << 16 | epoch << 2 | flag  (flag 1 = aggregate, 2 = inclusive).
+// Written by one relaxed agent-scope store (global_store sc1), read by relaxed agent-scope
+// loads: the value and its tag travel in one naturally aligned 8-byte word, so no fence is
+// needed (MI355X_MICROARCH.md, "granule" hand-off).
+__device__ __forceinline__ uint64_t gload(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NQ>
+__device__ __forceinline__ void publish(uint64_t* arr, uint64_t idx, const uint64_t (&v)[NQ],
+                                        uint32_t tag, uint32_t flag) {
+  const uint32_t l = lane_id();
+  if (l < NQ) {
+    uint64_t x = v[0];
+    if (NQ > 1 && l == 1) x = v[1 % NQ];
+    if (NQ > 2 && l == 2) x = v[2 % NQ];
+    gstore(arr + idx * NQ + l, (x << 16) | (uint64_t(tag) << 2) | flag);
+  }
+}
+
+// Wave-parallel decoupled look-back: lane j inspects predecessor (pred - j).  Returns false
+// on timeout (then excl is garbage and the caller raises LSMBLK_ERR_TIMEOUT).
+template <int NQ>
+__device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self, uint32_t tag,
+                         uint64_t (&excl)[NQ]) {
+  const uint32_t l = lane_id();
+  const uint64_t want_agg = (uint64_t(tag) << 2) | 1, want_inc = (uint64_t(tag) << 2) | 2;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) excl[q] = 0;
+  int64_t pred = int64_t(self) - 1;
+  uint32_t spins = 0;
+  while (pred >= 0) {
+    const int64_t idx = pred - int64_t(l);
+    for (;;) {
+      uint64_t vi[NQ], va[NQ];
+      bool li = true, la = true;
+      if (idx >= 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          vi[q] = gload(inc + idx * NQ + q);
+          li = li && ((vi[q] & 0xFFFF) == want_inc);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          va[q] = gload(agg + idx * NQ + q);
+          la = la && ((va[q] & 0xFFFF) == want_agg);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) vi[q] = va[q] = 0;
+      }
+      const uint64_t im = __ballot(li);
+      const uint64_t rm = __ballot(li || la);
+      const uint32_t first = im ? uint32_t(__builtin_ctzll(im)) : 64u;
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+      if ((rm & need) == need) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const uint64_t c = l < first ? (va[q] >> 16) : (l == first ? (vi[q] >> 16) : 0);
+          excl[q] += wave_sum(c);
+        }
+        if (first < 64) return true;
+        pred -= 64;
+        break;
+      }
+      if (++spins > kSpinLimit) return false;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr) {
+  uint32_t t = 0;
+  if (lane_id() == 0) t = atomicAdd(ctr, 1u);
+  return uni(__shfl(t, 0, 64));
+}
+
+__device__ __forceinline__ void raise_err(uint64_t* stats, uint32_t err) {
+  if (err && lane_id() == 0) atomicOr(reinterpret_cast<unsigned long long*>(stats + 3), (unsigned long long)err);
+}
+
+// ---------------------------------------------------------------- byte sources
+// An "image" is a block's bytes addressed block-relative; LdsImg reads the LDS staging copy,
+// GlbImg reads global memory through a bounds-checked buffer descriptor (OOB reads = 0).
+struct LdsImg {
+  const uint8_t* p;  // LDS address of block byte 0
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (uint32_t(p[i]) << 8) | p[i + 1]; }
+  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v = (v << 8) | p[i + j];
+    return v;
+  }
+};
+struct GlbImg {
+  rsrc_t r;
+  uint32_t lead;  // rsrc base = block start - lead
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, lead + i, 0, 0);
+  }
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
+  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v = (v << 8) | u8(i + j);
+    return v;
+  }
+};
+
+// 4 bytes starting at byte offset x of a 4-byte-aligned LDS buffer.
+__device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
+  const uint32_t i = x >> 2;
+  return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
+}
+
+// Store 16 bytes (dst 16-aligned) or, for a partially covered chunk, only bytes whose
+// mask bit is set.
+__device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t mask) {
+  if (mask == 0xFFFF) {
+    u32x4 q = {v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<u32x4*>(dst) = q;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (mask & (1u << j)) dst[j] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
+  }
+}
+
+// ================================================================ decode
+struct DecodeArgs {
+  const uint8_t* blocks;
+  const uint64_t* blk_off;
+  uint64_t nblk;
+  uint8_t* keys;
+  uint32_t* key_off;
+  uint8_t* vals;
+  uint32_t* val_off;
+  uint64_t* ts;
+  uint64_t entry_cap, key_cap, val_cap;
+  uint64_t* stats;
+  uint32_t* ticket;
+  uint64_t* agg;
+  uint64_t* inc;
+  uint32_t tag;
+};
+
+constexpr uint32_t kDecWaves = 4;
+constexpr uint32_t kDecImg = 4352;  // staged block bytes per wave (4 KiB blocks + lead + slack)
+constexpr uint32_t kDecMaxE = 128;  // entries with LDS tables (fast path)
+
+struct alignas(16) DecLds {
+  uint8_t img[kDecImg];
+  uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE], vsrc[kDecMaxE];
+  uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
+};
+
+struct BlockHdr {
+  uint32_t len, n, data_end, fks;
+  bool ok;
+};
+
+template <class Img>
+__device__ __forceinline__ BlockHdr parse_hdr(const Img& im, uint32_t len) {
+  BlockHdr h{len, 0, 0, 0, true};
+  if (len < 2) { h.ok = false; return h; }
+  h.n = im.u16(len - 2);
+  if (2 + 2 * h.n > len) { h.ok = false; h.n = 0; return h; }
+  h.data_end = len - 2 - 2 * h.n;
+  if (h.n) {
+    // get_first_key (iterator.rs:23-34) parses the entry at data position 0.
+    if (h.data_end < 4) { h.ok = false; return h; }
+    h.fks = im.u16(2);
+    if (4 + h.fks + 8 > h.data_end) h.ok = false;
+  }
+  return h;
+}
+
+// Corrected seek_to_offset (iterator.rs:125-139) with the validation rules of DESIGN.md.
+template <class Img>
+__device__ __forceinline__ bool parse_entry(const Img& im, const BlockHdr& h, uint32_t k,
+                                            uint32_t& off, uint32_t& p, uint32_t& s, uint32_t& vl) {
+  off = im.u16(h.data_end + 2 * k);
+  bool ok = off + 4 <= h.data_end;
+  p = im.u16(off);
+  s = im.u16(off + 2);
+  ok = ok && (off + 4 + s + 10 <= h.data_end) && (p <= h.fks) && (p + s > 0);
+  vl = im.u16(off + 12 + s);
+  ok = ok && (off + 14 + s + vl <= h.data_end);
+  if (!ok) { p = s = vl = 0; }
+  return ok;
+}
+
+// Simple path: per-entry lanes, any block size / entry count, byte-granular stores.
+template <class Img>
+__device__ void dec_simple_outputs(const DecodeArgs& a, const Img& im, const BlockHdr& h,
+                                   uint64_t E0, uint64_t K0, uint64_t V0) {
+  const uint32_t l = lane_id();
+  uint64_t kc = 0, vc = 0;
+  for (uint32_t c = 0; c < h.n; c += 64) {
+    const uint32_t k = c + l;
+    uint32_t off = 0, p = 0, s = 0, vl = 0;
+    if (k < h.n) parse_entry(im, h, k, off, p, s, vl);
+    const uint64_t kl = p + s;
+    const uint64_t ki = wave_incl_scan<uint64_t>(kl), vi = wave_incl_scan<uint64_t>(vl);
+    const uint64_t kpos = K0 + kc + ki - kl, vpos = V0 + vc + vi - vl;
+    kc += __shfl(ki, 63, 64);
+    vc += __shfl(vi, 63, 64);
+    if (k < h.n) {
+      const uint64_t e = E0 + k;
+      if (e < a.entry_cap) {
+        a.ts[e] = im.u64(off + 4 + s);
+        a.key_off[e] = uint32_t(kpos);
+        a.val_off[e] = uint32_t(vpos);
+      }
+      for (uint32_t t = 0; t < p; ++t)
+        if (kpos + t < a.key_cap) a.keys[kpos + t] = uint8_t(im.u8(4 + t));
+      for (uint32_t t = 0; t < s; ++t)
+        if (kpos + p + t < a.key_cap) a.keys[kpos + p + t] = uint8_t(im.u8(off + 4 + t));
+      for (uint32_t t = 0; t < vl; ++t)
+        if (vpos + t < a.val_cap) a.vals[vpos + t] = uint8_t(im.u8(off + 14 + s + t));
+    }
+  }
+}
+
+// Fast path: LDS image + LDS tables, coalesced aligned stores.
+__device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
+                                 uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V) {
+  const uint32_t l = lane_id();
+  const uint8_t* img = L.img;
+  const LdsImg im{L.img + lead};
+  // per-entry metadata
+  for (uint32_t k = l; k < h.n; k += 64) {
+    const uint64_t e = E0 + k;
+    if (e < a.entry_cap) {
+      a.ts[e] = im.u64(uint32_t(L.epos[k]) + 4 + L.sfx[k]);
+      a.key_off[e] = uint32_t(K0 + L.kout[k]);
+      a.val_off[e] = uint32_t(V0 + L.vout[k]);
+    }
+  }
+  // keys: dwords of the arena covering [K0, K0+K), bytes resolved per byte.
+  {
+    const uint64_t w_begin = K0 >> 2, w_end = (K0 + K + 3) >> 2;
+    for (uint64_t w = w_begin + l; w < w_end; w += 64) {
+      const int64_t r0 = int64_t(w * 4) - int64_t(K0);
+      uint32_t word = 0, mask = 0;
+      // cursor: entry containing max(r0, 0)
+      uint32_t rr = r0 < 0 ? 0u : uint32_t(r0);
+      uint32_t lo = 0, hi = h.n;  // largest k with kout[k] <= rr
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.kout[mid] <= rr) lo = mid; else hi = mid;
+      }
+      uint32_t k = lo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t r = r0 + j;
+        if (r < 0 || r >= int64_t(K)) continue;
+        const uint32_t ru = uint32_t(r);
+        while (k + 1 < h.n && L.kout[k + 1] <= ru) ++k;
+        const uint32_t t = ru - L.kout[k];
+        const uint32_t src = t < L.pfx[k] ? 4 + t : uint32_t(L.epos[k]) + 4 + t - L.pfx[k];
+        word |= uint32_t(img[lead + src]) << (8 * j);
+        mask |= 1u << j;
+      }
+      const uint64_t gb = w * 4;
+      if (mask == 0xF && gb + 4 <= a.key_cap) {
+        *reinterpret_cast<uint32_t*>(a.keys + gb) = word;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if ((mask & (1u << j)) && gb + j < a.key_cap) a.keys[gb + j] = uint8_t(word >> (8 * j));
+      }
+    }
+  }
+  // values: 16-B chunks of the arena covering [V0, V0+V).
+  {
+    const uint64_t c_begin = V0 >> 4, c_end = (V0 + V + 15) >> 4;
+    for (uint64_t c = c_begin + l; c < c_end; c += 64) {
+      const int64_t rb = int64_t(c * 16) - int64_t(V0);
+      const uint32_t rr = rb < 0 ? 0u : uint32_t(rb);
+      uint32_t lo = 0, hi = h.n;  // largest k with vout[k] <= rr
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.vout[mid] <= rr) lo = mid; else hi = mid;
+      }
+      uint32_t k = lo;
+      uint32_t v[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int64_t r0 = rb + 4 * d;
+        const uint32_t r0c = r0 < 0 ? 0u : uint32_t(r0);
+        while (k + 1 < h.n && L.vout[k + 1] <= r0c) ++k;
+        const int64_t endk = L.vout[k + 1];
+        const uint32_t x1 = uint32_t(int64_t(lead) + L.vsrc[k] + (r0 - int64_t(L.vout[k])));
+        uint32_t w1 = lds_dword_at(img, x1);
+        if (r0 + 4 <= endk) {
+          v[d] = w1;
+        } else if (k + 2 <= h.n && r0 + 4 <= int64_t(L.vout[k + 2])) {
+          const uint32_t x2 = uint32_t(int64_t(lead) + L.vsrc[k + 1] + (r0 - int64_t(L.vout[k + 1])));
+          const uint32_t w2 = lds_dword_at(img, x2);
+          const uint32_t nb = uint32_t(endk - r0);  // 1..3 bytes from value k
+          const uint32_t m = (1u << (8 * nb)) - 1;
+          v[d] = (w1 & m) | (w2 & ~m);
+        } else {
+          uint32_t word = 0;
+          uint32_t kk = k;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t r = r0 + j;
+            if (r < 0 || r >= int64_t(V)) continue;
+            const uint32_t ru = uint32_t(r);
+            while (kk + 1 < h.n && L.vout[kk + 1] <= ru) ++kk;
+            word |= uint32_t(img[lead + L.vsrc[kk] + (ru - L.vout[kk])]) << (8 * j);
+          }
+          v[d] = word;
+        }
+      }
+      uint32_t mask = 0;
+      const uint64_t gb = c * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int64_t r = rb + j;
+        if (r >= 0 && r < int64_t(V) && gb + j < a.val_cap) mask |= 1u << j;
+      }
+      store_chunk(a.vals + gb, v, mask);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
+  __shared__ DecLds lds[kDecWaves];
+  DecLds& L = lds[threadIdx.x >> 6];
+  const uint32_t l = lane_id();
+  const uint64_t b = take_ticket(a.ticket);
+  if (b >= a.nblk) return;
+  uint32_t err = 0;
+  const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
+  uint32_t len = 0;
+  if (end < start || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
+  else len = uint32_t(end - start);
+  const uint8_t* bp = a.blocks + start;
+  const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
+  const uint8_t* abase = bp - lead;
+  const rsrc_t R = make_rsrc(abase, lead + len);
+  const bool fits = lead + len + 16 <= kDecImg;
+
+  BlockHdr h;
+  if (fits) {
+    const uint32_t nchunk = (lead + len + 15) >> 4;
+    for (uint32_t c = l; c < nchunk; c += 64)
+      *reinterpret_cast<u32x4*>(L.img + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(R, c * 16, 0, 0);
+    wave_sync();
+    h = parse_hdr(LdsImg{L.img + lead}, len);
+  } else {
+    h = parse_hdr(GlbImg{R, lead}, len);
+  }
+  if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
+  const bool fast = fits && h.n <= kDecMaxE;
+
+  // phase 1: parse entries, block aggregates (entries, key bytes, value bytes)
+  uint64_t K = 0, V = 0;
+  bool bad = false;
+  if (fast) {
+    const LdsImg im{L.img + lead};
+    for (uint32_t c = 0; c < h.n; c += 64) {
+      const uint32_t k = c + l;
+      uint32_t off = 0, p = 0, s = 0, vl = 0;
+      bool ok = true;
+      if (k < h.n) ok = parse_entry(im, h, k, off, p, s, vl);
+      bad = bad || !ok;
+      const uint32_t kl = p + s;
+      const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
+      if (k < h.n) {
+        L.epos[k] = uint16_t(off);
+        L.pfx[k] = uint16_t(p);
+        L.sfx[k] = uint16_t(s);
+        L.vsrc[k] = uint16_t(off + 14 + s);
+        L.kout[k] = uint32_t(K) + ki - kl;
+        L.vout[k] = uint32_t(V) + vi - vl;
+      }
+      K += __shfl(ki, 63, 64);
+      V += __shfl(vi, 63, 64);
+    }
+    if (l == 0) {
+      L.kout[h.n] = uint32_t(K);
+      L.vout[h.n] = uint32_t(V);
+    }
+  } else {
+    for (uint32_t c = 0; c < h.n; c += 64) {
+      const uint32_t k = c + l;
+      uint32_t off = 0, p = 0, s = 0, vl = 0;
+      bool ok = true;
+      if (k < h.n) {
+        if (fits) ok = parse_entry(LdsImg{L.img + lead}, h, k, off, p, s, vl);
+        else ok = parse_entry(GlbImg{R, lead}, h, k, off, p, s, vl);
+      }
+      bad = bad || !ok;
+      K += wave_sum<uint64_t>(p + s);
+      V += wave_sum<uint64_t>(vl);
+    }
+  }
+  if (__ballot(bad)) err |= LSMBLK_ERR_MALFORMED;
+  uint64_t agg[3] = {h.n, K, V};
+  if (err) agg[0] = agg[1] = agg[2] = 0;
+
+  // publish + look-back
+  uint64_t excl[3] = {0, 0, 0};
+  if (b == 0) {
+    publish<3>(a.inc, b, agg, a.tag, 2);
+  } else {
+    publish<3>(a.agg, b, agg, a.tag, 1);
+    if (!lookback<3>(a.agg, a.inc, b, a.tag, excl)) err |= LSMBLK_ERR_TIMEOUT;
+    const uint64_t inc[3] = {excl[0] + agg[0], excl[1] + agg[1], excl[2] + agg[2]};
+    publish<3>(a.inc, b, inc, a.tag, 2);
+  }
+  wave_sync();
+  const uint64_t E0 = excl[0], K0 = excl[1], V0 = excl[2];
+  const uint64_t Et = E0 + agg[0], Kt = K0 + agg[1], Vt = V0 + agg[2];
+  if (Kt > 0xFFFFFFFFull || Vt > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+  if (Et > a.entry_cap || Kt > a.key_cap || Vt > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
+
+  if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW)) && h.n) {
+    if (fast) {
+      dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V));
+    } else if (fits) {
+      dec_simple_outputs(a, LdsImg{L.img + lead}, h, E0, K0, V0);
+    } else {
+      dec_simple_outputs(a, GlbImg{R, lead}, h, E0, K0, V0);
+    }
+  }
+  if (b == a.nblk - 1 && l == 0) {
+    a.stats[0] = Et;
+    a.stats[1] = Kt;
+    a.stats[2] = Vt;
+    if (Et <= a.entry_cap) {
+      a.key_off[Et] = uint32_t(Kt);
+      a.val_off[Et] = uint32_t(Vt);
+    }
+  }
+  raise_err(a.stats, err);
+}
+
+// ================================================================ encode: plan
+struct PlanArgs {
+  const uint8_t* keys;
+  const uint32_t* key_off;
+  const uint32_t* val_off;
+  uint64_t n;
+  const uint32_t* seg_start;
+  uint32_t nseg;
+  uint32_t block_size;
+  uint32_t* rec_first;  // scratch, n+1
+  uint32_t* rec_size;   // scratch, n+1
+  uint32_t* blk_first;  // dense, n+1
+  uint64_t* blk_off;    // user, blk_cap
+  uint64_t blk_cap, out_cap;
+  uint64_t* stats;
+  uint32_t* ticket;
+  uint64_t* agg;
+  uint64_t* inc;
+  uint32_t tag;
+};
+
+constexpr uint32_t kPlanWaves = 4;
+constexpr uint32_t kPlanW = 512;    // entries per LDS chunk
+constexpr uint32_t kPlanKB = 8192;  // key bytes per LDS chunk
+
+struct alignas(16) PlanLds {
+  uint8_t keys[kPlanKB + 32];
+  uint32_t koff[kPlanW + 1];
+  uint32_t voff[kPlanW + 1];
+};
+
+// Key bytes of the batch, served from the LDS chunk when it holds them.
+struct PlanKeys {
+  rsrc_t gk;          // whole key arena, base aligned down to 4
+  uint32_t glead;     // keys pointer & 3
+  const uint8_t* lk;  // LDS chunk (16-aligned)
+  uint32_t lbase;     // arena offset of lk[llead]
+  uint32_t llead;
+  uint32_t lend;      // arena offset one past the chunk's last byte; 0-length if keys not staged
+  __device__ __forceinline__ uint32_t dword(uint32_t pos) const {  // 4 bytes at arena pos
+    if (pos >= lbase && pos + 4 <= lend) return lds_dword_at(lk, llead + (pos - lbase));
+    const uint32_t x = glead + pos, al = x & ~3u;
+    const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(gk, al, 0, 0);
+    const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(gk, al + 4, 0, 0);
+    return __builtin_amdgcn_alignbyte(w1, w0, x & 3);
+  }
+};
+
+// LCP of the key at arena position kp (length kl) against the first key (fp, fl), whose
+// first 32 bytes are held in wave-uniform registers fkw[].
+__device__ __forceinline__ uint32_t lcp_first(const PlanKeys& K, const uint32_t (&fkw)[8], uint32_t fp,
+                                              uint32_t fl, uint32_t kp, uint32_t kl) {
+  const uint32_t m = fl < kl ? fl : kl;
+  uint32_t p = m;
+  bool done = false;
+#pragma unroll
+  for (uint32_t c = 0; c < 8; ++c) {
+    if (!done && 4 * c < m) {
+      const uint32_t x = fkw[c] ^ K.dword(kp + 4 * c);
+      if (x) {
+        const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
+        p = q < m ? q : m;
+        done = true;
+      }
+    } else {
+      done = true;
+    }
+  }
+  if (!done) {
+    for (uint32_t c = 8; 4 * c < m; ++c) {
+      const uint32_t x = K.dword(fp + 4 * c) ^ K.dword(kp + 4 * c);
+      if (x) {
+        const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
+        p = q < m ? q : m;
+        break;
+      }
+    }
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
+  __shared__ PlanLds lds[kPlanWaves];
+  PlanLds& L = lds[threadIdx.x >> 6];
+  const uint32_t l = lane_id();
+  const uint32_t g = take_ticket(a.ticket);
+  if (g >= a.nseg) return;
+  uint32_t err = 0;
+  uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
+  if ((g == 0 && s0 != 0) || (g == a.nseg - 1 && uint64_t(s1) != a.n) || s0 > s1 || uint64_t(s1) > a.n) {
+    err |= LSMBLK_ERR_SEGMENTS;
+    s1 = s0 = (s0 > a.n ? uint32_t(a.n) : s0);
+    if (s1 < s0) s1 = s0;
+  }
+  const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys);
+  PlanKeys K;
+  K.glead = uint32_t(kaddr & 3);
+  const uint32_t ktotal = uni(a.key_off[a.n]);
+  K.gk = make_rsrc(a.keys - K.glead, K.glead + ktotal);
+  K.lk = L.keys;
+  K.lbase = K.lend = 0;
+  K.llead = 0;
+  uint32_t c0 = 0, c1 = 0;  // chunk covers entries [c0, c1) with offsets [c0, c1]
+
+  auto load_chunk = [&](uint32_t from) {
+    c0 = from;
+    c1 = (s1 - from) < kPlanW ? s1 : from + kPlanW;
+    for (uint32_t i = l; i <= c1 - c0; i += 64) {
+      L.koff[i] = a.key_off[c0 + i];
+      L.voff[i] = a.val_off[c0 + i];
+    }
+    wave_sync();
+    const uint32_t kb0 = uni(L.koff[0]), kb1 = uni(L.koff[c1 - c0]);
+    const uint32_t al = (K.glead + kb0) & ~15u, llead = (K.glead + kb0) & 15u;
+    if (llead + (kb1 - kb0) + 8 <= kPlanKB + 32 - 8) {
+      const rsrc_t R = K.gk;
+      const uint32_t nchunk = (llead + (kb1 - kb0) + 15) >> 4;
+      for (uint32_t c = l; c < nchunk; c += 64)
+        *reinterpret_cast<u32x4*>(L.keys + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(R, al + c * 16, 0, 0);
+      K.lbase = kb0;
+      K.llead = llead;
+      K.lend = kb1;
+    } else {
+      K.lbase = K.lend = 0;  // keys from global
+    }
+    wave_sync();
+  };
+
+  uint32_t nb = 0;
+  uint64_t bytes = 0;
+  uint32_t s = s0;
+  const uint64_t bs = a.block_size;
+  while (s < s1) {
+    if (!(s >= c0 && s < c1)) load_chunk(s);
+    // first key of the block (ts is irrelevant to the size rule)
+    const uint32_t fp = uni(L.koff[s - c0]), fl = uni(L.koff[s - c0 + 1]) - fp;
+    uint32_t fkw[8];
+#pragma unroll
+    for (uint32_t c = 0; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
+    uint64_t carry = 2;  // estimated_size() of an empty builder
+    uint32_t j0 = s;
+    for (;;) {
+      const uint32_t wend = (s1 - j0) < 64 ? s1 : j0 + 64;
+      if (!(j0 >= c0 && wend <= c1)) {
+        load_chunk(j0);
+      }
+      const uint32_t e = j0 + l;
+      const bool valid = e < s1;
+      uint64_t gr = 0;
+      uint32_t klen = 0, vlen = 0;
+      if (valid) {
+        const uint32_t kp = L.koff[e - c0];
+        klen = L.koff[e - c0 + 1] - kp;
+        vlen = L.voff[e - c0 + 1] - L.voff[e - c0];
+        const uint32_t p = e == s ? 0u : lcp_first(K, fkw, fp, fl, kp, klen);
+        gr = uint64_t(klen) + vlen + 16 - p;  // data growth + 2-byte offset slot
+        if (klen == 0) err |= LSMBLK_ERR_EMPTY_KEY;
+      }
+      const uint64_t incl = wave_incl_scan<uint64_t>(gr);
+      const uint64_t before = carry + incl - gr;  // estimated_size() before adding e
+      // builder.rs:56-60: reject when est + raw_len + vlen + 6 > block_size (not first entry)
+      const bool stop = !valid || (e != s && before + klen + 8 + vlen + 6 > bs);
+      const uint64_t m = __ballot(stop);
+      if (m) {
+        const uint32_t f = uint32_t(__builtin_ctzll(m));
+        const uint64_t size = __shfl(before, f, 64);
+        if (l == 0) {
+          a.rec_first[s0 + nb] = s;
+          a.rec_size[s0 + nb] = uint32_t(size);
+        }
+        ++nb;
+        bytes += size;
+        s = j0 + f;
+        break;
+      }
+      carry += __shfl(incl, 63, 64);
+      j0 += 64;
+    }
+  }
+
+  // segment totals -> dense block numbering and output offsets
+  uint64_t agg[2] = {nb, bytes};
+  uint64_t excl[2] = {0, 0};
+  if (g == 0) {
+    publish<2>(a.inc, g, agg, a.tag, 2);
+  } else {
+    publish<2>(a.agg, g, agg, a.tag, 1);
+    if (!lookback<2>(a.agg, a.inc, g, a.tag, excl)) err |= LSMBLK_ERR_TIMEOUT;
+    const uint64_t inc[2] = {excl[0] + agg[0], excl[1] + agg[1]};
+    publish<2>(a.inc, g, inc, a.tag, 2);
+  }
+  // make this wave's record stores visible to its own later loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const uint64_t B0 = excl[0], O0 = excl[1];
+  uint64_t oc = O0;
+  for (uint32_t c = 0; c < nb; c += 64) {
+    const uint32_t i = c + l;
+    uint32_t sz = 0, first = 0;
+    if (i < nb) {
+      sz = a.rec_size[s0 + i];
+      first = a.rec_first[s0 + i];
+    }
+    const uint64_t incl = wave_incl_scan<uint64_t>(sz);
+    if (i < nb) {
+      const uint64_t bi = B0 + i;
+      a.blk_first[bi] = first;
+      if (bi < a.blk_cap) a.blk_off[bi] = oc + incl - sz;
+    }
+    oc += __shfl(incl, 63, 64);
+  }
+  if (g == a.nseg - 1 && l == 0) {
+    const uint64_t Bt = B0 + nb, Ot = O0 + bytes;
+    a.blk_first[Bt] = uint32_t(a.n);
+    if (Bt < a.blk_cap) a.blk_off[Bt] = Ot;
+    a.stats[0] = Bt;
+    a.stats[1] = Ot;
+    if (Bt + 1 > a.blk_cap || Ot > a.out_cap) err |= LSMBLK_ERR_CAPACITY;
+  }
+  raise_err(a.stats, err);
+}
+
+// ================================================================ encode: emit
+struct EmitArgs {
+  const uint8_t* keys;
+  const uint32_t* key_off;
+  const uint8_t* vals;
+  const uint32_t* val_off;
+  const uint64_t* ts;
+  const uint32_t* blk_first;
+  const uint64_t* blk_off;
+  uint8_t* out;
+  uint64_t out_cap, blk_cap;
+  uint64_t n;  // entries; arena sizes are key_off[n], val_off[n]
+  uint64_t* stats;
+};
+
+constexpr uint32_t kEmitWaves = 4;
+constexpr uint32_t kEmitKCap = 1088;
+constexpr uint32_t kEmitVCap = 4160;
+constexpr uint32_t kEmitOCap = 4160;
+constexpr uint32_t kEmitMaxE = 128;
+
+struct alignas(16) EmitLds {
+  uint8_t kimg[kEmitKCap];
+  uint8_t vimg[kEmitVCap];
+  uint8_t oimg[kEmitOCap];
+  uint32_t epos[kEmitMaxE];
+  uint32_t vdst[kEmitMaxE + 1];
+  uint32_t vend[kEmitMaxE];
+  uint32_t vsrc[kEmitMaxE];
+};
+
+__device__ __forceinline__ void lds_be(uint8_t* p, uint64_t v, int nbytes) {
+  for (int i = 0; i < nbytes; ++i) p[i] = uint8_t(v >> (8 * (nbytes - 1 - i)));
+}
+
+// Global byte readers for the simple path.
+struct GlbBytes {
+  rsrc_t r;
+  uint32_t lead;
+  __device__ __forceinline__ uint32_t u8(uint32_t pos) const {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, lead + pos, 0, 0);
+  }
+};
+
+__device__ void emit_simple(const EmitArgs& a, const GlbBytes& KB, const GlbBytes& VB, uint32_t s,
+                            uint32_t n, uint64_t O, uint64_t size, uint32_t& err) {
+  const uint32_t l = lane_id();
+  const uint32_t fp = uni(a.key_off[s]), fl = uni(a.key_off[s + 1]) - fp;
+  uint64_t dc = 0;
+  auto put = [&](uint64_t pos, uint32_t byte) {
+    if (O + pos < a.out_cap) a.out[O + pos] = uint8_t(byte);
+  };
+  for (uint32_t c = 0; c < n; c += 64) {
+    const uint32_t k = c + l;
+    uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
+    if (k < n) {
+      kp = a.key_off[s + k];
+      kl = a.key_off[s + k + 1] - kp;
+      vp = a.val_off[s + k];
+      vl = a.val_off[s + k + 1] - vp;
+      if (k != 0) {
+        const uint32_t m = fl < kl ? fl : kl;
+        while (p < m && KB.u8(fp + p) == KB.u8(kp + p)) ++p;
+      }
+    }
+    const uint64_t dg = k < n ? uint64_t(kl) + vl + 14 - p : 0;
+    const uint64_t incl = wave_incl_scan<uint64_t>(dg);
+    const uint64_t pos = dc + incl - dg;
+    dc += __shfl(incl, 63, 64);
+    if (k < n) {
+      const uint32_t sfx = kl - p;
+      put(pos + 0, (p >> 8) & 0xFF);
+      put(pos + 1, p & 0xFF);
+      put(pos + 2, (sfx >> 8) & 0xFF);
+      put(pos + 3, sfx & 0xFF);
+      for (uint32_t t = 0; t < sfx; ++t) put(pos + 4 + t, KB.u8(kp + p + t));
+      const uint64_t tsv = a.ts[s + k];
+      for (int t = 0; t < 8; ++t) put(pos + 4 + sfx + t, uint32_t(tsv >> (56 - 8 * t)) & 0xFF);
+      put(pos + 12 + sfx, (vl >> 8) & 0xFF);
+      put(pos + 13 + sfx, vl & 0xFF);
+      for (uint32_t t = 0; t < vl; ++t) put(pos + 14 + sfx + t, VB.u8(vp + t));
+      // offset slot (data.len() as u16) is written below once data_len is known
+    }
+  }
+  const uint64_t data_len = dc;
+  if (data_len + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
+  uint64_t dc2 = 0;
+  for (uint32_t c = 0; c < n; c += 64) {
+    const uint32_t k = c + l;
+    uint32_t kl = 0, vl = 0, p = 0;
+    if (k < n) {
+      const uint32_t kp = a.key_off[s + k];
+      kl = a.key_off[s + k + 1] - kp;
+      vl = a.val_off[s + k + 1] - a.val_off[s + k];
+      if (k != 0) {
+        const uint32_t m = fl < kl ? fl : kl;
+        while (p < m && KB.u8(fp + p) == KB.u8(kp + p)) ++p;
+      }
+    }
+    const uint64_t dg = k < n ? uint64_t(kl) + vl + 14 - p : 0;
+    const uint64_t incl = wave_incl_scan<uint64_t>(dg);
+    const uint64_t pos = dc2 + incl - dg;
+    dc2 += __shfl(incl, 63, 64);
+    if (k < n) {
+      put(data_len + 2 * k, uint32_t(pos >> 8) & 0xFF);
+      put(data_len + 2 * k + 1, uint32_t(pos) & 0xFF);
+    }
+  }
+  if (l == 0) {
+    put(size - 2, (n >> 8) & 0xFF);
+    put(size - 1, n & 0xFF);
+  }
+}
+
+__global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
+  __shared__ EmitLds lds[kEmitWaves];
+  EmitLds& L = lds[threadIdx.x >> 6];
+  const uint32_t l = lane_id();
+  const uint64_t nblk = uni64(a.stats[0]);
+  const uint64_t nwaves = uint64_t(gridDim.x) * kEmitWaves;
+  uint32_t err = 0;
+  const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
+  for (uint64_t bi = uint64_t(blockIdx.x) * kEmitWaves + (threadIdx.x >> 6); bi < nblk; bi += nwaves) {
+    const uint64_t biu = uni64(bi);
+    if (biu + 1 >= a.blk_cap) break;  // blk_off not materialized (capacity error raised by plan)
+    const uint32_t s = uni(a.blk_first[biu]), e = uni(a.blk_first[biu + 1]);
+    const uint32_t n = e - s;
+    const uint64_t O = uni64(a.blk_off[biu]);
+    const uint64_t size = uni64(a.blk_off[biu + 1]) - O;
+    const uint32_t kb0 = uni(a.key_off[s]), kb1 = uni(a.key_off[e]);
+    const uint32_t vb0 = uni(a.val_off[s]), vb1 = uni(a.val_off[e]);
+    const uint32_t klead = uint32_t((kaddr + kb0) & 15), vlead = uint32_t((vaddr + vb0) & 15);
+    const uint32_t olead = uint32_t(O & 15);
+    const bool fast = n <= kEmitMaxE && klead + (kb1 - kb0) + 8 <= kEmitKCap &&
+                      vlead + (vb1 - vb0) + 8 <= kEmitVCap && olead + size + 8 <= kEmitOCap;
+    if (!fast) {
+      const uint32_t kg = uint32_t(kaddr & 3), vg = uint32_t(vaddr & 3);
+      const uint32_t kt = uni(a.key_off[a.n]), vt = uni(a.val_off[a.n]);
+      const GlbBytes KB{make_rsrc(a.keys - kg, kg + kt), kg};
+      const GlbBytes VB{make_rsrc(a.vals - vg, vg + vt), vg};
+      emit_simple(a, KB, VB, s, n, O, size, err);
+      continue;
+    }
+    // stage keys and values of the block
+    {
+      const rsrc_t RK = make_rsrc(a.keys + kb0 - klead, klead + (kb1 - kb0));
+      const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
+      for (uint32_t c = l; c < nk; c += 64)
+        *reinterpret_cast<u32x4*>(L.kimg + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(RK, c * 16, 0, 0);
+      const rsrc_t RV = make_rsrc(a.vals + vb0 - vlead, vlead + (vb1 - vb0));
+      const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
+      for (uint32_t c = l; c < nv; c += 64)
+        *reinterpret_cast<u32x4*>(L.vimg + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(RV, c * 16, 0, 0);
+    }
+    wave_sync();
+    // entry lanes: prefix, positions, non-value bytes and value edge bytes into oimg
+    const uint32_t fl = uni(a.key_off[s + 1]) - kb0;  // first key is at kimg[klead]
+    uint32_t dc = 0;
+    for (uint32_t c = 0; c < n; c += 64) {
+      const uint32_t k = c + l;
+      uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
+      uint64_t tsv = 0;
+      if (k < n) {
+        kp = a.key_off[s + k] - kb0;
+        kl = a.key_off[s + k + 1] - kb0 - kp;
+        vp = a.val_off[s + k] - vb0;
+        vl = a.val_off[s + k + 1] - vb0 - vp;
+        tsv = a.ts[s + k];
+        if (k != 0) {
+          const uint32_t m = fl < kl ? fl : kl;
+          p = m;
+          for (uint32_t q = 0; q < m; q += 4) {
+            const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
+            if (x) {
+              const uint32_t z = q + (__builtin_ctz(x) >> 3);
+              p = z < m ? z : m;
+              break;
+            }
+          }
+        }
+      }
+      const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
+      const uint32_t incl = wave_incl_scan<uint32_t>(dg);
+      const uint32_t pos = dc + incl - dg;
+      dc += __shfl(incl, 63, 64);
+      if (k < n) {
+        const uint32_t sfx = kl - p;
+        uint8_t* o = L.oimg + olead + pos;
+        lds_be(o, p & 0xFFFF, 2);
+        lds_be(o + 2, sfx & 0xFFFF, 2);
+        const uint8_t* ks = L.kimg + klead + kp + p;
+        for (uint32_t t = 0; t < sfx; ++t) o[4 + t] = ks[t];
+        lds_be(o + 4 + sfx, tsv, 8);
+        lds_be(o + 12 + sfx, vl & 0xFFFF, 2);
+        const uint32_t A = olead + pos + 14 + sfx, Bv = A + vl;
+        const uint32_t a4 = (A + 3) & ~3u, b4 = Bv & ~3u;
+        const uint8_t* vs = L.vimg + vlead + vp;
+        if (a4 >= b4) {
+          for (uint32_t t = 0; t < vl; ++t) L.oimg[A + t] = vs[t];
+        } else {
+          for (uint32_t x = A; x < a4; ++x) L.oimg[x] = vs[x - A];
+          for (uint32_t x = b4; x < Bv; ++x) L.oimg[x] = vs[x - A];
+        }
+        L.epos[k] = pos;
+        L.vdst[k] = pos + 14 + sfx;
+        L.vend[k] = pos + 14 + sfx + vl;
+        L.vsrc[k] = vlead + vp;
+      }
+    }
+    const uint32_t data_len = dc;
+    if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
+    wave_sync();
+    // offsets table + entry count (u16 BE, `as u16`)
+    for (uint32_t k = l; k < n; k += 64) lds_be(L.oimg + olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
+    if (l == 0) lds_be(L.oimg + olead + data_len + 2 * n, n & 0xFFFF, 2);
+    // value bulk: whole image dwords that lie inside one value
+    {
+      const uint32_t nw = (olead + uint32_t(size) + 3) >> 2;
+      uint32_t k = 0;
+      bool first_iter = true;
+      for (uint32_t W = l; W < nw; W += 64) {
+        const int32_t x = int32_t(4 * W) - int32_t(olead);
+        if (first_iter) {
+          uint32_t lo = 0, hi = n;
+          const int32_t xc = x < 0 ? 0 : x;
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (int32_t(L.vdst[mid]) <= xc) lo = mid; else hi = mid;
+          }
+          k = lo;
+          first_iter = false;
+        }
+        while (k + 1 < n && int32_t(L.vdst[k + 1]) <= x) ++k;
+        if (x >= int32_t(L.vdst[k]) && x + 4 <= int32_t(L.vend[k])) {
+          const uint32_t src = L.vsrc[k] + uint32_t(x - int32_t(L.vdst[k]));
+          reinterpret_cast<uint32_t*>(L.oimg)[W] = lds_dword_at(L.vimg, src);
+        }
+      }
+    }
+    wave_sync();
+    // flush the image: 16-B chunks, partial chunks at the ends byte-wise
+    {
+      uint8_t* gbase = a.out + (O - olead);
+      const uint32_t nc = (olead + uint32_t(size) + 15) >> 4;
+      for (uint32_t c = l; c < nc; c += 64) {
+        const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + c * 16);
+        const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+        uint32_t mask = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t x = c * 16 + j;
+          if (x >= olead && x < olead + size && (O - olead) + x < a.out_cap) mask |= 1u << j;
+        }
+        store_chunk(gbase + c * 16, v, mask);
+      }
+    }
+    wave_sync();
+  }
+  raise_err(a.stats, err);
+}
+
+__global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64_t cap) {
+  if (threadIdx.x == 0 && cap + 1 > 0) {
+    key_off[0] = 0;
+    val_off[0] = 0;
+  }
+}
+
+}  // namespace
+
+// ================================================================ host side
+struct lsmblk_ctx {
+  int device = 0;
+  std::mutex mu;
+  uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket
+  uint64_t* dec_agg = nullptr;   // 3 granules per block
+  uint64_t* dec_inc = nullptr;
+  uint64_t dec_cap = 0;
+  uint64_t* seg_agg = nullptr;   // 2 granules per segment
+  uint64_t* seg_inc = nullptr;
+  uint64_t seg_cap = 0;
+  uint32_t* rec_first = nullptr; // n+1
+  uint32_t* rec_size = nullptr;
+  uint32_t* blk_first = nullptr;
+  uint64_t rec_cap = 0;
+  uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
+};
+
+namespace {
+
+template <typename T>
+int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per) {
+  if (need <= *cap) return LSMBLK_OK;
+  uint64_t nc = need + need / 4 + 1024;
+  if (*p) {
+    if (hipDeviceSynchronize() != hipSuccess) return LSMBLK_E_HIP;
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (hipMalloc(reinterpret_cast<void**>(p), nc * per * sizeof(T)) != hipSuccess) {
+    *cap = 0;
+    return LSMBLK_E_NOMEM;
+  }
+  if (hipMemset(*p, 0, nc * per * sizeof(T)) != hipSuccess) return LSMBLK_E_HIP;
+  *cap = nc;
+  return LSMBLK_OK;
+}
+
+int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t segs) {
+  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  int rc;
+  uint64_t cap;
+  if (blocks > c->dec_cap) {
+    cap = c->dec_cap;
+    if ((rc = grow(&c->dec_agg, &cap, blocks, 3))) return rc;
+    cap = c->dec_cap;
+    if ((rc = grow(&c->dec_inc, &cap, blocks, 3))) return rc;
+    c->dec_cap = cap;
+    c->epoch = 0;
+  }
+  if (segs > c->seg_cap) {
+    cap = c->seg_cap;
+    if ((rc = grow(&c->seg_agg, &cap, segs, 2))) return rc;
+    cap = c->seg_cap;
+    if ((rc = grow(&c->seg_inc, &cap, segs, 2))) return rc;
+    c->seg_cap = cap;
+    c->epoch = 0;
+  }
+  if (entries + 1 > c->rec_cap) {
+    cap = c->rec_cap;
+    if ((rc = grow(&c->rec_first, &cap, entries + 1, 1))) return rc;
+    cap = c->rec_cap;
+    if ((rc = grow(&c->rec_size, &cap, entries + 1, 1))) return rc;
+    cap = c->rec_cap;
+    if ((rc = grow(&c->blk_first, &cap, entries + 1, 1))) return rc;
+    c->rec_cap = cap;
+  }
+  return LSMBLK_OK;
+}
+
+// Next look-back epoch; on wrap the status arrays are cleared on the stream.
+int next_epoch(lsmblk_ctx* c, hipStream_t st) {
+  if (c->epoch == 0 || c->epoch >= 16383) {
+    if (c->dec_cap) {
+      if (hipMemsetAsync(c->dec_agg, 0, c->dec_cap * 3 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+      if (hipMemsetAsync(c->dec_inc, 0, c->dec_cap * 3 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    }
+    if (c->seg_cap) {
+      if (hipMemsetAsync(c->seg_agg, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+      if (hipMemsetAsync(c->seg_inc, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    }
+    c->epoch = 0;
+  }
+  ++c->epoch;
+  return LSMBLK_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
+  if (!out) return LSMBLK_E_INVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LSMBLK_E_HIP;
+  auto* c = new (std::nothrow) lsmblk_ctx();
+  if (!c) return LSMBLK_E_NOMEM;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->counters, 64) != hipSuccess) {
+    delete c;
+    return LSMBLK_E_HIP;
+  }
+  *out = c;
+  return LSMBLK_OK;
+}
+
+void lsmblk_ctx_destroy(lsmblk_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(c->counters);
+  (void)hipFree(c->dec_agg);
+  (void)hipFree(c->dec_inc);
+  (void)hipFree(c->seg_agg);
+  (void)hipFree(c->seg_inc);
+  (void)hipFree(c->rec_first);
+  (void)hipFree(c->rec_size);
+  (void)hipFree(c->blk_first);
+  delete c;
+}
+
+int lsmblk_ctx_reserve(lsmblk_ctx* c, uint64_t max_blocks, uint64_t max_entries, uint64_t max_segments) {
+  if (!c) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return reserve_locked(c, max_blocks, max_entries, max_segments);
+}
+
+int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
+                        const lsmblk_kv_stream* out, uint64_t* stats, void* stream) {
+  if (!c || !blk_off || !out || !stats) return LSMBLK_E_INVAL;
+  if (!aligned16(out->keys) || !aligned16(out->vals) || !out->key_off || !out->val_off) return LSMBLK_E_INVAL;
+  if (nblk >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int rc = reserve_locked(c, nblk, 0, 0);
+  if (rc) return rc;
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (nblk == 0) {
+    hipLaunchKernelGGL(finish_empty_decode, dim3(1), dim3(64), 0, st, out->key_off, out->val_off, out->entry_cap);
+    return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  }
+  if ((rc = next_epoch(c, st))) return rc;
+  if (hipMemsetAsync(c->counters, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
+  DecodeArgs a;
+  a.blocks = blocks;
+  a.blk_off = blk_off;
+  a.nblk = nblk;
+  a.keys = out->keys;
+  a.key_off = out->key_off;
+  a.vals = out->vals;
+  a.val_off = out->val_off;
+  a.ts = out->ts;
+  a.entry_cap = out->entry_cap;
+  a.key_cap = out->key_cap;
+  a.val_cap = out->val_cap;
+  a.stats = stats;
+  a.ticket = c->counters;
+  a.agg = c->dec_agg;
+  a.inc = c->dec_inc;
+  a.tag = c->epoch;
+  const uint64_t grid = (nblk + kDecWaves - 1) / kDecWaves;
+  hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(grid)), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* seg_start, uint32_t nseg,
+                        uint32_t block_size, uint8_t* out, uint64_t out_cap, uint64_t* blk_off, uint64_t blk_cap,
+                        uint64_t* stats, void* stream) {
+  if (!c || !in || !seg_start || !blk_off || !stats || !aligned16(out)) return LSMBLK_E_INVAL;
+  if (in->n >= 0xFFFFFFFFull || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
+  if (block_size == 0) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int rc = reserve_locked(c, 0, in->n, nseg);
+  if (rc) return rc;
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (nseg == 0) {
+    // no segments: zero blocks; blk_off[0] = 0
+    if (in->n != 0) return LSMBLK_E_INVAL;
+    if (blk_cap >= 1 && hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    return LSMBLK_OK;
+  }
+  if ((rc = next_epoch(c, st))) return rc;
+  if (hipMemsetAsync(c->counters, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
+  PlanArgs p;
+  p.keys = in->keys;
+  p.key_off = in->key_off;
+  p.val_off = in->val_off;
+  p.n = in->n;
+  p.seg_start = seg_start;
+  p.nseg = nseg;
+  p.block_size = block_size;
+  p.rec_first = c->rec_first;
+  p.rec_size = c->rec_size;
+  p.blk_first = c->blk_first;
+  p.blk_off = blk_off;
+  p.blk_cap = blk_cap;
+  p.out_cap = out_cap;
+  p.stats = stats;
+  p.ticket = c->counters + 1;
+  p.agg = c->seg_agg;
+  p.inc = c->seg_inc;
+  p.tag = c->epoch;
+  hipLaunchKernelGGL(plan_kernel, dim3((nseg + kPlanWaves - 1) / kPlanWaves), dim3(256), 0, st, p);
+  if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
+  EmitArgs e;
+  e.keys = in->keys;
+  e.key_off = in->key_off;
+  e.vals = in->vals;
+  e.val_off = in->val_off;
+  e.ts = in->ts;
+  e.blk_first = c->blk_first;
+  e.blk_off = blk_off;
+  e.out = out;
+  e.out_cap = out_cap;
+  e.blk_cap = blk_cap;
+  e.n = in->n;
+  e.stats = stats;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const uint32_t grid = uint32_t(cus) * 3;
+  hipLaunchKernelGGL(emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+}  // extern "C"

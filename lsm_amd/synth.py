@@ -1,0 +1,94 @@
+"""Synthetic KV streams for the bench / tests (BASELINE.json configs).
+
+All keys are sorted and unique (as a memtable flush or compaction feeds SsTableBuilder),
+ts are 40-bit random, values random bytes, seeds fixed.
+
+  U  uniform     16-B keys, 100-B values                       (block_size 4096)
+  Z  zipf        16-B key = one of 1024 random 12-B prefixes (Zipf s=1.1) || 4-B BE counter
+  M  mixed       16-B keys, values log-uniform in [8, 4096]    (block_size 65536)
+"""
+import numpy as np
+
+
+def _offsets(lengths):
+    off = np.zeros(len(lengths) + 1, np.uint64)
+    np.cumsum(lengths, out=off[1:])
+    if off[-1] >= 2 ** 32:
+        raise ValueError("arena exceeds the u32 offsets of one batch")
+    return off.astype(np.uint32)
+
+
+def _random_bytes(rng, n):
+    return np.frombuffer(rng.bytes(int(n)), np.uint8).copy() if n else np.zeros(0, np.uint8)
+
+
+def _sorted_keys16(rng, n):
+    """n sorted unique 16-B keys spread uniformly over the 128-bit space."""
+    step = np.uint64((2 ** 64 - 1) // max(n, 1))
+    hi = np.arange(n, dtype=np.uint64) * step + rng.integers(0, int(step), n, dtype=np.uint64)
+    lo = rng.integers(0, 2 ** 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    k = np.empty((n, 16), np.uint8)
+    k[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
+    k[:, 8:] = lo.astype(">u8").view(np.uint8).reshape(n, 8)
+    return k.reshape(-1)
+
+
+def _ts(rng, n):
+    return rng.integers(0, 2 ** 40, n, dtype=np.uint64)
+
+
+def gen_uniform(n, seed=42, key_len=16, value_len=100):
+    rng = np.random.default_rng(seed)
+    assert key_len == 16
+    keys = _sorted_keys16(rng, n)
+    vals = _random_bytes(rng, n * value_len)
+    return (keys, _offsets(np.full(n, key_len, np.uint64)), vals,
+            _offsets(np.full(n, value_len, np.uint64)), _ts(rng, n))
+
+
+def gen_zipf(n, seed=43, nprefix=1024, s=1.1, value_len=100):
+    rng = np.random.default_rng(seed)
+    prefixes = np.frombuffer(rng.bytes(12 * nprefix), np.uint8).reshape(nprefix, 12)
+    order = np.lexsort(prefixes.T[::-1])          # sort prefixes bytewise
+    prefixes = prefixes[order]
+    w = 1.0 / np.arange(1, nprefix + 1) ** s
+    popularity = rng.permutation(nprefix)          # which sorted prefix gets which Zipf rank
+    p = w[popularity]
+    p /= p.sum()
+    counts = rng.multinomial(n, p)
+    if counts.max() >= 2 ** 32:
+        raise ValueError("counter overflow")
+    pidx = np.repeat(np.arange(nprefix), counts)
+    starts = np.repeat(np.cumsum(counts) - counts, counts)
+    ctr = (np.arange(n) - starts).astype(np.uint32)
+    keys = np.empty((n, 16), np.uint8)
+    keys[:, :12] = prefixes[pidx]
+    keys[:, 12:] = ctr.astype(">u4").view(np.uint8).reshape(n, 4)
+    vals = _random_bytes(rng, n * value_len)
+    return (keys.reshape(-1), _offsets(np.full(n, 16, np.uint64)), vals,
+            _offsets(np.full(n, value_len, np.uint64)), _ts(rng, n))
+
+
+def gen_mixed(n, seed=44, vmin=8, vmax=4096):
+    rng = np.random.default_rng(seed)
+    keys = _sorted_keys16(rng, n)
+    vl = np.exp(rng.uniform(np.log(vmin), np.log(vmax + 1), n)).astype(np.uint64)
+    vl = np.clip(vl, vmin, vmax)
+    vals = _random_bytes(rng, int(vl.sum()))
+    return keys, _offsets(np.full(n, 16, np.uint64)), vals, _offsets(vl), _ts(rng, n)
+
+
+GENERATORS = {"U": gen_uniform, "Z": gen_zipf, "M": gen_mixed}
+BLOCK_SIZE = {"U": 4096, "Z": 4096, "M": 65536}
+
+
+def segments_by_bytes(key_off, val_off, target=2 << 20):
+    """Segment (SST) starts: a new segment each time the running encoded-size estimate
+    (klen + vlen + 16 per entry) crosses a multiple of `target` bytes."""
+    n = len(key_off) - 1
+    if n == 0:
+        return np.zeros(1, np.uint32)
+    sz = (np.diff(key_off.astype(np.int64)) + np.diff(val_off.astype(np.int64)) + 16)
+    seg_id = (np.cumsum(sz) - sz) // target
+    starts = np.flatnonzero(np.diff(seg_id)) + 1
+    return np.concatenate([[0], starts, [n]]).astype(np.uint32)

@@ -1,0 +1,197 @@
+"""ctypes wrapper over the C restatement (lsmblk_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as
+the checker or the timed CPU baseline.  The product package (lsm_amd) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "liblsmblk_oracle.so")
+_lib = None
+
+ORC_OK, ORC_E_INVAL, ORC_E_MALFORMED, ORC_E_CAPACITY, ORC_E_OVERFLOW = 0, -1, -2, -3, -7
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        P, S, U32, U64, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        L.orc_builder_new.restype = P
+        L.orc_builder_new.argtypes = [S]
+        L.orc_builder_free.argtypes = [P]
+        L.orc_builder_add.argtypes = [P, P, S, U64, P, S]
+        L.orc_builder_add.restype = I
+        L.orc_builder_is_empty.argtypes = [P]
+        L.orc_builder_estimated_size.argtypes = [P]
+        L.orc_builder_estimated_size.restype = S
+        L.orc_builder_finish.argtypes = [P, P, S, ctypes.POINTER(S)]
+        L.orc_encode_segments.argtypes = [P, P, U32, S, P, U64, P, U64,
+                                          ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.orc_decode_blocks.argtypes = [P, P, U64, P, U64, U64, U64,
+                                        ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.orc_segment_like_compaction.argtypes = [P, S, U64, P, U64, ctypes.POINTER(U64)]
+        L.orc_block_seek_key.argtypes = [P, S, P, S]
+        L.orc_block_seek_key.restype = S
+        L.orc_block_entry_verbatim.argtypes = [P, S, S, ctypes.POINTER(U32), ctypes.POINTER(U32),
+                                               ctypes.POINTER(S), ctypes.POINTER(S)]
+        L.orc_crc32.argtypes = [P, S]
+        L.orc_crc32.restype = U32
+        _lib = L
+    return _lib
+
+
+class _OrcKV(ctypes.Structure):
+    _fields_ = [("keys", ctypes.c_void_p), ("key_off", ctypes.c_void_p), ("vals", ctypes.c_void_p),
+                ("val_off", ctypes.c_void_p), ("ts", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+
+
+@dataclass
+class KV:
+    """SoA KV stream in host memory (numpy)."""
+    keys: np.ndarray      # u8
+    key_off: np.ndarray   # u32[n+1]
+    vals: np.ndarray      # u8
+    val_off: np.ndarray   # u32[n+1]
+    ts: np.ndarray        # u64[n]
+
+    @property
+    def n(self):
+        return len(self.ts)
+
+    def entry(self, i):
+        return (bytes(self.keys[self.key_off[i]:self.key_off[i + 1]]), int(self.ts[i]),
+                bytes(self.vals[self.val_off[i]:self.val_off[i + 1]]))
+
+    def entries(self):
+        return [self.entry(i) for i in range(self.n)]
+
+    @staticmethod
+    def from_entries(entries):
+        keys = b"".join(k for k, _, _ in entries)
+        vals = b"".join(v for _, _, v in entries)
+        ko = np.zeros(len(entries) + 1, np.uint32)
+        vo = np.zeros(len(entries) + 1, np.uint32)
+        ko[1:] = np.cumsum([len(k) for k, _, _ in entries]) if entries else []
+        vo[1:] = np.cumsum([len(v) for _, _, v in entries]) if entries else []
+        return KV(np.frombuffer(keys, np.uint8).copy(), ko, np.frombuffer(vals, np.uint8).copy(), vo,
+                  np.array([t for _, t, _ in entries], np.uint64))
+
+    def _c(self):
+        for a in (self.keys, self.key_off, self.vals, self.val_off, self.ts):
+            assert a.flags["C_CONTIGUOUS"]
+        s = _OrcKV(self.keys.ctypes.data, self.key_off.ctypes.data, self.vals.ctypes.data,
+                   self.val_off.ctypes.data, self.ts.ctypes.data, self.n)
+        return s
+
+
+def _ptr(a):
+    return a.ctypes.data if a.size else None
+
+
+def encode_segments(kv: KV, seg_start, block_size: int):
+    """-> (rc, blocks u8, blk_off u64[nblk+1])."""
+    seg = np.ascontiguousarray(seg_start, np.uint32)
+    nseg = len(seg) - 1
+    # upper bounds: every entry its own block, plus trailer bytes
+    out_cap = int(len(kv.keys) + len(kv.vals) + 18 * kv.n + 16)
+    blk_cap = kv.n + 1
+    out = np.zeros(max(out_cap, 1), np.uint8)
+    blk_off = np.zeros(blk_cap, np.uint64)
+    nb, nbytes = ctypes.c_uint64(), ctypes.c_uint64()
+    c = kv._c()
+    rc = lib().orc_encode_segments(ctypes.byref(c), seg.ctypes.data, nseg, block_size,
+                                   out.ctypes.data, out_cap, blk_off.ctypes.data, blk_cap,
+                                   ctypes.byref(nb), ctypes.byref(nbytes))
+    return rc, out[:nbytes.value], blk_off[:nb.value + 1]
+
+
+def decode_blocks(blocks, blk_off):
+    """-> (rc, KV)."""
+    blocks = np.ascontiguousarray(blocks, np.uint8)
+    blk_off = np.ascontiguousarray(blk_off, np.uint64)
+    nblk = len(blk_off) - 1
+    n, K, V = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    L = lib()
+    # first pass with zero capacity to learn the totals
+    empty = _OrcKV(None, None, None, None, None, 0)
+    rc = L.orc_decode_blocks(_ptr(blocks), blk_off.ctypes.data, nblk, ctypes.byref(empty), 0, 0, 0,
+                             ctypes.byref(n), ctypes.byref(K), ctypes.byref(V))
+    if rc not in (ORC_OK, ORC_E_CAPACITY):
+        return rc, None
+    kv = KV(np.zeros(max(K.value, 1), np.uint8), np.zeros(n.value + 1, np.uint32),
+            np.zeros(max(V.value, 1), np.uint8), np.zeros(n.value + 1, np.uint32),
+            np.zeros(n.value, np.uint64))
+    c = _OrcKV(kv.keys.ctypes.data, kv.key_off.ctypes.data, kv.vals.ctypes.data,
+               kv.val_off.ctypes.data, kv.ts.ctypes.data if n.value else None, 0)
+    rc = L.orc_decode_blocks(_ptr(blocks), blk_off.ctypes.data, nblk, ctypes.byref(c), n.value,
+                             K.value, V.value, ctypes.byref(n), ctypes.byref(K), ctypes.byref(V))
+    kv.keys = kv.keys[:K.value]
+    kv.vals = kv.vals[:V.value]
+    return rc, kv
+
+
+def segment_like_compaction(kv: KV, block_size: int, target_sst_size: int):
+    seg = np.zeros(kv.n + 2, np.uint32)
+    ns = ctypes.c_uint64()
+    c = kv._c()
+    rc = lib().orc_segment_like_compaction(ctypes.byref(c), block_size, target_sst_size,
+                                           seg.ctypes.data, len(seg), ctypes.byref(ns))
+    assert rc == ORC_OK, rc
+    return seg[:ns.value + 1]
+
+
+class Builder:
+    """Per-entry BlockBuilder (src/block/builder.rs) on the C restatement."""
+
+    def __init__(self, block_size):
+        self.h = lib().orc_builder_new(block_size)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_builder_free(self.h)
+
+    def add(self, key: bytes, ts: int, value: bytes) -> int:
+        return lib().orc_builder_add(self.h, key, len(key), ts, value, len(value))
+
+    def is_empty(self):
+        return bool(lib().orc_builder_is_empty(self.h))
+
+    def estimated_size(self):
+        return lib().orc_builder_estimated_size(self.h)
+
+    def finish(self) -> bytes:
+        cap = self.estimated_size()
+        buf = ctypes.create_string_buffer(cap)
+        ln = ctypes.c_size_t()
+        rc = lib().orc_builder_finish(self.h, buf, cap, ctypes.byref(ln))
+        assert rc == ORC_OK, rc
+        return buf.raw[:ln.value]
+
+
+def seek_key(block: bytes, key: bytes) -> int:
+    return lib().orc_block_seek_key(block, len(block), key, len(key))
+
+
+def entry_verbatim(block: bytes, idx: int):
+    p, s = ctypes.c_uint32(), ctypes.c_uint32()
+    vb, ve = ctypes.c_size_t(), ctypes.c_size_t()
+    rc = lib().orc_block_entry_verbatim(block, len(block), idx, ctypes.byref(p), ctypes.byref(s),
+                                        ctypes.byref(vb), ctypes.byref(ve))
+    assert rc == ORC_OK
+    return p.value, s.value, vb.value, ve.value
+
+
+def crc32(data: bytes) -> int:
+    return lib().orc_crc32(data, len(data))

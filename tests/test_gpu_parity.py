@@ -1,0 +1,228 @@
+"""GPU parity: the HIP batch path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact -- encoded blocks byte for byte, decoded KV streams array for array.
+The oracle (oracle/lsmblk_oracle.c) is only the checker here.
+"""
+import numpy as np
+import pytest
+import torch
+
+from lsm_amd import batch, synth
+from lsm_amd._lib import LSMBLK_E_CAPACITY, LSMBLK_E_MALFORMED, LsmBlkError
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+def to_dev(kv: O.KV):
+    return batch.KVStream.from_numpy(kv.keys, kv.key_off, kv.vals, kv.val_off, kv.ts)
+
+
+def dev_blocks(blocks, blk_off, shift=0):
+    buf = torch.zeros(len(blocks) + shift + 16, dtype=torch.uint8, device="cuda")
+    if len(blocks):
+        buf[shift:shift + len(blocks)] = torch.from_numpy(np.ascontiguousarray(blocks))
+    off = torch.from_numpy(np.ascontiguousarray(blk_off, np.uint64).view(np.int64)).cuda()
+    return buf[shift:shift + len(blocks)], off
+
+
+def assert_kv_equal(dkv: batch.KVStream, ref: O.KV):
+    keys, ko, vals, vo, ts = dkv.to_numpy()
+    assert dkv.n == ref.n
+    np.testing.assert_array_equal(ko, ref.key_off)
+    np.testing.assert_array_equal(vo, ref.val_off)
+    np.testing.assert_array_equal(ts, ref.ts)
+    np.testing.assert_array_equal(keys, ref.keys[:ref.key_off[-1]])
+    np.testing.assert_array_equal(vals, ref.vals[:ref.val_off[-1]])
+
+
+def roundtrip_check(kv: O.KV, seg, block_size, shift=0):
+    """GPU encode == oracle encode; GPU decode(oracle blocks) == oracle decode."""
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, block_size)
+    assert rc == 0
+    blocks, blk_off = batch.encode_kv(to_dev(kv), seg, block_size)
+    got_off = blk_off.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got_off, ref_off)
+    got = blocks.cpu().numpy()
+    assert len(got) == len(ref_blocks)
+    mism = np.flatnonzero(got != ref_blocks)
+    assert mism.size == 0, f"first mismatching byte {mism[:8]} of {len(got)}"
+    rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
+    assert rc == 0
+    db, do = dev_blocks(ref_blocks, ref_off, shift)
+    dkv = batch.decode_blocks(db, do)
+    assert_kv_equal(dkv, ref_kv)
+    return ref_blocks, ref_off
+
+
+def week1_day3_kv():
+    # src/tests/week1_day3.rs:45-65
+    return O.KV.from_entries([(b"key_%03d" % (i * 5), 0, b"value_%010d" % i) for i in range(100)])
+
+
+def test_kat_week1_day3_block():
+    kv = week1_day3_kv()
+    blocks, off = roundtrip_check(kv, [0, 100], 10000)
+    assert len(off) == 2 and len(blocks) == 3486
+
+
+def test_week1_day4_day7_block_size_128():
+    kv = week1_day3_kv()
+    _, off = roundtrip_check(kv, [0, 100], 128)
+    assert len(off) - 1 == 34  # week1_day7.rs:83-87 expects <= 34 with ts
+
+
+def test_week3_day1_multi_version():
+    # src/tests/week3_day1.rs:31-40
+    ents = [(b"key%05d" % (i // 5), 5 - (i % 5), b"value%05d" % i) for i in range(100)]
+    kv = O.KV.from_entries(ents)
+    roundtrip_check(kv, [0, 100], 128)
+
+
+def test_block_size_16_every_entry_own_block():
+    ents = [(k, 0, v) for k, v in [(b"11", b"11"), (b"22", b"22"), (b"33", b"11"), (b"44", b"22"),
+                                   (b"55", b"11"), (b"66", b"22")]]
+    kv = O.KV.from_entries(ents)
+    _, off = roundtrip_check(kv, [0, 6], 16)
+    assert len(off) - 1 == 6
+
+
+@pytest.mark.parametrize("cfg,n", [("U", 10000), ("Z", 20000), ("M", 3000)])
+def test_configs_small(cfg, n):
+    kv = O.KV(*synth.GENERATORS[cfg](n, seed=7))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 256 << 10)
+    roundtrip_check(kv, seg, synth.BLOCK_SIZE[cfg])
+
+
+def test_cpu_plumbing_config_323_blocks():
+    kv = O.KV(*synth.gen_uniform(10000, seed=0))
+    _, off = roundtrip_check(kv, [0, kv.n], 4096)
+    assert len(off) - 1 == 323
+
+
+def test_unaligned_block_stream():
+    kv = O.KV(*synth.gen_uniform(3000, seed=3))
+    roundtrip_check(kv, [0, kv.n], 4096, shift=3)
+
+
+def test_unaligned_key_and_value_arenas():
+    kv = O.KV(*synth.gen_zipf(5000, seed=5))
+    rc, ref_blocks, ref_off = O.encode_segments(kv, [0, kv.n], 4096)
+    d = to_dev(kv)
+    # re-home the arenas at odd addresses
+    kbuf = torch.zeros(d.keys.numel() + 32, dtype=torch.uint8, device="cuda")
+    vbuf = torch.zeros(d.vals.numel() + 32, dtype=torch.uint8, device="cuda")
+    kbuf[5:5 + d.keys.numel()] = d.keys
+    vbuf[11:11 + d.vals.numel()] = d.vals
+    d.keys, d.vals = kbuf[5:5 + d.keys.numel()], vbuf[11:11 + d.vals.numel()]
+    blocks, blk_off = batch.encode_kv(d, [0, kv.n], 4096)
+    np.testing.assert_array_equal(blocks.cpu().numpy(), ref_blocks)
+
+
+def test_many_tiny_entries_per_block():
+    # 1-byte keys cannot be unique for long; use 2..4-byte keys and empty values (tombstones)
+    rng = np.random.default_rng(1)
+    keys = sorted({bytes(rng.integers(0, 256, rng.integers(1, 5), dtype=np.uint8)) for _ in range(6000)})
+    ents = [(k, int(rng.integers(0, 1 << 40)), b"" if i % 3 else b"v") for i, k in enumerate(keys)]
+    kv = O.KV.from_entries(ents)
+    _, off = roundtrip_check(kv, [0, kv.n], 4096)
+    assert (np.diff(off) > 0).all()
+
+
+def test_long_keys_and_shared_prefixes():
+    rng = np.random.default_rng(2)
+    base = bytes(rng.integers(0, 256, 90, dtype=np.uint8))
+    keys = sorted({base[:int(rng.integers(20, 90))] + bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+                   for _ in range(2000)})
+    ents = [(k, i, bytes(rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8)))
+            for i, k in enumerate(keys)]
+    kv = O.KV.from_entries(ents)
+    roundtrip_check(kv, [0, kv.n], 4096)
+    roundtrip_check(kv, [0, 700, 700, 1500, kv.n], 1024)  # includes an empty segment
+
+
+def test_oversize_entries_and_u16_wrap():
+    # a 70000-byte value: always accepted as a block's first entry; value_len `as u16` wraps
+    ents = [(b"a", 1, b"x" * 10), (b"b", 2, bytes(range(256)) * 273 + b"yz"), (b"c", 3, b"z" * 5000),
+            (b"d", 4, b"w")]
+    kv = O.KV.from_entries(ents)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, [0, kv.n], 4096)
+    blocks, blk_off = batch.encode_kv(to_dev(kv), [0, kv.n], 4096)
+    np.testing.assert_array_equal(blk_off.cpu().numpy().view(np.uint64), ref_off)
+    np.testing.assert_array_equal(blocks.cpu().numpy(), ref_blocks)
+
+
+def test_one_entry_segments():
+    kv = O.KV(*synth.gen_uniform(500, seed=9))
+    roundtrip_check(kv, np.arange(kv.n + 1, dtype=np.uint32), 4096)
+
+
+def test_malformed_block_reported():
+    kv = week1_day3_kv()
+    rc, blocks, off = O.encode_segments(kv, [0, 100], 4096)
+    bad = blocks.copy()
+    bad[int(off[1]) - 2:int(off[1])] = 0xFF  # entry count 65535: offsets would start before the block
+    db, do = dev_blocks(bad, off)
+    with pytest.raises(LsmBlkError) as e:
+        batch.decode_blocks(db, do)
+    assert e.value.status == LSMBLK_E_MALFORMED
+
+
+def test_decode_capacity_reports_required_sizes():
+    kv = O.KV(*synth.gen_uniform(2000, seed=4))
+    rc, blocks, off = O.encode_segments(kv, [0, kv.n], 4096)
+    db, do = dev_blocks(blocks, off)
+    out = batch.KVStream(torch.zeros(1024, dtype=torch.uint8, device="cuda"),
+                         torch.zeros(101, dtype=torch.int32, device="cuda"),
+                         torch.zeros(1024, dtype=torch.uint8, device="cuda"),
+                         torch.zeros(101, dtype=torch.int32, device="cuda"),
+                         torch.zeros(100, dtype=torch.int64, device="cuda"), 0)
+    stats = torch.zeros(4, dtype=torch.int64, device="cuda")
+    batch.decode_into(db, do, len(off) - 1, out, stats, 100, 1024, 1024)
+    torch.cuda.synchronize()
+    s = stats.cpu().tolist()
+    assert s[:3] == [kv.n, len(kv.keys), len(kv.vals)]
+    assert batch._status(stats) == LSMBLK_E_CAPACITY
+
+
+def test_repeated_calls_are_stable():
+    kv = O.KV(*synth.gen_zipf(8000, seed=11))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 128 << 10)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, 4096)
+    d = to_dev(kv)
+    db, do = dev_blocks(ref_blocks, ref_off)
+    for _ in range(5):
+        blocks, blk_off = batch.encode_kv(d, seg, 4096)
+        np.testing.assert_array_equal(blocks.cpu().numpy(), ref_blocks)
+        dkv = batch.decode_blocks(db, do)
+        assert dkv.n == kv.n
+
+
+@pytest.mark.parametrize("cfg,n,target", [("U", 400_000, 2 << 20), ("Z", 400_000, 2 << 20), ("M", 40_000, 8 << 20)])
+def test_roundtrip_properties_large(cfg, n, target):
+    """At sizes beyond quick oracle checks: decode(encode(kv)) == kv and
+    encode(decode(blocks)) == blocks, plus an oracle check of a sampled segment."""
+    kv = O.KV(*synth.GENERATORS[cfg](n, seed=21))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, target)
+    d = to_dev(kv)
+    blocks, blk_off = batch.encode_kv(d, seg, synth.BLOCK_SIZE[cfg])
+    dkv = batch.decode_blocks(blocks, blk_off)
+    keys, ko, vals, vo, ts = dkv.to_numpy()
+    np.testing.assert_array_equal(ko, kv.key_off)
+    np.testing.assert_array_equal(vo, kv.val_off)
+    np.testing.assert_array_equal(ts, kv.ts)
+    assert torch.equal(dkv.keys[:len(kv.keys)].cpu(), torch.from_numpy(kv.keys))
+    assert torch.equal(dkv.vals[:len(kv.vals)].cpu(), torch.from_numpy(kv.vals))
+    blocks2, blk_off2 = batch.encode_kv(dkv, seg, synth.BLOCK_SIZE[cfg])
+    assert torch.equal(blocks2, blocks) and torch.equal(blk_off2, blk_off)
+    # full oracle check (the C restatement handles these sizes in about a second)
+    rc, rb, ro = O.encode_segments(kv, seg, synth.BLOCK_SIZE[cfg])
+    assert rc == 0
+    np.testing.assert_array_equal(blk_off.cpu().numpy().view(np.uint64), ro)
+    np.testing.assert_array_equal(blocks.cpu().numpy(), rb)
