@@ -74,9 +74,10 @@ SIGNATURES = [
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_build.SO):
-            raise RuntimeError(f"liblsmblk.so not built ({_build.SO}); run __graft_entry__.build()")
-        L = ctypes.CDLL(_build.SO)
+        so = os.environ.get("LSMBLK_SO_OVERRIDE", _build.SO)  # debug builds only
+        if not os.path.exists(so):
+            raise RuntimeError(f"liblsmblk.so not built ({so}); run __graft_entry__.build()")
+        L = ctypes.CDLL(so)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)
             fn.restype = res

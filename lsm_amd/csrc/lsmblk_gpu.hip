@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -66,8 +67,13 @@ __device__ __forceinline__ T wave_sum(T v) {
   for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   return v;
 }
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)nbytes, 0x00020000);
+// Buffer descriptors: raw buffer loads return 0 for every dword that extends past
+// num_records, so each descriptor is based at a 16-B-aligned absolute address and its size
+// rounded up to 16 B.  A 16-B-aligned chunk holding at least one valid byte never crosses a
+// page, so the extra tail bytes are always mapped (their values are never used).
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p16, uint32_t nbytes) {
+  const uint32_t n = nbytes >= 0xFFFFFFF0u ? 0xFFFFFFFFu : (nbytes + 15) & ~15u;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p16), (short)0, (int)n, 0x00020000);
 }
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF); }
 
@@ -76,22 +82,30 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFF) << 
 // Written by one relaxed agent-scope store (global_store sc1), read by relaxed agent-scope
 // loads: the value and its tag travel in one naturally aligned 8-byte word, so no fence is
 // needed (MI355X_MICROARCH.md, "granule" hand-off).
-__device__ __forceinline__ uint64_t gload(const uint64_t* p) {
+// Poll protocol (kernel argument `poll`): 0 = sc1 loads; 1 = sc1 loads + agent acquire
+// fence between polls; 2 = agent-scope atomic RMW (fetch_or 0) polls and atomic-swap
+// publishes, performed at the coherence point.
+__device__ __forceinline__ uint64_t gload(const uint64_t* p, uint32_t poll) {
+  if (poll == 2)
+    return __hip_atomic_fetch_or(const_cast<uint64_t*>(p), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void gstore(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void gstore(uint64_t* p, uint64_t v, uint32_t poll) {
+  if (poll == 2)
+    (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int NQ>
 __device__ __forceinline__ void publish(uint64_t* arr, uint64_t idx, const uint64_t (&v)[NQ],
-                                        uint32_t tag, uint32_t flag) {
+                                        uint32_t tag, uint32_t flag, uint32_t poll) {
   const uint32_t l = lane_id();
   if (l < NQ) {
     uint64_t x = v[0];
     if (NQ > 1 && l == 1) x = v[1 % NQ];
     if (NQ > 2 && l == 2) x = v[2 % NQ];
-    gstore(arr + idx * NQ + l, (x << 16) | (uint64_t(tag) << 2) | flag);
+    gstore(arr + idx * NQ + l, (x << 16) | (uint64_t(tag) << 2) | flag, poll);
   }
 }
 
@@ -99,7 +113,7 @@ __device__ __forceinline__ void publish(uint64_t* arr, uint64_t idx, const uint6
 // on timeout (then excl is garbage and the caller raises LSMBLK_ERR_TIMEOUT).
 template <int NQ>
 __device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self, uint32_t tag,
-                         uint64_t (&excl)[NQ]) {
+                         uint32_t poll, uint64_t (&excl)[NQ]) {
   const uint32_t l = lane_id();
   const uint64_t want_agg = (uint64_t(tag) << 2) | 1, want_inc = (uint64_t(tag) << 2) | 2;
 #pragma unroll
@@ -114,12 +128,12 @@ __device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self
       if (idx >= 0) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          vi[q] = gload(inc + idx * NQ + q);
+          vi[q] = gload(inc + idx * NQ + q, poll);
           li = li && ((vi[q] & 0xFFFF) == want_inc);
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          va[q] = gload(agg + idx * NQ + q);
+          va[q] = gload(agg + idx * NQ + q, poll);
           la = la && ((va[q] & 0xFFFF) == want_agg);
         }
       } else {
@@ -140,7 +154,20 @@ __device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self
         pred -= 64;
         break;
       }
-      if (++spins > kSpinLimit) return false;
+      if (++spins > kSpinLimit) {
+#ifdef LSMBLK_DEVICE_DEBUG
+        const uint64_t lm = __ballot(la);
+        if (l == 0)
+          printf("lookback timeout self=%llu pred=%lld incmask=%llx readymask=%llx aggmask=%llx first=%u\n",
+                 (unsigned long long)self, (long long)pred, (unsigned long long)im, (unsigned long long)rm,
+                 (unsigned long long)lm, first);
+        if (l == first - 1 || l == 0)
+          printf("  lane %u idx=%lld inc=%llx agg=%llx\n", l, (long long)idx, (unsigned long long)vi[0],
+                 (unsigned long long)va[0]);
+#endif
+        return false;
+      }
+      if (poll == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __builtin_amdgcn_s_sleep(2);
     }
   }
@@ -222,6 +249,7 @@ struct DecodeArgs {
   uint64_t* agg;
   uint64_t* inc;
   uint32_t tag;
+  uint32_t poll;
 };
 
 constexpr uint32_t kDecWaves = 4;
@@ -436,6 +464,11 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
   }
   if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
   const bool fast = fits && h.n <= kDecMaxE;
+#ifdef LSMBLK_DEVICE_DEBUG
+  if (l == 0) printf("dec b=%llu start=%llu end=%llu len=%u lead=%u fits=%d n=%u data_end=%u fks=%u ok=%d err=%u img0=%02x %02x %02x %02x last=%02x %02x\n",
+                     (unsigned long long)b, (unsigned long long)start, (unsigned long long)end, len, lead, (int)fits, h.n, h.data_end, h.fks, (int)h.ok, err,
+                     L.img[lead], L.img[lead + 1], L.img[lead + 2], L.img[lead + 3], L.img[lead + len - 2], L.img[lead + len - 1]);
+#endif
 
   // phase 1: parse entries, block aggregates (entries, key bytes, value bytes)
   uint64_t K = 0, V = 0;
@@ -486,12 +519,12 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
   // publish + look-back
   uint64_t excl[3] = {0, 0, 0};
   if (b == 0) {
-    publish<3>(a.inc, b, agg, a.tag, 2);
+    publish<3>(a.inc, b, agg, a.tag, 2, a.poll);
   } else {
-    publish<3>(a.agg, b, agg, a.tag, 1);
-    if (!lookback<3>(a.agg, a.inc, b, a.tag, excl)) err |= LSMBLK_ERR_TIMEOUT;
+    publish<3>(a.agg, b, agg, a.tag, 1, a.poll);
+    if (!lookback<3>(a.agg, a.inc, b, a.tag, a.poll, excl)) err |= LSMBLK_ERR_TIMEOUT;
     const uint64_t inc[3] = {excl[0] + agg[0], excl[1] + agg[1], excl[2] + agg[2]};
-    publish<3>(a.inc, b, inc, a.tag, 2);
+    publish<3>(a.inc, b, inc, a.tag, 2, a.poll);
   }
   wave_sync();
   const uint64_t E0 = excl[0], K0 = excl[1], V0 = excl[2];
@@ -508,6 +541,11 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
       dec_simple_outputs(a, GlbImg{R, lead}, h, E0, K0, V0);
     }
   }
+#ifdef LSMBLK_DEVICE_DEBUG
+  if (l == 0) printf("dec b=%llu agg=%llu %llu %llu excl=%llu %llu %llu err=%u\n", (unsigned long long)b,
+                     (unsigned long long)agg[0], (unsigned long long)agg[1], (unsigned long long)agg[2],
+                     (unsigned long long)E0, (unsigned long long)K0, (unsigned long long)V0, err);
+#endif
   if (b == a.nblk - 1 && l == 0) {
     a.stats[0] = Et;
     a.stats[1] = Kt;
@@ -539,6 +577,7 @@ struct PlanArgs {
   uint64_t* agg;
   uint64_t* inc;
   uint32_t tag;
+  uint32_t poll;
 };
 
 constexpr uint32_t kPlanWaves = 4;
@@ -554,7 +593,7 @@ struct alignas(16) PlanLds {
 // Key bytes of the batch, served from the LDS chunk when it holds them.
 struct PlanKeys {
   rsrc_t gk;          // whole key arena, base aligned down to 4
-  uint32_t glead;     // keys pointer & 3
+  uint32_t glead;     // keys pointer & 15 (descriptor base is 16-B aligned)
   const uint8_t* lk;  // LDS chunk (16-aligned)
   uint32_t lbase;     // arena offset of lk[llead]
   uint32_t llead;
@@ -616,7 +655,7 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
   }
   const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys);
   PlanKeys K;
-  K.glead = uint32_t(kaddr & 3);
+  K.glead = uint32_t(kaddr & 15);
   const uint32_t ktotal = uni(a.key_off[a.n]);
   K.gk = make_rsrc(a.keys - K.glead, K.glead + ktotal);
   K.lk = L.keys;
@@ -704,12 +743,12 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
   uint64_t agg[2] = {nb, bytes};
   uint64_t excl[2] = {0, 0};
   if (g == 0) {
-    publish<2>(a.inc, g, agg, a.tag, 2);
+    publish<2>(a.inc, g, agg, a.tag, 2, a.poll);
   } else {
-    publish<2>(a.agg, g, agg, a.tag, 1);
-    if (!lookback<2>(a.agg, a.inc, g, a.tag, excl)) err |= LSMBLK_ERR_TIMEOUT;
+    publish<2>(a.agg, g, agg, a.tag, 1, a.poll);
+    if (!lookback<2>(a.agg, a.inc, g, a.tag, a.poll, excl)) err |= LSMBLK_ERR_TIMEOUT;
     const uint64_t inc[2] = {excl[0] + agg[0], excl[1] + agg[1]};
-    publish<2>(a.inc, g, inc, a.tag, 2);
+    publish<2>(a.inc, g, inc, a.tag, 2, a.poll);
   }
   // make this wave's record stores visible to its own later loads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -879,7 +918,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     const bool fast = n <= kEmitMaxE && klead + (kb1 - kb0) + 8 <= kEmitKCap &&
                       vlead + (vb1 - vb0) + 8 <= kEmitVCap && olead + size + 8 <= kEmitOCap;
     if (!fast) {
-      const uint32_t kg = uint32_t(kaddr & 3), vg = uint32_t(vaddr & 3);
+      const uint32_t kg = uint32_t(kaddr & 15), vg = uint32_t(vaddr & 15);
       const uint32_t kt = uni(a.key_off[a.n]), vt = uni(a.val_off[a.n]);
       const GlbBytes KB{make_rsrc(a.keys - kg, kg + kt), kg};
       const GlbBytes VB{make_rsrc(a.vals - vg, vg + vt), vg};
@@ -1029,6 +1068,7 @@ struct lsmblk_ctx {
   uint32_t* blk_first = nullptr;
   uint64_t rec_cap = 0;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
+  uint32_t poll = 2;             // look-back poll protocol (see gload)
 };
 
 namespace {
@@ -1113,6 +1153,7 @@ int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
   auto* c = new (std::nothrow) lsmblk_ctx();
   if (!c) return LSMBLK_E_NOMEM;
   c->device = device;
+  if (const char* e = getenv("LSMBLK_POLL_MODE")) c->poll = uint32_t(atoi(e));
   if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->counters, 64) != hipSuccess) {
     delete c;
     return LSMBLK_E_HIP;
@@ -1175,6 +1216,7 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   a.agg = c->dec_agg;
   a.inc = c->dec_inc;
   a.tag = c->epoch;
+  a.poll = c->poll;
   const uint64_t grid = (nblk + kDecWaves - 1) / kDecWaves;
   hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(grid)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
@@ -1218,6 +1260,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   p.agg = c->seg_agg;
   p.inc = c->seg_inc;
   p.tag = c->epoch;
+  p.poll = c->poll;
   hipLaunchKernelGGL(plan_kernel, dim3((nseg + kPlanWaves - 1) / kPlanWaves), dim3(256), 0, st, p);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   EmitArgs e;
