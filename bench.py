@@ -1,0 +1,262 @@
+"""bench.py -- device-resident SSTable block decode + re-encode throughput (BASELINE.json metric).
+
+One step = decode the whole resident batch of encoded blocks into the SoA KV stream, then
+re-encode that stream into blocks from the segment (SST) starts alone (the anti-shortcut
+rule of SURVEY.md section 8(d)): the reference's Block::decode + BlockIterator walk
+followed by SsTableBuilder::add / BlockBuilder over every SST.  The re-encoded bytes are
+checked equal to the input after the timed region.
+
+Default workload (configs[1]): 1,048,576 x 4 KiB blocks per GPU, uniform sorted 16-B keys,
+100-B values, 40-bit ts, 2 MiB segments.  --config Z / M select the other single-GPU configs.
+
+  python bench.py --gpus N --steps K --warmup W          (N>1: torchrun, one rank per GPU)
+
+Prints ONE JSON line on rank 0.  `value` = encoded-block GiB processed per second by all
+ranks (weak scaling: every rank owns its own 1 Mi blocks; no collective on the data path,
+only the timing barrier / max-reduce).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from lsm_amd import batch, synth  # noqa: E402
+from lsm_amd._lib import check, lib  # noqa: E402
+
+METRIC = "GiB/s device-resident SSTable block encode+decode, 4 KiB blocks, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GiB = float(1 << 30)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="U", choices=["U", "Z", "M"])
+    p.add_argument("--blocks", type=int, default=None, help="blocks per GPU (default 1 Mi for U/Z, 64 Ki for M)")
+    p.add_argument("--segment-bytes", type=int, default=2 << 20)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pcie", action="store_true", help="also time the H2D+D2H-inclusive rate (DESIGN.md)")
+    return p.parse_args()
+
+
+def build_workload(cfg, nblk, seg_bytes, seed, dev):
+    """Synthetic KV stream -> GPU-encoded blocks truncated to exactly nblk blocks."""
+    bs = synth.BLOCK_SIZE[cfg]
+    per_block = {"U": 31.0, "Z": 34.5, "M": 95.0}[cfg]
+    n = int(nblk * per_block * 1.03) + 1024
+    t = time.time()
+    keys, ko, vals, vo, ts = synth.GENERATORS[cfg](n, seed=seed)
+    seg = synth.segments_by_bytes(ko, vo, seg_bytes)
+    d = batch.KVStream.from_numpy(keys, ko, vals, vo, ts, device=dev)
+    del keys, vals
+    blocks, blk_off = batch.encode_kv(d, seg, bs)
+    del d
+    total_blocks = blk_off.numel() - 1
+    if total_blocks < nblk:
+        raise RuntimeError(f"generated {total_blocks} < {nblk} blocks; raise per_block estimate")
+    end = int(blk_off[nblk].item())
+    blocks = blocks[:end].clone()
+    blk_off = blk_off[:nblk + 1].clone()
+    kv = batch.decode_blocks(blocks, blk_off)            # exactly the entries of the kept blocks
+    seg = seg[seg < kv.n]
+    seg = np.concatenate([seg, [kv.n]]).astype(np.uint32)
+    log(f"[rank] workload {cfg}: {nblk} blocks, {kv.n} entries, {end / GiB:.3f} GiB encoded, "
+        f"{len(seg) - 1} segments, setup {time.time() - t:.1f}s")
+    return blocks, blk_off, kv, seg, bs
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} != --gpus {args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = args.config
+    nblk = args.blocks or (65536 if cfg == "M" else 1 << 20)
+
+    blocks, blk_off, kv, seg, bs = build_workload(cfg, nblk, args.segment_bytes, 1000 + rank, dev)
+    E = int(blocks.numel())
+    K = int(kv.key_off[kv.n].item()) & 0xFFFFFFFF
+    V = int(kv.val_off[kv.n].item()) & 0xFFFFFFFF
+    n = kv.n
+    D = K + V + 16 * n  # decoded SoA bytes: key + value + u64 ts + u32 key_off + u32 val_off
+
+    # preallocated buffers, workspace reserved: the timed region does no allocation
+    out_kv = batch.KVStream(batch._aligned_empty(K + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
+                            batch._aligned_empty(V + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
+                            torch.empty(n, dtype=torch.int64, device=dev), n)
+    out_cap, blk_cap = E + 16, nblk + 2
+    out_blocks = batch._aligned_empty(out_cap, dev)
+    out_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    seg_t = torch.from_numpy(seg.view(np.int32)).to(dev)
+    st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
+    st_enc = torch.zeros(4, dtype=torch.int64, device=dev)
+    ctx = batch._ctx(local)
+    check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
+        if ev is not None:
+            ev[1].record(stream)
+        batch.encode_into(out_kv, seg_t, len(seg) - 1, bs, out_blocks, out_cap, out_off, blk_cap, st_enc)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    dec_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    enc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    # correctness of the last step: re-encoded bytes == input bytes
+    sd, se = st_dec.cpu().tolist(), st_enc.cpu().tolist()
+    ok = (sd[3] == 0 and se[3] == 0 and sd[0] == n and se[0] == nblk and se[1] == E
+          and torch.equal(out_blocks[:E], blocks) and torch.equal(out_off[:nblk + 1], blk_off))
+    if not ok:
+        log(f"ROUND TRIP MISMATCH dec_stats={sd} enc_stats={se}")
+
+    t_max = elapsed
+    ok_all = ok
+    if world > 1:
+        tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max, ok_all = float(tt[0].item()), tt[1].item() == 0.0
+
+    result = None
+    if rank == 0:
+        value = world * E * args.steps / t_max / GiB
+        ms_per_step = t_max / args.steps * 1e3
+        # dominant kernel's roofline: algorithmic bytes per launch / launch duration
+        dec_bytes, enc_bytes = E + D + 8 * (nblk + 1), D + E + 8 * (nblk + 1)
+        dom_name, dom_bytes, dom_ms = ("decode", dec_bytes, dec_ms) if dec_ms >= enc_ms else ("encode", enc_bytes, enc_ms)
+        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            tj = json.load(open(tpath))
+            if tj.get("workload") == cfg and tj.get("blocks") == nblk:
+                traffic = tj.get(dom_name)
+        result = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"{cfg}: {nblk} blocks/GPU x block_size {bs}, decode + re-encode "
+                                   f"({'16-B uniform keys, 100-B values' if cfg == 'U' else ('Zipf 12-B prefixes, 100-B values' if cfg == 'Z' else '16-B keys, 8 B-4 KiB values')})",
+                       "blocks_per_gpu": nblk, "entries_per_gpu": n, "encoded_bytes_per_gpu": E,
+                       "decoded_bytes_per_gpu": D, "block_size": bs, "segments_per_gpu": len(seg) - 1,
+                       "parallelism": f"block-sharded x{world} (no data-path collective)",
+                       "roundtrip_bit_exact": bool(ok_all)},
+            "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
+                         "decode_ms": round(dec_ms, 4), "encode_ms": round(enc_ms, 4),
+                         "step_algorithmic_bytes": dec_bytes + enc_bytes},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
+        if args.pcie:
+            result["pcie_inclusive_gib_s"] = pcie_inclusive(blocks, blk_off, E, out_kv, n, K, V, seg_t, seg, bs,
+                                                            out_blocks, out_cap, out_off, blk_cap, nblk, dev)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if result is not None:
+        print(json.dumps(result), flush=True)
+    return 0 if ok_all else 1
+
+
+def cpu_baseline(blocks, blk_off, seg, bs, seconds):
+    """The oracle's C restatement (single thread) on a bounded sample of the same workload:
+    decode + re-encode of the first 16 Ki blocks, repeated for ~`seconds`."""
+    from oracle import oracle as O
+    nb = min(16384, blk_off.numel() - 1)
+    off = blk_off[:nb + 1].cpu().numpy().view(np.uint64)
+    host_blocks = blocks[:int(off[-1])].cpu().numpy()
+    rc, kv = O.decode_blocks(host_blocks, off)
+    assert rc == 0
+    s = seg[seg < kv.n]
+    s = np.concatenate([s, [kv.n]]).astype(np.uint32)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        rc1, kv2 = O.decode_blocks(host_blocks, off)
+        rc2, b2, o2 = O.encode_segments(kv2, s, bs)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    assert rc1 == 0 and rc2 == 0 and np.array_equal(b2, host_blocks)
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(len(host_blocks) * reps / dt / GiB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{nb} blocks ({len(host_blocks) / 2**20:.1f} MiB encoded) decode+re-encode x{reps}, "
+                      f"oracle/lsmblk_oracle.c -O3 single thread, {cpu}, host nproc={os.cpu_count()}"}
+
+
+def pcie_inclusive(blocks, blk_off, E, out_kv, n, K, V, seg_t, seg, bs, out_blocks, out_cap, out_off, blk_cap,
+                   nblk, dev, reps=3):
+    """Blocks start and end in pinned host memory: H2D, decode, re-encode, D2H."""
+    hin = torch.empty(E, dtype=torch.uint8, pin_memory=True)
+    hin.copy_(blocks.cpu())
+    hout = torch.empty(E, dtype=torch.uint8, pin_memory=True)
+    dbuf = torch.empty_like(blocks)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dbuf.copy_(hin, non_blocking=True)
+        batch.decode_into(dbuf, blk_off, nblk, out_kv, st, n, K + 16, V + 16)
+        batch.encode_into(out_kv, seg_t, len(seg) - 1, bs, out_blocks, out_cap, out_off, blk_cap, st)
+        hout.copy_(out_blocks[:E], non_blocking=True)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    assert torch.equal(hout, hin)
+    return round(E / dt / GiB, 3)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
