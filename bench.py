@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pcie", action="store_true", help="also time the H2D+D2H-inclusive rate (DESIGN.md)")
+    p.add_argument("--ablate", type=int, default=None,
+                   help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
     return p.parse_args()
 
 
@@ -127,6 +129,8 @@ def main():
         if ev is not None:
             ev[2].record(stream)
 
+    if args.ablate is not None:
+        return ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -202,6 +206,37 @@ def main():
     if result is not None:
         print(json.dumps(result), flush=True)
     return 0 if ok_all else 1
+
+
+def ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream):
+    from lsm_amd._lib import lib as L
+    res = {}
+    for mask in sorted({0, 1, 2, 4, 8, 14, 15, args.ablate}):
+        check(L().lsmblk_debug_set(ctx, 1, mask))
+        for _ in range(2):
+            batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res[mask] = round(e0.elapsed_time(e1) / args.steps, 3)
+    check(L().lsmblk_debug_set(ctx, 1, 0))
+    polls = {}
+    for pm in (0, 1, 2):
+        check(L().lsmblk_debug_set(ctx, 0, pm))
+        for _ in range(2):
+            batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        polls[pm] = (round(e0.elapsed_time(e1) / args.steps, 3), st_dec.cpu().tolist()[3])
+    print(json.dumps({"ablation_decode_ms_by_skip_mask": res, "decode_ms_err_by_poll_mode": polls}), flush=True)
+    return 0
 
 
 def cpu_baseline(blocks, blk_off, seg, bs, seconds):

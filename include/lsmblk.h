@@ -145,6 +145,14 @@ void lsmblk_ctx_destroy(lsmblk_ctx* ctx);
 int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entries,
                        uint64_t max_segments);
 
+/* Diagnostics (timing experiments only; results are WRONG while a skip mask is set):
+ *   LSMBLK_DEBUG_POLL_MODE    look-back poll protocol: 0 sc1 loads, 1 + agent acquire,
+ *                             2 sc1 first then agent atomic-RMW re-polls (default)
+ *   LSMBLK_DEBUG_DECODE_SKIP  decode ablation mask: 1 look-back, 2 keys, 4 values, 8 metadata */
+#define LSMBLK_DEBUG_POLL_MODE 0
+#define LSMBLK_DEBUG_DECODE_SKIP 1
+int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
+
 /* Decode nblk blocks (block b = blocks[blk_off[b] .. blk_off[b+1]), blk_off u64[nblk+1])
  * into the SoA stream `out` (outputs must be 16-byte aligned).  Asynchronous: completion
  * and error flags are in `stats` once the stream reaches this point. */

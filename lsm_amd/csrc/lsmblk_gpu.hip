@@ -122,23 +122,34 @@ __device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self
   uint32_t spins = 0;
   while (pred >= 0) {
     const int64_t idx = pred - int64_t(l);
+    uint64_t vi[NQ], va[NQ];
+    bool li = idx < 0, la = false;  // lanes before block 0 read as "inclusive 0"
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) vi[q] = va[q] = 0;
+    uint32_t round = 0;
     for (;;) {
-      uint64_t vi[NQ], va[NQ];
-      bool li = true, la = true;
-      if (idx >= 0) {
+      // Only lanes still unresolved poll.  A granule carrying the current epoch tag is the
+      // value its producer wrote (each is written once per epoch), so a ready observation
+      // is final; only not-ready observations are re-polled (first round plain sc1 loads,
+      // later rounds the protocol `poll`).
+      const uint32_t pm = round == 0 ? 0u : poll;
+      if (!li && !la) {
+        bool ri = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          vi[q] = gload(inc + idx * NQ + q, poll);
-          li = li && ((vi[q] & 0xFFFF) == want_inc);
+          vi[q] = gload(inc + idx * NQ + q, pm);
+          ri = ri && ((vi[q] & 0xFFFF) == want_inc);
         }
+        li = ri;
+        if (!ri) {
+          bool ra = true;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          va[q] = gload(agg + idx * NQ + q, poll);
-          la = la && ((va[q] & 0xFFFF) == want_agg);
+          for (int q = 0; q < NQ; ++q) {
+            va[q] = gload(agg + idx * NQ + q, pm);
+            ra = ra && ((va[q] & 0xFFFF) == want_agg);
+          }
+          la = ra;
         }
-      } else {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) vi[q] = va[q] = 0;
       }
       const uint64_t im = __ballot(li);
       const uint64_t rm = __ballot(li || la);
@@ -154,21 +165,10 @@ __device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self
         pred -= 64;
         break;
       }
-      if (++spins > kSpinLimit) {
-#ifdef LSMBLK_DEVICE_DEBUG
-        const uint64_t lm = __ballot(la);
-        if (l == 0)
-          printf("lookback timeout self=%llu pred=%lld incmask=%llx readymask=%llx aggmask=%llx first=%u\n",
-                 (unsigned long long)self, (long long)pred, (unsigned long long)im, (unsigned long long)rm,
-                 (unsigned long long)lm, first);
-        if (l == first - 1 || l == 0)
-          printf("  lane %u idx=%lld inc=%llx agg=%llx\n", l, (long long)idx, (unsigned long long)vi[0],
-                 (unsigned long long)va[0]);
-#endif
-        return false;
-      }
+      ++round;
+      if (++spins > kSpinLimit) return false;
       if (poll == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
     }
   }
   return true;
@@ -245,12 +245,13 @@ struct DecodeArgs {
   uint64_t* ts;
   uint64_t entry_cap, key_cap, val_cap;
   uint64_t* stats;
-  uint32_t* ticket;
-  uint64_t* agg;
-  uint64_t* inc;
-  uint32_t tag;
-  uint32_t poll;
+  const uint32_t* agg;        // per-block (entries, key bytes, value bytes), from dec_count_kernel
+  const uint64_t* tile_pre;   // per-tile exclusive prefix (entries, key bytes, value bytes)
+  uint32_t skip;  // ablation mask (lsmblk_debug_set, timing experiments only): 2 keys,
+                  // 4 values, 8 per-entry metadata
 };
+
+constexpr uint32_t kTile = 64;  // blocks per count tile
 
 constexpr uint32_t kDecWaves = 4;
 constexpr uint32_t kDecImg = 4352;  // staged block bytes per wave (4 KiB blocks + lead + slack)
@@ -332,11 +333,12 @@ __device__ void dec_simple_outputs(const DecodeArgs& a, const Img& im, const Blo
 
 // Fast path: LDS image + LDS tables, coalesced aligned stores.
 __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
-                                 uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V) {
+                                 uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V, uint32_t skip) {
   const uint32_t l = lane_id();
   const uint8_t* img = L.img;
   const LdsImg im{L.img + lead};
   // per-entry metadata
+  if (!(skip & 8))
   for (uint32_t k = l; k < h.n; k += 64) {
     const uint64_t e = E0 + k;
     if (e < a.entry_cap) {
@@ -346,7 +348,7 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
     }
   }
   // keys: dwords of the arena covering [K0, K0+K), bytes resolved per byte.
-  {
+  if (!(skip & 2)) {
     const uint64_t w_begin = K0 >> 2, w_end = (K0 + K + 3) >> 2;
     for (uint64_t w = w_begin + l; w < w_end; w += 64) {
       const int64_t r0 = int64_t(w * 4) - int64_t(K0);
@@ -381,7 +383,7 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
     }
   }
   // values: 16-B chunks of the arena covering [V0, V0+V).
-  {
+  if (!(skip & 4)) {
     const uint64_t c_begin = V0 >> 4, c_end = (V0 + V + 15) >> 4;
     for (uint64_t c = c_begin + l; c < c_end; c += 64) {
       const int64_t rb = int64_t(c * 16) - int64_t(V0);
@@ -435,12 +437,8 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
   }
 }
 
-__global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
-  __shared__ DecLds lds[kDecWaves];
-  DecLds& L = lds[threadIdx.x >> 6];
+__device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   const uint32_t l = lane_id();
-  const uint64_t b = take_ticket(a.ticket);
-  if (b >= a.nblk) return;
   uint32_t err = 0;
   const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
   uint32_t len = 0;
@@ -454,9 +452,15 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
 
   BlockHdr h;
   if (fits) {
+    // all loads in flight before the first LDS write (kDecImg / 1 KiB = at most 5 per lane)
     const uint32_t nchunk = (lead + len + 15) >> 4;
-    for (uint32_t c = l; c < nchunk; c += 64)
-      *reinterpret_cast<u32x4*>(L.img + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(R, c * 16, 0, 0);
+    u32x4 v[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
     wave_sync();
     h = parse_hdr(LdsImg{L.img + lead}, len);
   } else {
@@ -516,15 +520,20 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
   uint64_t agg[3] = {h.n, K, V};
   if (err) agg[0] = agg[1] = agg[2] = 0;
 
-  // publish + look-back
-  uint64_t excl[3] = {0, 0, 0};
-  if (b == 0) {
-    publish<3>(a.inc, b, agg, a.tag, 2, a.poll);
-  } else {
-    publish<3>(a.agg, b, agg, a.tag, 1, a.poll);
-    if (!lookback<3>(a.agg, a.inc, b, a.tag, a.poll, excl)) err |= LSMBLK_ERR_TIMEOUT;
-    const uint64_t inc[3] = {excl[0] + agg[0], excl[1] + agg[1], excl[2] + agg[2]};
-    publish<3>(a.inc, b, inc, a.tag, 2, a.poll);
+  // output bases: tile prefix + this tile's earlier blocks (one coalesced load per lane)
+  uint64_t excl[3];
+  {
+    const uint64_t t = b / kTile, j = b % kTile;
+    uint64_t cn = 0, ck = 0, cv = 0;
+    if (l < j) {
+      const uint64_t q = t * kTile + l;
+      cn = a.agg[3 * q];
+      ck = a.agg[3 * q + 1];
+      cv = a.agg[3 * q + 2];
+    }
+    excl[0] = a.tile_pre[3 * t] + wave_sum(cn);
+    excl[1] = a.tile_pre[3 * t + 1] + wave_sum(ck);
+    excl[2] = a.tile_pre[3 * t + 2] + wave_sum(cv);
   }
   wave_sync();
   const uint64_t E0 = excl[0], K0 = excl[1], V0 = excl[2];
@@ -534,7 +543,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
 
   if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW)) && h.n) {
     if (fast) {
-      dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V));
+      dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
     } else if (fits) {
       dec_simple_outputs(a, LdsImg{L.img + lead}, h, E0, K0, V0);
     } else {
@@ -546,16 +555,188 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
                      (unsigned long long)agg[0], (unsigned long long)agg[1], (unsigned long long)agg[2],
                      (unsigned long long)E0, (unsigned long long)K0, (unsigned long long)V0, err);
 #endif
-  if (b == a.nblk - 1 && l == 0) {
-    a.stats[0] = Et;
-    a.stats[1] = Kt;
-    a.stats[2] = Vt;
-    if (Et <= a.entry_cap) {
-      a.key_off[Et] = uint32_t(Kt);
-      a.val_off[Et] = uint32_t(Vt);
+  raise_err(a.stats, err);
+}
+
+// One wave per block, no inter-wave waiting: the bases come from the count + scan passes.
+__global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
+  __shared__ DecLds lds[kDecWaves];
+  const uint64_t b = uint64_t(blockIdx.x) * kDecWaves + (threadIdx.x >> 6);
+  if (b < a.nblk) decode_block(a, lds[threadIdx.x >> 6], b);
+}
+
+// ---------------------------------------------------------------- decode pass 1: count
+// Header-only parse of every block (trailer, offsets table, 4-6 header bytes per entry) ->
+// per-block (entries, key bytes, value bytes) and per-tile sums.  16 lanes per block, four
+// blocks in flight per wave, one 64-block tile per workgroup.  Plain global byte loads:
+// every address is validated against the block length before it is dereferenced.
+struct CountArgs {
+  const uint8_t* blocks;
+  const uint64_t* blk_off;
+  uint64_t nblk;
+  uint32_t* agg;        // 3 per block
+  uint64_t* tile_sum;   // 3 per tile
+  uint64_t* stats;
+};
+
+__device__ __forceinline__ uint32_t gb16(const uint8_t* p, uint32_t i) {
+  return (uint32_t(p[i]) << 8) | p[i + 1];
+}
+
+__global__ __launch_bounds__(256) void dec_count_kernel(CountArgs a) {
+  __shared__ uint64_t red[4][3];
+  const uint32_t l = lane_id(), w = threadIdx.x >> 6, grp = l >> 4, sl = l & 15;
+  const uint64_t tile = blockIdx.x;
+  uint64_t tn = 0, tk = 0, tv = 0;
+  uint32_t err = 0;
+#pragma unroll 1
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint64_t b = tile * kTile + w * 16 + r * 4 + grp;
+    uint32_t n = 0;
+    uint64_t K = 0, V = 0;
+    bool ok = true;
+    if (b < a.nblk) {
+      const uint64_t start = a.blk_off[b], end = a.blk_off[b + 1];
+      ok = end >= start && end - start <= 0x7FFFFFF0ull;
+      const uint32_t len = ok ? uint32_t(end - start) : 0u;
+      const uint8_t* p = a.blocks + start;
+      ok = ok && len >= 2;
+      if (ok) {
+        n = gb16(p, len - 2);
+        ok = 2 + 2 * n <= len;
+      }
+      uint32_t data_end = ok ? len - 2 - 2 * n : 0u, fks = 0;
+      if (ok && n) {
+        ok = data_end >= 4;
+        if (ok) {
+          fks = gb16(p, 2);
+          ok = 4 + fks + 8 <= data_end;
+        }
+      }
+      if (!ok) n = 0;
+      for (uint32_t k = sl; k < n; k += 16) {
+        const uint32_t off = gb16(p, data_end + 2 * k);
+        bool e_ok = off + 4 <= data_end;
+        uint32_t ps = 0, ss = 0, vl = 0;
+        if (e_ok) {
+          ps = gb16(p, off);
+          ss = gb16(p, off + 2);
+          e_ok = off + 4 + ss + 10 <= data_end && ps <= fks && ps + ss > 0;
+        }
+        if (e_ok) {
+          vl = gb16(p, off + 12 + ss);
+          e_ok = off + 14 + ss + vl <= data_end;
+        }
+        ok = ok && e_ok;
+        K += ps + ss;
+        V += vl;
+      }
+    }
+    // reduce over the 16 lanes of this block
+#pragma unroll
+    for (uint32_t d = 8; d >= 1; d >>= 1) {
+      K += __shfl_xor(K, d, 16);
+      V += __shfl_xor(V, d, 16);
+      ok = __shfl_xor(int(ok), d, 16) && ok;
+    }
+    if (!ok) {
+      err |= LSMBLK_ERR_MALFORMED;
+      n = 0;
+      K = V = 0;
+    }
+    if (b < a.nblk && sl == 0) {
+      a.agg[3 * b] = n;
+      a.agg[3 * b + 1] = uint32_t(K > 0xFFFFFFFFull ? 0xFFFFFFFFull : K);
+      a.agg[3 * b + 2] = uint32_t(V > 0xFFFFFFFFull ? 0xFFFFFFFFull : V);
+      if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+    }
+    if (sl == 0) {
+      tn += n;
+      tk += K;
+      tv += V;
     }
   }
+  tn = wave_sum(tn);
+  tk = wave_sum(tk);
+  tv = wave_sum(tv);
+  if (l == 0) {
+    red[w][0] = tn;
+    red[w][1] = tk;
+    red[w][2] = tv;
+  }
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
   raise_err(a.stats, err);
+  __syncthreads();
+  if (threadIdx.x < 3)
+    a.tile_sum[3 * tile + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                         red[3][threadIdx.x];
+}
+
+// ---------------------------------------------------------------- decode pass 2: tile scan
+// One workgroup: exclusive scan of the per-tile sums; totals, capacity / overflow checks and
+// the key_off[N] / val_off[N] sentinels.
+struct ScanArgs {
+  const uint64_t* tile_sum;
+  uint64_t* tile_pre;
+  uint64_t ntiles;
+  uint32_t* key_off;
+  uint32_t* val_off;
+  uint64_t entry_cap, key_cap, val_cap;
+  uint64_t* stats;
+};
+
+__global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
+  __shared__ uint64_t part[1024][3];
+  const uint32_t t = threadIdx.x;
+  const uint64_t per = (a.ntiles + 1023) / 1024, lo = t * per, hi = lo + per < a.ntiles ? lo + per : a.ntiles;
+  uint64_t s0 = 0, s1 = 0, s2 = 0;
+  for (uint64_t i = lo; i < hi; ++i) {
+    s0 += a.tile_sum[3 * i];
+    s1 += a.tile_sum[3 * i + 1];
+    s2 += a.tile_sum[3 * i + 2];
+  }
+  part[t][0] = s0;
+  part[t][1] = s1;
+  part[t][2] = s2;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over the 1024 partials
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    uint64_t x0 = 0, x1 = 0, x2 = 0;
+    if (t >= d) {
+      x0 = part[t - d][0];
+      x1 = part[t - d][1];
+      x2 = part[t - d][2];
+    }
+    __syncthreads();
+    part[t][0] += x0;
+    part[t][1] += x1;
+    part[t][2] += x2;
+    __syncthreads();
+  }
+  uint64_t e0 = t ? part[t - 1][0] : 0, e1 = t ? part[t - 1][1] : 0, e2 = t ? part[t - 1][2] : 0;
+  for (uint64_t i = lo; i < hi; ++i) {
+    a.tile_pre[3 * i] = e0;
+    a.tile_pre[3 * i + 1] = e1;
+    a.tile_pre[3 * i + 2] = e2;
+    e0 += a.tile_sum[3 * i];
+    e1 += a.tile_sum[3 * i + 1];
+    e2 += a.tile_sum[3 * i + 2];
+  }
+  if (t == 1023) {
+    const uint64_t N = part[1023][0], K = part[1023][1], V = part[1023][2];
+    a.stats[0] = N;
+    a.stats[1] = K;
+    a.stats[2] = V;
+    uint32_t err = 0;
+    if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+    if (N > a.entry_cap || K > a.key_cap || V > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
+    if (N <= a.entry_cap) {
+      a.key_off[N] = uint32_t(K);
+      a.val_off[N] = uint32_t(V);
+    }
+    if (err) atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)err);
+  }
 }
 
 // ================================================================ encode: plan
@@ -1057,9 +1238,11 @@ struct lsmblk_ctx {
   int device = 0;
   std::mutex mu;
   uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket
-  uint64_t* dec_agg = nullptr;   // 3 granules per block
-  uint64_t* dec_inc = nullptr;
+  uint32_t* dec_agg = nullptr;   // (entries, key bytes, value bytes) per block
   uint64_t dec_cap = 0;
+  uint64_t* tile_sum = nullptr;  // 3 per 64-block tile
+  uint64_t* tile_pre = nullptr;
+  uint64_t tile_cap = 0;
   uint64_t* seg_agg = nullptr;   // 2 granules per segment
   uint64_t* seg_inc = nullptr;
   uint64_t seg_cap = 0;
@@ -1068,13 +1251,19 @@ struct lsmblk_ctx {
   uint32_t* blk_first = nullptr;
   uint64_t rec_cap = 0;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
-  uint32_t poll = 2;             // look-back poll protocol (see gload)
+  uint32_t poll = 0;             // look-back poll protocol (see gload)
+  uint32_t skip = 0;             // decode ablation mask (timing experiments only)
 };
 
 namespace {
 
+// Look-back status granules live in uncached device memory: every poll and publish goes to
+// the coherence point, so no XCD's L2 can hold a stale copy (MI355X L2s are per XCD and not
+// coherent with each other).
+constexpr unsigned kStatusFlags = hipDeviceMallocUncached;
+
 template <typename T>
-int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per) {
+int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per, unsigned flags = 0) {
   if (need <= *cap) return LSMBLK_OK;
   uint64_t nc = need + need / 4 + 1024;
   if (*p) {
@@ -1082,7 +1271,9 @@ int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per) {
     (void)hipFree(*p);
     *p = nullptr;
   }
-  if (hipMalloc(reinterpret_cast<void**>(p), nc * per * sizeof(T)) != hipSuccess) {
+  const hipError_t e = flags ? hipExtMallocWithFlags(reinterpret_cast<void**>(p), nc * per * sizeof(T), flags)
+                            : hipMalloc(reinterpret_cast<void**>(p), nc * per * sizeof(T));
+  if (e != hipSuccess) {
     *cap = 0;
     return LSMBLK_E_NOMEM;
   }
@@ -1096,18 +1287,21 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
   int rc;
   uint64_t cap;
   if (blocks > c->dec_cap) {
-    cap = c->dec_cap;
-    if ((rc = grow(&c->dec_agg, &cap, blocks, 3))) return rc;
-    cap = c->dec_cap;
-    if ((rc = grow(&c->dec_inc, &cap, blocks, 3))) return rc;
-    c->dec_cap = cap;
-    c->epoch = 0;
+    if ((rc = grow(&c->dec_agg, &c->dec_cap, blocks, 3))) return rc;
+  }
+  const uint64_t tiles = (blocks + kTile - 1) / kTile;
+  if (tiles > c->tile_cap) {
+    cap = c->tile_cap;
+    if ((rc = grow(&c->tile_sum, &cap, tiles, 3))) return rc;
+    cap = c->tile_cap;
+    if ((rc = grow(&c->tile_pre, &cap, tiles, 3))) return rc;
+    c->tile_cap = cap;
   }
   if (segs > c->seg_cap) {
     cap = c->seg_cap;
-    if ((rc = grow(&c->seg_agg, &cap, segs, 2))) return rc;
+    if ((rc = grow(&c->seg_agg, &cap, segs, 2, kStatusFlags))) return rc;
     cap = c->seg_cap;
-    if ((rc = grow(&c->seg_inc, &cap, segs, 2))) return rc;
+    if ((rc = grow(&c->seg_inc, &cap, segs, 2, kStatusFlags))) return rc;
     c->seg_cap = cap;
     c->epoch = 0;
   }
@@ -1126,10 +1320,6 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
 // Next look-back epoch; on wrap the status arrays are cleared on the stream.
 int next_epoch(lsmblk_ctx* c, hipStream_t st) {
   if (c->epoch == 0 || c->epoch >= 16383) {
-    if (c->dec_cap) {
-      if (hipMemsetAsync(c->dec_agg, 0, c->dec_cap * 3 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-      if (hipMemsetAsync(c->dec_inc, 0, c->dec_cap * 3 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-    }
     if (c->seg_cap) {
       if (hipMemsetAsync(c->seg_agg, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
       if (hipMemsetAsync(c->seg_inc, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
@@ -1154,7 +1344,7 @@ int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
   if (!c) return LSMBLK_E_NOMEM;
   c->device = device;
   if (const char* e = getenv("LSMBLK_POLL_MODE")) c->poll = uint32_t(atoi(e));
-  if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->counters, 64) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->counters, 2048) != hipSuccess) {
     delete c;
     return LSMBLK_E_HIP;
   }
@@ -1168,13 +1358,23 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipDeviceSynchronize();
   (void)hipFree(c->counters);
   (void)hipFree(c->dec_agg);
-  (void)hipFree(c->dec_inc);
+  (void)hipFree(c->tile_sum);
+  (void)hipFree(c->tile_pre);
   (void)hipFree(c->seg_agg);
   (void)hipFree(c->seg_inc);
   (void)hipFree(c->rec_first);
   (void)hipFree(c->rec_size);
   (void)hipFree(c->blk_first);
   delete c;
+}
+
+int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
+  if (!c) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (key == LSMBLK_DEBUG_POLL_MODE && value <= 2) c->poll = value;
+  else if (key == LSMBLK_DEBUG_DECODE_SKIP) c->skip = value;
+  else return LSMBLK_E_INVAL;
+  return LSMBLK_OK;
 }
 
 int lsmblk_ctx_reserve(lsmblk_ctx* c, uint64_t max_blocks, uint64_t max_entries, uint64_t max_segments) {
@@ -1197,8 +1397,26 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
     hipLaunchKernelGGL(finish_empty_decode, dim3(1), dim3(64), 0, st, out->key_off, out->val_off, out->entry_cap);
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
-  if ((rc = next_epoch(c, st))) return rc;
-  if (hipMemsetAsync(c->counters, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
+  const uint64_t ntiles = (nblk + kTile - 1) / kTile;
+  CountArgs ca;
+  ca.blocks = blocks;
+  ca.blk_off = blk_off;
+  ca.nblk = nblk;
+  ca.agg = c->dec_agg;
+  ca.tile_sum = c->tile_sum;
+  ca.stats = stats;
+  hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
+  ScanArgs sa;
+  sa.tile_sum = c->tile_sum;
+  sa.tile_pre = c->tile_pre;
+  sa.ntiles = ntiles;
+  sa.key_off = out->key_off;
+  sa.val_off = out->val_off;
+  sa.entry_cap = out->entry_cap;
+  sa.key_cap = out->key_cap;
+  sa.val_cap = out->val_cap;
+  sa.stats = stats;
+  hipLaunchKernelGGL(dec_scan_kernel, dim3(1), dim3(1024), 0, st, sa);
   DecodeArgs a;
   a.blocks = blocks;
   a.blk_off = blk_off;
@@ -1212,11 +1430,9 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   a.key_cap = out->key_cap;
   a.val_cap = out->val_cap;
   a.stats = stats;
-  a.ticket = c->counters;
   a.agg = c->dec_agg;
-  a.inc = c->dec_inc;
-  a.tag = c->epoch;
-  a.poll = c->poll;
+  a.tile_pre = c->tile_pre;
+  a.skip = c->skip;
   const uint64_t grid = (nblk + kDecWaves - 1) / kDecWaves;
   hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(grid)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
@@ -1240,7 +1456,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
     return LSMBLK_OK;
   }
   if ((rc = next_epoch(c, st))) return rc;
-  if (hipMemsetAsync(c->counters, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipMemsetAsync(c->counters, 0, 2048, st) != hipSuccess) return LSMBLK_E_HIP;
   PlanArgs p;
   p.keys = in->keys;
   p.key_off = in->key_off;
@@ -1256,7 +1472,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   p.blk_cap = blk_cap;
   p.out_cap = out_cap;
   p.stats = stats;
-  p.ticket = c->counters + 1;
+  p.ticket = c->counters + 256;
   p.agg = c->seg_agg;
   p.inc = c->seg_inc;
   p.tag = c->epoch;
