@@ -51,26 +51,45 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Wave64 inclusive scan / sum of u32 with DPP (row_shr 1,2,4,8 then row_bcast 15 / 31):
+// pure VALU, no ds_bpermute traffic through the LDS crossbar.
+#define LSM_DPP(v, ctrl, rmask) __builtin_amdgcn_update_dpp(0u, (v), (ctrl), (rmask), 0xF, false)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  v += LSM_DPP(v, 0x111, 0xF);  // row_shr:1
+  v += LSM_DPP(v, 0x112, 0xF);  // row_shr:2
+  v += LSM_DPP(v, 0x114, 0xF);  // row_shr:4
+  v += LSM_DPP(v, 0x118, 0xF);  // row_shr:8
+  v += LSM_DPP(v, 0x142, 0xA);  // row_bcast:15 -> rows 1, 3
+  v += LSM_DPP(v, 0x143, 0xC);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+  return __builtin_amdgcn_readlane(wave_incl_scan32(v), 63);
+}
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
-  const uint32_t l = lane_id();
+  if constexpr (sizeof(T) == 4) {
+    return T(wave_incl_scan32(uint32_t(v)));
+  } else {
+    const uint32_t l = lane_id();
 #pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    T t = __shfl_up(v, d, 64);
-    if (l >= d) v += t;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      T t = __shfl_up(v, d, 64);
+      if (l >= d) v += t;
+    }
+    return v;
   }
-  return v;
 }
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return T(__builtin_amdgcn_readlane(wave_incl_scan32(uint32_t(v)), 63));
+  } else {
 #pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+  }
 }
-// Buffer descriptors: raw buffer loads return 0 for every dword that extends past
-// num_records, so each descriptor is based at a 16-B-aligned absolute address and its size
-// rounded up to 16 B.  A 16-B-aligned chunk holding at least one valid byte never crosses a
-// page, so the extra tail bytes are always mapped (their values are never used).
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p16, uint32_t nbytes) {
   const uint32_t n = nbytes >= 0xFFFFFFF0u ? 0xFFFFFFFFu : (nbytes + 15) & ~15u;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p16), (short)0, (int)n, 0x00020000);
@@ -263,6 +282,31 @@ struct alignas(16) DecLds {
   uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
 };
 
+// largest k in [0, n) with tab[k] <= r (tab[0] == 0 <= r)
+__device__ __forceinline__ uint32_t upper_entry(const uint32_t* tab, uint32_t n, uint32_t r) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (tab[mid] <= r) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// 16 bytes at LDS byte offset x (any alignment) via three 8-B reads: ds_read_b64 at a 16-B
+// lane stride is bank-conflict free, ds_read_b32 at that stride is a 4-way conflict.
+__device__ __forceinline__ void lds_read16(const uint8_t* base, uint32_t x, uint32_t (&v)[4]) {
+  const uint2* q = reinterpret_cast<const uint2*>(base + (x & ~7u));
+  const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
+  const uint32_t sh = x & 3;
+  const bool hi = (x & 4) != 0;
+  const uint32_t w0 = hi ? q0.y : q0.x, w1 = hi ? q1.x : q0.y, w2 = hi ? q1.y : q1.x;
+  const uint32_t w3 = hi ? q2.x : q1.y, w4 = hi ? q2.y : q2.x;
+  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+}
+
 struct BlockHdr {
   uint32_t len, n, data_end, fks;
   bool ok;
@@ -331,108 +375,136 @@ __device__ void dec_simple_outputs(const DecodeArgs& a, const Img& im, const Blo
   }
 }
 
+// Store 16 output bytes of a region chunk (region byte rb .. rb+15 at global address gb),
+// masking bytes outside [0, size) or beyond the capacity.
+__device__ __forceinline__ void store_region_chunk(uint8_t* base, uint64_t gb, int32_t rb, uint32_t size,
+                                                   uint64_t cap, const uint32_t (&v)[4]) {
+  uint32_t mask = 0xFFFF;
+  if (rb < 0 || rb + 16 > int32_t(size) || gb + 16 > cap) {
+    mask = 0;
+    for (int i = 0; i < 16; ++i) {
+      const int32_t r = rb + i;
+      if (r >= 0 && r < int32_t(size) && gb + i < cap) mask |= 1u << i;
+    }
+  }
+  store_chunk(base + gb, v, mask);
+}
+
+// Byte-wise value chunk (region boundary or edge chunks).
+__device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead, uint32_t n, int32_t rb,
+                                                 uint32_t V, uint32_t (&v)[4]) {
+  uint32_t k = upper_entry(L.vout, n, rb < 0 ? 0u : uint32_t(rb));
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t r = rb + 4 * d + i;
+      if (r < 0 || r >= int32_t(V)) continue;
+      while (k + 1 < n && int32_t(L.vout[k + 1]) <= r) ++k;
+      word |= uint32_t(L.img[lead + L.vsrc[k] + (uint32_t(r) - L.vout[k])]) << (8 * i);
+    }
+    v[d] = word;
+  }
+}
+
 // Fast path: LDS image + LDS tables, coalesced aligned stores.
 __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
                                  uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V, uint32_t skip) {
   const uint32_t l = lane_id();
   const uint8_t* img = L.img;
-  const LdsImg im{L.img + lead};
-  // per-entry metadata
-  if (!(skip & 8))
-  for (uint32_t k = l; k < h.n; k += 64) {
-    const uint64_t e = E0 + k;
-    if (e < a.entry_cap) {
-      a.ts[e] = im.u64(uint32_t(L.epos[k]) + 4 + L.sfx[k]);
-      a.key_off[e] = uint32_t(K0 + L.kout[k]);
-      a.val_off[e] = uint32_t(V0 + L.vout[k]);
+  const uint32_t n = h.n;
+  // per-entry metadata (entry lanes)
+  if (!(skip & 8)) {
+    for (uint32_t k = l; k < n; k += 64) {
+      const uint64_t e = E0 + k;
+      if (e < a.entry_cap) {
+        const uint32_t x = lead + L.epos[k] + 4 + L.sfx[k];  // big-endian u64 ts after the suffix
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(img) + (x >> 2);
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], x & 3);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w[2], w[1], x & 3);
+        a.ts[e] = __builtin_bswap64((uint64_t(hi) << 32) | lo);
+        a.key_off[e] = uint32_t(K0 + L.kout[k]);
+        a.val_off[e] = uint32_t(V0 + L.vout[k]);
+      }
     }
   }
-  // keys: dwords of the arena covering [K0, K0+K), bytes resolved per byte.
+  // keys: 16-B chunks covering [K0, K0+K).  A key is two pieces, first-key prefix (image
+  // byte 4 + t) and own suffix (image byte epos + 4 + t - p); a dword inside one piece is
+  // one unaligned LDS read, anything else is resolved byte by byte.
   if (!(skip & 2)) {
-    const uint64_t w_begin = K0 >> 2, w_end = (K0 + K + 3) >> 2;
-    for (uint64_t w = w_begin + l; w < w_end; w += 64) {
-      const int64_t r0 = int64_t(w * 4) - int64_t(K0);
-      uint32_t word = 0, mask = 0;
-      // cursor: entry containing max(r0, 0)
-      uint32_t rr = r0 < 0 ? 0u : uint32_t(r0);
-      uint32_t lo = 0, hi = h.n;  // largest k with kout[k] <= rr
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (L.kout[mid] <= rr) lo = mid; else hi = mid;
-      }
-      uint32_t k = lo;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t r = r0 + j;
-        if (r < 0 || r >= int64_t(K)) continue;
-        const uint32_t ru = uint32_t(r);
-        while (k + 1 < h.n && L.kout[k + 1] <= ru) ++k;
-        const uint32_t t = ru - L.kout[k];
-        const uint32_t src = t < L.pfx[k] ? 4 + t : uint32_t(L.epos[k]) + 4 + t - L.pfx[k];
-        word |= uint32_t(img[lead + src]) << (8 * j);
-        mask |= 1u << j;
-      }
-      const uint64_t gb = w * 4;
-      if (mask == 0xF && gb + 4 <= a.key_cap) {
-        *reinterpret_cast<uint32_t*>(a.keys + gb) = word;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if ((mask & (1u << j)) && gb + j < a.key_cap) a.keys[gb + j] = uint8_t(word >> (8 * j));
-      }
-    }
-  }
-  // values: 16-B chunks of the arena covering [V0, V0+V).
-  if (!(skip & 4)) {
-    const uint64_t c_begin = V0 >> 4, c_end = (V0 + V + 15) >> 4;
-    for (uint64_t c = c_begin + l; c < c_end; c += 64) {
-      const int64_t rb = int64_t(c * 16) - int64_t(V0);
-      const uint32_t rr = rb < 0 ? 0u : uint32_t(rb);
-      uint32_t lo = 0, hi = h.n;  // largest k with vout[k] <= rr
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (L.vout[mid] <= rr) lo = mid; else hi = mid;
-      }
-      uint32_t k = lo;
+    const uint32_t offK = uint32_t(K0 & 15);
+    const uint64_t gbase = K0 - offK;
+    const uint32_t nc = (offK + K + 15) >> 4;
+    for (uint32_t j = l; j < nc; j += 64) {
+      const int32_t rb = int32_t(16 * j) - int32_t(offK);
+      uint32_t k = upper_entry(L.kout, n, rb < 0 ? 0u : uint32_t(rb));
       uint32_t v[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const int64_t r0 = rb + 4 * d;
-        const uint32_t r0c = r0 < 0 ? 0u : uint32_t(r0);
-        while (k + 1 < h.n && L.vout[k + 1] <= r0c) ++k;
-        const int64_t endk = L.vout[k + 1];
-        const uint32_t x1 = uint32_t(int64_t(lead) + L.vsrc[k] + (r0 - int64_t(L.vout[k])));
-        uint32_t w1 = lds_dword_at(img, x1);
-        if (r0 + 4 <= endk) {
-          v[d] = w1;
-        } else if (k + 2 <= h.n && r0 + 4 <= int64_t(L.vout[k + 2])) {
-          const uint32_t x2 = uint32_t(int64_t(lead) + L.vsrc[k + 1] + (r0 - int64_t(L.vout[k + 1])));
-          const uint32_t w2 = lds_dword_at(img, x2);
-          const uint32_t nb = uint32_t(endk - r0);  // 1..3 bytes from value k
-          const uint32_t m = (1u << (8 * nb)) - 1;
-          v[d] = (w1 & m) | (w2 & ~m);
+        const int32_t r0 = rb + 4 * d;
+        while (k + 1 < n && int32_t(L.kout[k + 1]) <= r0) ++k;
+        const int32_t t0 = r0 - int32_t(L.kout[k]);
+        const int32_t p = L.pfx[k];
+        if (r0 >= 0 && r0 + 4 <= int32_t(L.kout[k + 1]) && (t0 >= p || t0 + 4 <= p)) {
+          const uint32_t src = t0 >= p ? uint32_t(L.epos[k]) + 4 + uint32_t(t0 - p) : 4u + uint32_t(t0);
+          v[d] = lds_dword_at(img, lead + src);
         } else {
-          uint32_t word = 0;
-          uint32_t kk = k;
+          uint32_t word = 0, kk = k;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int64_t r = r0 + j;
-            if (r < 0 || r >= int64_t(V)) continue;
-            const uint32_t ru = uint32_t(r);
-            while (kk + 1 < h.n && L.vout[kk + 1] <= ru) ++kk;
-            word |= uint32_t(img[lead + L.vsrc[kk] + (ru - L.vout[kk])]) << (8 * j);
+          for (int i = 0; i < 4; ++i) {
+            const int32_t r = r0 + i;
+            if (r < 0 || r >= int32_t(K)) continue;
+            while (kk + 1 < n && int32_t(L.kout[kk + 1]) <= r) ++kk;
+            const uint32_t t = uint32_t(r) - L.kout[kk];
+            const uint32_t src = t < L.pfx[kk] ? 4 + t : uint32_t(L.epos[kk]) + 4 + t - L.pfx[kk];
+            word |= uint32_t(img[lead + src]) << (8 * i);
           }
           v[d] = word;
         }
       }
-      uint32_t mask = 0;
-      const uint64_t gb = c * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int64_t r = rb + j;
-        if (r >= 0 && r < int64_t(V) && gb + j < a.val_cap) mask |= 1u << j;
+      store_region_chunk(a.keys, gbase + 16 * j, rb, K, a.key_cap, v);
+    }
+  }
+  // values, pass 1: chunks lying inside one value (no divergence: others are skipped)
+  if (!(skip & 4)) {
+    const uint32_t offV = uint32_t(V0 & 15);
+    const uint64_t gbase = V0 - offV;
+    const uint32_t nc = (offV + V + 15) >> 4;
+    for (uint32_t j = l; j < nc; j += 64) {
+      const int32_t rb = int32_t(16 * j) - int32_t(offV);
+      if (rb < 0 || rb + 16 > int32_t(V)) continue;
+      const uint32_t k = upper_entry(L.vout, n, uint32_t(rb));
+      if (rb + 16 > int32_t(L.vout[k + 1])) continue;
+      uint32_t v[4];
+      lds_read16(img, lead + L.vsrc[k] + uint32_t(rb) - L.vout[k], v);
+      store_region_chunk(a.vals, gbase + 16 * j, rb, V, a.val_cap, v);
+    }
+    // pass 2: the chunk holding each in-chunk value boundary (owned by its first boundary)
+    // and the two partial edge chunks, byte-wise.
+    const uint32_t jlast = (offV + V - 1) >> 4;
+    for (uint32_t c = 0; c < n + 64; c += 64) {
+      const uint32_t k = c + l;
+      int32_t j = -1;
+      if (k >= 1 && k < n) {
+        const uint32_t bk = L.vout[k] + offV;
+        if ((bk & 15) != 0 && L.vout[k] > 0 && L.vout[k] < V) {
+          const uint32_t jb = bk >> 4;
+          const uint32_t bp = L.vout[k - 1] + offV;
+          const bool prev_same = k >= 2 && (bp & 15) != 0 && L.vout[k - 1] > 0 && (bp >> 4) == jb;
+          const bool edge = (jb == 0 && offV != 0) || (jb == jlast && ((offV + V) & 15) != 0);
+          if (!prev_same && !edge) j = int32_t(jb);
+        }
+      } else if (c == 0 && l == 62 && offV != 0) {
+        j = 0;
+      } else if (c == 0 && l == 63 && ((offV + V) & 15) != 0 && !(jlast == 0 && offV != 0)) {
+        j = int32_t(jlast);
       }
-      store_chunk(a.vals + gb, v, mask);
+      if (j < 0) continue;
+      const int32_t rb = 16 * j - int32_t(offV);
+      uint32_t v[4];
+      value_chunk_slow(L, lead, n, rb, V, v);
+      store_region_chunk(a.vals, gbase + 16 * uint32_t(j), rb, V, a.val_cap, v);
     }
   }
 }
