@@ -1182,16 +1182,29 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     {
       const rsrc_t RK = make_rsrc(a.keys + kb0 - klead, klead + (kb1 - kb0));
       const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
-      for (uint32_t c = l; c < nk; c += 64)
-        *reinterpret_cast<u32x4*>(L.kimg + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(RK, c * 16, 0, 0);
       const rsrc_t RV = make_rsrc(a.vals + vb0 - vlead, vlead + (vb1 - vb0));
       const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
-      for (uint32_t c = l; c < nv; c += 64)
-        *reinterpret_cast<u32x4*>(L.vimg + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(RV, c * 16, 0, 0);
+      // all loads in flight before the LDS writes: <= 2 key and <= 5 value chunks per lane
+      u32x4 kq[2], vq[5];
+#pragma unroll
+      for (uint32_t i = 0; i < 2; ++i)
+        if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, 0);
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i)
+        if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, 0);
+#pragma unroll
+      for (uint32_t i = 0; i < 2; ++i)
+        if (l + 64 * i < nk) *reinterpret_cast<u32x4*>(L.kimg + (l + 64 * i) * 16) = kq[i];
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i)
+        if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.vimg + (l + 64 * i) * 16) = vq[i];
     }
     wave_sync();
     // entry lanes: prefix, positions, non-value bytes and value edge bytes into oimg
     const uint32_t fl = uni(a.key_off[s + 1]) - kb0;  // first key is at kimg[klead]
+    uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
     uint32_t dc = 0;
     for (uint32_t c = 0; c < n; c += 64) {
       const uint32_t k = c + l;
@@ -1206,12 +1219,26 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         if (k != 0) {
           const uint32_t m = fl < kl ? fl : kl;
           p = m;
-          for (uint32_t q = 0; q < m; q += 4) {
+          bool done = false;
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) {
+            if (!done && 4 * i < m) {
+              const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
+              if (x) {
+                const uint32_t z = 4 * i + (__builtin_ctz(x) >> 3);
+                p = z < m ? z : m;
+                done = true;
+              }
+            } else {
+              done = true;
+            }
+          }
+          for (uint32_t q = 16; !done && q < m; q += 4) {
             const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
             if (x) {
               const uint32_t z = q + (__builtin_ctz(x) >> 3);
               p = z < m ? z : m;
-              break;
+              done = true;
             }
           }
         }
@@ -1250,43 +1277,53 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     // offsets table + entry count (u16 BE, `as u16`)
     for (uint32_t k = l; k < n; k += 64) lds_be(L.oimg + olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
     if (l == 0) lds_be(L.oimg + olead + data_len + 2 * n, n & 0xFFFF, 2);
-    // value bulk: whole image dwords that lie inside one value
+    // value bulk: 16-B image chunks; a chunk inside one value is one 16-B LDS read + one
+    // ds_write_b128, otherwise its dwords that lie inside a value are copied one by one
+    // (the remaining value bytes were written by the entry lanes above).
     {
-      const uint32_t nw = (olead + uint32_t(size) + 3) >> 2;
-      uint32_t k = 0;
-      bool first_iter = true;
-      for (uint32_t W = l; W < nw; W += 64) {
-        const int32_t x = int32_t(4 * W) - int32_t(olead);
-        if (first_iter) {
-          uint32_t lo = 0, hi = n;
-          const int32_t xc = x < 0 ? 0 : x;
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (int32_t(L.vdst[mid]) <= xc) lo = mid; else hi = mid;
-          }
-          k = lo;
-          first_iter = false;
+      const uint32_t nc = (olead + uint32_t(size) + 15) >> 4;
+      for (uint32_t c = l; c < nc; c += 64) {
+        const int32_t x = int32_t(16 * c) - int32_t(olead);
+        const int32_t xc = x < 0 ? 0 : x;
+        uint32_t lo = 0, hi = n;  // largest k with vdst[k] <= xc
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (int32_t(L.vdst[mid]) <= xc) lo = mid; else hi = mid;
         }
-        while (k + 1 < n && int32_t(L.vdst[k + 1]) <= x) ++k;
-        if (x >= int32_t(L.vdst[k]) && x + 4 <= int32_t(L.vend[k])) {
-          const uint32_t src = L.vsrc[k] + uint32_t(x - int32_t(L.vdst[k]));
-          reinterpret_cast<uint32_t*>(L.oimg)[W] = lds_dword_at(L.vimg, src);
+        uint32_t k = lo;
+        if (x >= int32_t(L.vdst[k]) && x + 16 <= int32_t(L.vend[k])) {
+          uint32_t v[4];
+          lds_read16(L.vimg, L.vsrc[k] + uint32_t(x - int32_t(L.vdst[k])), v);
+          u32x4 q = {v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<u32x4*>(L.oimg + 16 * c) = q;
+        } else {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const int32_t xd = x + 4 * d;
+            while (k + 1 < n && int32_t(L.vdst[k + 1]) <= xd) ++k;
+            if (xd >= int32_t(L.vdst[k]) && xd + 4 <= int32_t(L.vend[k]))
+              reinterpret_cast<uint32_t*>(L.oimg)[4 * c + d] =
+                  lds_dword_at(L.vimg, L.vsrc[k] + uint32_t(xd - int32_t(L.vdst[k])));
+          }
         }
       }
     }
     wave_sync();
-    // flush the image: 16-B chunks, partial chunks at the ends byte-wise
+    // flush the image: 16-B chunks; only the two end chunks can be partial
     {
       uint8_t* gbase = a.out + (O - olead);
       const uint32_t nc = (olead + uint32_t(size) + 15) >> 4;
+      const uint64_t room = a.out_cap - (O - olead);  // bytes of out from gbase on
       for (uint32_t c = l; c < nc; c += 64) {
         const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + c * 16);
         const uint32_t v[4] = {q.x, q.y, q.z, q.w};
-        uint32_t mask = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const uint32_t x = c * 16 + j;
-          if (x >= olead && x < olead + size && (O - olead) + x < a.out_cap) mask |= 1u << j;
+        uint32_t mask = 0xFFFF;
+        if (16 * c < olead || 16 * c + 16 > olead + size || 16 * c + 16 > room) {
+          mask = 0;
+          for (int j = 0; j < 16; ++j) {
+            const uint32_t xj = c * 16 + j;
+            if (xj >= olead && xj < olead + size && xj < room) mask |= 1u << j;
+          }
         }
         store_chunk(gbase + c * 16, v, mask);
       }
