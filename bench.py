@@ -163,20 +163,26 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max, ok_all = float(tt[0].item()), tt[1].item() == 0.0
 
+    # per-kernel durations: a short profiling pass after the timed region, HIP events recorded
+    # by liblsmblk.so on the launch stream around every kernel (diagnostics only, not timed)
+    kms = kernel_times(ctx, step, dev, reps=3)
+
     result = None
     if rank == 0:
         value = world * E * args.steps / t_max / GiB
         ms_per_step = t_max / args.steps * 1e3
-        # dominant kernel's roofline: algorithmic bytes per launch / launch duration
-        dec_bytes, enc_bytes = E + D + 8 * (nblk + 1), D + E + 8 * (nblk + 1)
-        dom_name, dom_bytes, dom_ms = ("decode", dec_bytes, dec_ms) if dec_ms >= enc_ms else ("encode", enc_bytes, enc_ms)
-        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+        # algorithmic bytes per launch of each kernel (DESIGN.md "Kernels")
+        hdr = 8 * (nblk + 1) + 2 * nblk + 8 * n          # count: blk_off, trailers, offsets + entry headers
+        algo = {"dec_count": hdr, "dec_scan": 0, "decode": E + D + 8 * (nblk + 1) + 12 * nblk,
+                "plan": 8 * (n + 1) + K + 8 * nblk, "emit": D + E + 16 * (nblk + 1)}
+        dom = max(kms, key=lambda k: kms[k])
+        achieved = algo[dom] / (kms[dom] * 1e-3) / 1e9
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             if tj.get("workload") == cfg and tj.get("blocks") == nblk:
-                traffic = tj.get(dom_name)
+                traffic = tj.get("bytes_per_launch", {}).get(dom)
         result = {
             "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -188,11 +194,12 @@ def main():
                        "decoded_bytes_per_gpu": D, "block_size": bs, "segments_per_gpu": len(seg) - 1,
                        "parallelism": f"block-sharded x{world} (no data-path collective)",
                        "roundtrip_bit_exact": bool(ok_all)},
-            "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
-                         "decode_ms": round(dec_ms, 4), "encode_ms": round(enc_ms, 4),
-                         "step_algorithmic_bytes": dec_bytes + enc_bytes},
+                         "bytes_per_launch": algo[dom], "launch_ms": round(kms[dom], 4),
+                         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
+                         "stage_ms": {"decode": round(dec_ms, 4), "encode": round(enc_ms, 4)},
+                         "step_algorithmic_bytes": algo["decode"] + algo["emit"]},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -206,6 +213,24 @@ def main():
     if result is not None:
         print(json.dumps(result), flush=True)
     return 0 if ok_all else 1
+
+
+KERNELS = ["dec_count", "dec_scan", "decode", "plan", "emit"]
+
+
+def kernel_times(ctx, step, dev, reps=3):
+    import ctypes
+    check(lib().lsmblk_debug_set(ctx, 2, 1))
+    acc = {k: [] for k in KERNELS}
+    buf = (ctypes.c_float * 5)()
+    for _ in range(reps):
+        step()
+        torch.cuda.synchronize(dev)
+        check(lib().lsmblk_ctx_kernel_times(ctx, buf))
+        for i, k in enumerate(KERNELS):
+            acc[k].append(buf[i])
+    check(lib().lsmblk_debug_set(ctx, 2, 0))
+    return {k: float(np.mean(v)) for k, v in acc.items()}
 
 
 def ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream):

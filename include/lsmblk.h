@@ -151,7 +151,13 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
  *   LSMBLK_DEBUG_DECODE_SKIP  decode ablation mask: 1 look-back, 2 keys, 4 values, 8 metadata */
 #define LSMBLK_DEBUG_POLL_MODE 0
 #define LSMBLK_DEBUG_DECODE_SKIP 1
+#define LSMBLK_DEBUG_KERNEL_TIMING 2 /* 1: record HIP events around every kernel launch */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
+/* Durations (ms) of the kernels of the last timed decode / encode call on this context:
+ * [0] dec_count [1] dec_scan [2] decode [3] plan [4] emit; -1 if not recorded.  Waits for
+ * the recorded events. */
+#define LSMBLK_KERNELS 5
+int lsmblk_ctx_kernel_times(lsmblk_ctx* ctx, float* ms);
 
 /* Decode nblk blocks (block b = blocks[blk_off[b] .. blk_off[b+1]), blk_off u64[nblk+1])
  * into the SoA stream `out` (outputs must be 16-byte aligned).  Asynchronous: completion

@@ -1362,6 +1362,9 @@ struct lsmblk_ctx {
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
   uint32_t skip = 0;             // decode ablation mask (timing experiments only)
+  bool timing = false;           // record HIP events around every kernel (diagnostics)
+  hipEvent_t ev[8] = {};         // decode: 0 count 1 scan 2 decode 3 | encode: 4 plan 5 emit 6
+  bool dec_timed = false, enc_timed = false;
 };
 
 namespace {
@@ -1474,15 +1477,47 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->rec_first);
   (void)hipFree(c->rec_size);
   (void)hipFree(c->blk_first);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 
 int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
   if (!c) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (key == LSMBLK_DEBUG_POLL_MODE && value <= 2) c->poll = value;
-  else if (key == LSMBLK_DEBUG_DECODE_SKIP) c->skip = value;
-  else return LSMBLK_E_INVAL;
+  if (key == LSMBLK_DEBUG_POLL_MODE && value <= 2) {
+    c->poll = value;
+  } else if (key == LSMBLK_DEBUG_DECODE_SKIP) {
+    c->skip = value;
+  } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
+    if (value && !c->ev[0]) {
+      if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+      for (auto& e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) return LSMBLK_E_HIP;
+    }
+    c->timing = value != 0;
+  } else {
+    return LSMBLK_E_INVAL;
+  }
+  return LSMBLK_OK;
+}
+
+int lsmblk_ctx_kernel_times(lsmblk_ctx* c, float* ms) {
+  if (!c || !ms) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (int i = 0; i < LSMBLK_KERNELS; ++i) ms[i] = -1.f;
+  if (!c->ev[0]) return LSMBLK_OK;
+  auto span = [&](int a, int b, float* out) -> int {
+    if (hipEventSynchronize(c->ev[b]) != hipSuccess) return LSMBLK_E_HIP;
+    return hipEventElapsedTime(out, c->ev[a], c->ev[b]) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  };
+  int rc = LSMBLK_OK;
+  if (c->dec_timed) {
+    if ((rc = span(0, 1, &ms[0])) || (rc = span(1, 2, &ms[1])) || (rc = span(2, 3, &ms[2]))) return rc;
+  }
+  if (c->enc_timed) {
+    if ((rc = span(4, 5, &ms[3])) || (rc = span(5, 6, &ms[4]))) return rc;
+  }
   return LSMBLK_OK;
 }
 
@@ -1514,7 +1549,10 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   ca.agg = c->dec_agg;
   ca.tile_sum = c->tile_sum;
   ca.stats = stats;
+  c->dec_timed = c->timing;
+  if (c->timing) (void)hipEventRecord(c->ev[0], st);
   hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
+  if (c->timing) (void)hipEventRecord(c->ev[1], st);
   ScanArgs sa;
   sa.tile_sum = c->tile_sum;
   sa.tile_pre = c->tile_pre;
@@ -1526,6 +1564,7 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   sa.val_cap = out->val_cap;
   sa.stats = stats;
   hipLaunchKernelGGL(dec_scan_kernel, dim3(1), dim3(1024), 0, st, sa);
+  if (c->timing) (void)hipEventRecord(c->ev[2], st);
   DecodeArgs a;
   a.blocks = blocks;
   a.blk_off = blk_off;
@@ -1544,6 +1583,7 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   a.skip = c->skip;
   const uint64_t grid = (nblk + kDecWaves - 1) / kDecWaves;
   hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(grid)), dim3(256), 0, st, a);
+  if (c->timing) (void)hipEventRecord(c->ev[3], st);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1586,7 +1626,10 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   p.inc = c->seg_inc;
   p.tag = c->epoch;
   p.poll = c->poll;
+  c->enc_timed = c->timing;
+  if (c->timing) (void)hipEventRecord(c->ev[4], st);
   hipLaunchKernelGGL(plan_kernel, dim3((nseg + kPlanWaves - 1) / kPlanWaves), dim3(256), 0, st, p);
+  if (c->timing) (void)hipEventRecord(c->ev[5], st);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   EmitArgs e;
   e.keys = in->keys;
@@ -1605,6 +1648,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   const uint32_t grid = uint32_t(cus) * 3;
   hipLaunchKernelGGL(emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  if (c->timing) (void)hipEventRecord(c->ev[6], st);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 

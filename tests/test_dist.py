@@ -1,0 +1,67 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the sharding helpers used for N>1."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lsm_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # block-parallel: timing max-reduce
+        t = shard.max_over_ranks(1.0 + rank)
+        # compaction-shaped: each rank holds an overlapping sorted run of block first keys
+        first_keys = [b"key%06d" % i for i in range(rank * 500, rank * 500 + 1500, 3)]
+        spl = shard.exchange_splitters(first_keys, samples=32)
+        q.put((rank, t, spl))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_block_ranges_cover():
+    for n in (0, 1, 7, 1 << 20):
+        for w in (1, 2, 3, 8):
+            r = shard.block_ranges(n, w)
+            assert r[0][0] == 0 and r[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+            assert max(h - l for l, h in r) - min(h - l for l, h in r) <= 1
+
+
+def test_choose_splitters_and_owner():
+    keys = [b"%04d" % i for i in range(100)]
+    spl = shard.choose_splitters(keys, 4)
+    assert spl == [b"0025", b"0050", b"0075"]
+    assert [shard.owner_of(k, spl) for k in (b"0000", b"0025", b"0049", b"0099")] == [0, 1, 1, 3]
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_exchange():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    (r0, t0, s0), (r1, t1, s1) = res
+    assert t0 == t1 == 2.0
+    assert s0 == s1 and len(s0) == 1
+    # the splitter lies inside the union of both runs
+    assert b"key000000" < s0[0] < b"key002000"

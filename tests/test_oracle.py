@@ -73,9 +73,11 @@ def test_generate_block_known_answer():
     enc = generate_block(O.Builder).finish()
     assert len(enc) == 3486
     assert zlib.crc32(enc) == 0x8C8796D4
-    assert enc[:33] == bytes.fromhex("0000" "0007") + b"key_000" + bytes(8) + bytes.fromhex("0010") + \
+    # entry 0: prefix 0, suffix 7, "key_000", ts 0 (8 B), value_len 16, "value_0000000000"
+    assert enc[:37] == bytes.fromhex("0000" "0007") + b"key_000" + bytes(8) + bytes.fromhex("0010") + \
         b"value_0000000000"
-    assert enc[33:37] == bytes.fromhex("0006") + bytes.fromhex("0001")  # entry 1: prefix 6, suffix 1
+    assert enc[37:42] == bytes.fromhex("0006") + bytes.fromhex("0001") + b"5"  # entry 1: "key_00" + "5"
+    assert enc[-2:] == bytes.fromhex("0064")  # 100 entries
 
 
 def test_block_iterator_expectations():  # :91-117 (corrected iterator)
