@@ -130,6 +130,15 @@ def main():
             ev[2].record(stream)
 
     if args.ablate is not None:
+        if args.ablate >= 16:  # encode-side masks: per-kernel times with the mask applied
+            res = {}
+            for mask in (0, 16, 32, 64, 112, 128, 240):
+                check(lib().lsmblk_debug_set(ctx, 1, mask))
+                step()
+                res[mask] = kernel_times(ctx, step, dev, reps=2)["emit"]
+            check(lib().lsmblk_debug_set(ctx, 1, 0))
+            print(json.dumps({"ablation_emit_ms_by_skip_mask": res}), flush=True)
+            return 0
         return ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream)
     for _ in range(args.warmup):
         step()

@@ -63,6 +63,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
   v += LSM_DPP(v, 0x143, 0xC);  // row_bcast:31 -> rows 2, 3
   return v;
 }
+__device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
+  v = max(v, LSM_DPP(v, 0x111, 0xF));
+  v = max(v, LSM_DPP(v, 0x112, 0xF));
+  v = max(v, LSM_DPP(v, 0x114, 0xF));
+  v = max(v, LSM_DPP(v, 0x118, 0xF));
+  v = max(v, LSM_DPP(v, 0x142, 0xA));
+  v = max(v, LSM_DPP(v, 0x143, 0xC));
+  return v;
+}
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   return __builtin_amdgcn_readlane(wave_incl_scan32(v), 63);
 }
@@ -276,10 +285,13 @@ constexpr uint32_t kDecWaves = 4;
 constexpr uint32_t kDecImg = 4352;  // staged block bytes per wave (4 KiB blocks + lead + slack)
 constexpr uint32_t kDecMaxE = 128;  // entries with LDS tables (fast path)
 
+constexpr uint32_t kDecChunks = kDecImg / 16 + 2;  // 16-B output chunks of a region (V, K <= len)
+
 struct alignas(16) DecLds {
   uint8_t img[kDecImg];
   uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE], vsrc[kDecMaxE];
   uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
+  uint32_t kcent[kDecChunks], vcent[kDecChunks];  // region chunk -> last entry starting at/before it
 };
 
 // largest k in [0, n) with tab[k] <= r (tab[0] == 0 <= r)
@@ -429,6 +441,23 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
       }
     }
   }
+  // chunk -> entry tables: entry k marks the first region chunk starting at or after its
+  // first byte; a wave max-scan over the chunk lanes then yields, for every chunk, the last
+  // entry starting at or before it (no per-chunk binary search)
+  const uint32_t offKc = uint32_t(K0 & 15), offVc = uint32_t(V0 & 15);
+  const uint32_t nck = (offKc + K + 15) >> 4, ncv = (offVc + V + 15) >> 4;
+  const bool ktab = nck <= kDecChunks;
+  for (uint32_t j = l; j < ncv; j += 64) L.vcent[j] = 0;
+  if (ktab)
+    for (uint32_t j = l; j < nck; j += 64) L.kcent[j] = 0;
+  wave_sync();
+  for (uint32_t k = l; k < n; k += 64) {
+    const uint32_t jv = (L.vout[k] + offVc + 15) >> 4;
+    if (jv < ncv && L.vout[k + 1] > L.vout[k]) atomicMax(&L.vcent[jv], k);
+    const uint32_t jk = (L.kout[k] + offKc + 15) >> 4;
+    if (ktab && jk < nck) atomicMax(&L.kcent[jk], k);
+  }
+  wave_sync();
   // keys: 16-B chunks covering [K0, K0+K).  A key is two pieces, first-key prefix (image
   // byte 4 + t) and own suffix (image byte epos + 4 + t - p); a dword inside one piece is
   // one unaligned LDS read, anything else is resolved byte by byte.
@@ -436,9 +465,17 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
     const uint32_t offK = uint32_t(K0 & 15);
     const uint64_t gbase = K0 - offK;
     const uint32_t nc = (offK + K + 15) >> 4;
-    for (uint32_t j = l; j < nc; j += 64) {
+    uint32_t carry = 0;
+    for (uint32_t j0 = 0; j0 < nc; j0 += 64) {
+      const uint32_t j = j0 + l;
+      uint32_t k;
+      if (ktab) {
+        k = max(wave_incl_max32(j < nc ? L.kcent[j] : 0u), carry);
+        carry = __builtin_amdgcn_readlane(k, 63);
+      }
+      if (j >= nc) continue;
       const int32_t rb = int32_t(16 * j) - int32_t(offK);
-      uint32_t k = upper_entry(L.kout, n, rb < 0 ? 0u : uint32_t(rb));
+      if (!ktab) k = upper_entry(L.kout, n, rb < 0 ? 0u : uint32_t(rb));
       uint32_t v[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -471,11 +508,15 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
     const uint32_t offV = uint32_t(V0 & 15);
     const uint64_t gbase = V0 - offV;
     const uint32_t nc = (offV + V + 15) >> 4;
-    for (uint32_t j = l; j < nc; j += 64) {
+    uint32_t carry = 0;
+    for (uint32_t j0 = 0; j0 < nc; j0 += 64) {
+      const uint32_t j = j0 + l;
+      const uint32_t k = max(wave_incl_max32(j < nc ? L.vcent[j] : 0u), carry);
+      carry = __builtin_amdgcn_readlane(k, 63);
+      if (j >= nc) continue;
       const int32_t rb = int32_t(16 * j) - int32_t(offV);
       if (rb < 0 || rb + 16 > int32_t(V)) continue;
-      const uint32_t k = upper_entry(L.vout, n, uint32_t(rb));
-      if (rb + 16 > int32_t(L.vout[k + 1])) continue;
+      if (rb < int32_t(L.vout[k]) || rb + 16 > int32_t(L.vout[k + 1])) continue;
       uint32_t v[4];
       lds_read16(img, lead + L.vsrc[k] + uint32_t(rb) - L.vout[k], v);
       store_region_chunk(a.vals, gbase + 16 * j, rb, V, a.val_cap, v);
@@ -1048,6 +1089,8 @@ struct EmitArgs {
   uint64_t out_cap, blk_cap;
   uint64_t n;  // entries; arena sizes are key_off[n], val_off[n]
   uint64_t* stats;
+  uint32_t skip;  // ablation mask (timing experiments only): 16 entry-lane byte writes,
+                  // 32 bulk value copy, 64 flush, 128 LCP
 };
 
 constexpr uint32_t kEmitWaves = 4;
@@ -1060,6 +1103,7 @@ struct alignas(16) EmitLds {
   uint8_t kimg[kEmitKCap];
   uint8_t vimg[kEmitVCap];
   uint8_t oimg[kEmitOCap];
+  uint32_t cent[kEmitOCap / 16 + 1];  // image chunk -> last entry whose value starts at or before it
   uint32_t epos[kEmitMaxE];
   uint32_t vdst[kEmitMaxE + 1];
   uint32_t vend[kEmitMaxE];
@@ -1149,6 +1193,19 @@ __device__ void emit_simple(const EmitArgs& a, const GlbBytes& KB, const GlbByte
   }
 }
 
+// Block metadata of one emit unit: two levels of dependent loads (block tables, then the
+// entry offsets of its first/last entry).
+struct EmitMeta {
+  uint64_t bi;
+  uint32_t s, e, n;
+  uint64_t O, size;
+  uint32_t kb0, kb1, vb0, vb1;
+};
+
+// Persistent waves, software-pipelined one block ahead: while block i is processed, the
+// metadata, the key/value staging loads and the first 64 entries' offsets/ts of block i+1
+// are already in flight (the wave is latency-bound otherwise: ~3 dependent global round
+// trips per block).  LDS caps occupancy at 3 waves/SIMD, so the prefetch registers are free.
 __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
   __shared__ EmitLds lds[kEmitWaves];
   EmitLds& L = lds[threadIdx.x >> 6];
@@ -1157,41 +1214,89 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
   const uint64_t nwaves = uint64_t(gridDim.x) * kEmitWaves;
   uint32_t err = 0;
   const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
-  for (uint64_t bi = uint64_t(blockIdx.x) * kEmitWaves + (threadIdx.x >> 6); bi < nblk; bi += nwaves) {
-    const uint64_t biu = uni64(bi);
-    if (biu + 1 >= a.blk_cap) break;  // blk_off not materialized (capacity error raised by plan)
-    const uint32_t s = uni(a.blk_first[biu]), e = uni(a.blk_first[biu + 1]);
-    const uint32_t n = e - s;
-    const uint64_t O = uni64(a.blk_off[biu]);
-    const uint64_t size = uni64(a.blk_off[biu + 1]) - O;
-    const uint32_t kb0 = uni(a.key_off[s]), kb1 = uni(a.key_off[e]);
-    const uint32_t vb0 = uni(a.val_off[s]), vb1 = uni(a.val_off[e]);
+  const uint64_t lim = nblk < a.blk_cap ? nblk : (a.blk_cap ? a.blk_cap - 1 : 0);  // blk_off[bi+1] must exist
+
+  auto meta1 = [&](uint64_t bi, EmitMeta& m) {
+    m.bi = bi;
+    m.s = uni(a.blk_first[bi]);
+    m.e = uni(a.blk_first[bi + 1]);
+    m.n = m.e - m.s;
+    m.O = uni64(a.blk_off[bi]);
+    m.size = uni64(a.blk_off[bi + 1]) - m.O;
+  };
+  auto meta2 = [&](EmitMeta& m) {
+    m.kb0 = uni(a.key_off[m.s]);
+    m.kb1 = uni(a.key_off[m.e]);
+    m.vb0 = uni(a.val_off[m.s]);
+    m.vb1 = uni(a.val_off[m.e]);
+  };
+  auto is_fast = [&](const EmitMeta& m) {
+    const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
+    return m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
+           vlead + (m.vb1 - m.vb0) + 8 <= kEmitVCap && uint32_t(m.O & 15) + m.size + 8 <= kEmitOCap;
+  };
+  u32x4 kq[2], vq[5];
+  uint32_t pf_ko0 = 0, pf_ko1 = 0, pf_vo0 = 0, pf_vo1 = 0;
+  uint64_t pf_ts = 0;
+  auto issue = [&](const EmitMeta& m) {  // staging + first-chunk entry loads of block m
+    const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
+    const rsrc_t RK = make_rsrc(a.keys + m.kb0 - klead, klead + (m.kb1 - m.kb0));
+    const uint32_t nk = (klead + (m.kb1 - m.kb0) + 15) >> 4;
+    const rsrc_t RV = make_rsrc(a.vals + m.vb0 - vlead, vlead + (m.vb1 - m.vb0));
+    const uint32_t nv = (vlead + (m.vb1 - m.vb0) + 15) >> 4;
+#pragma unroll
+    for (uint32_t i = 0; i < 2; ++i)
+      if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, 0);
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, 0);
+    if (l < m.n) {
+      pf_ko0 = a.key_off[m.s + l];
+      pf_ko1 = a.key_off[m.s + l + 1];
+      pf_vo0 = a.val_off[m.s + l];
+      pf_vo1 = a.val_off[m.s + l + 1];
+      pf_ts = a.ts[m.s + l];
+    }
+  };
+
+  uint64_t bi0 = uint64_t(blockIdx.x) * kEmitWaves + (threadIdx.x >> 6);
+  if (bi0 >= lim) {
+    raise_err(a.stats, err);
+    return;
+  }
+  EmitMeta cur;
+  meta1(uni64(bi0), cur);
+  meta2(cur);
+  bool cur_fast = is_fast(cur);
+  if (cur_fast) issue(cur);
+  for (;;) {
+    const uint64_t bn = cur.bi + nwaves;
+    const bool has_next = bn < lim;
+    EmitMeta nxt;
+    if (has_next) meta1(uni64(bn), nxt);  // level-1 of the next block, in flight now
+    const uint32_t s = cur.s, n = cur.n;
+    const uint64_t O = cur.O, size = cur.size;
+    const uint32_t kb0 = cur.kb0, kb1 = cur.kb1, vb0 = cur.vb0, vb1 = cur.vb1;
     const uint32_t klead = uint32_t((kaddr + kb0) & 15), vlead = uint32_t((vaddr + vb0) & 15);
     const uint32_t olead = uint32_t(O & 15);
-    const bool fast = n <= kEmitMaxE && klead + (kb1 - kb0) + 8 <= kEmitKCap &&
-                      vlead + (vb1 - vb0) + 8 <= kEmitVCap && olead + size + 8 <= kEmitOCap;
-    if (!fast) {
+    bool nxt_fast = false;
+    if (!cur_fast) {
       const uint32_t kg = uint32_t(kaddr & 15), vg = uint32_t(vaddr & 15);
       const uint32_t kt = uni(a.key_off[a.n]), vt = uni(a.val_off[a.n]);
       const GlbBytes KB{make_rsrc(a.keys - kg, kg + kt), kg};
       const GlbBytes VB{make_rsrc(a.vals - vg, vg + vt), vg};
       emit_simple(a, KB, VB, s, n, O, size, err);
+      if (!has_next) break;
+      meta2(nxt);
+      nxt_fast = is_fast(nxt);
+      if (nxt_fast) issue(nxt);
+      cur = nxt;
+      cur_fast = nxt_fast;
       continue;
     }
-    // stage keys and values of the block
-    {
-      const rsrc_t RK = make_rsrc(a.keys + kb0 - klead, klead + (kb1 - kb0));
+    {  // land the staged keys / values of the current block
       const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
-      const rsrc_t RV = make_rsrc(a.vals + vb0 - vlead, vlead + (vb1 - vb0));
       const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
-      // all loads in flight before the LDS writes: <= 2 key and <= 5 value chunks per lane
-      u32x4 kq[2], vq[5];
-#pragma unroll
-      for (uint32_t i = 0; i < 2; ++i)
-        if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, 0);
-#pragma unroll
-      for (uint32_t i = 0; i < 5; ++i)
-        if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, 0);
 #pragma unroll
       for (uint32_t i = 0; i < 2; ++i)
         if (l + 64 * i < nk) *reinterpret_cast<u32x4*>(L.kimg + (l + 64 * i) * 16) = kq[i];
@@ -1199,9 +1304,12 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       for (uint32_t i = 0; i < 5; ++i)
         if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.vimg + (l + 64 * i) * 16) = vq[i];
     }
+    if (has_next) meta2(nxt);  // level-2 of the next block
     wave_sync();
     // entry lanes: prefix, positions, non-value bytes and value edge bytes into oimg
     const uint32_t fl = uni(a.key_off[s + 1]) - kb0;  // first key is at kimg[klead]
+    const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of this block
+    for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
     uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
 #pragma unroll
     for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
@@ -1211,12 +1319,18 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
       uint64_t tsv = 0;
       if (k < n) {
-        kp = a.key_off[s + k] - kb0;
-        kl = a.key_off[s + k + 1] - kb0 - kp;
-        vp = a.val_off[s + k] - vb0;
-        vl = a.val_off[s + k + 1] - vb0 - vp;
-        tsv = a.ts[s + k];
-        if (k != 0) {
+        uint32_t ko0, ko1, vo0, vo1;
+        if (c == 0) {  // prefetched one block ahead
+          ko0 = pf_ko0; ko1 = pf_ko1; vo0 = pf_vo0; vo1 = pf_vo1; tsv = pf_ts;
+        } else {
+          ko0 = a.key_off[s + k]; ko1 = a.key_off[s + k + 1];
+          vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1]; tsv = a.ts[s + k];
+        }
+        kp = ko0 - kb0;
+        kl = ko1 - ko0;
+        vp = vo0 - vb0;
+        vl = vo1 - vo0;
+        if (k != 0 && !(a.skip & 128)) {
           const uint32_t m = fl < kl ? fl : kl;
           p = m;
           bool done = false;
@@ -1247,7 +1361,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       const uint32_t incl = wave_incl_scan<uint32_t>(dg);
       const uint32_t pos = dc + incl - dg;
       dc += __shfl(incl, 63, 64);
-      if (k < n) {
+      if (k < n && !(a.skip & 16)) {
         const uint32_t sfx = kl - p;
         uint8_t* o = L.oimg + olead + pos;
         lds_be(o, p & 0xFFFF, 2);
@@ -1265,10 +1379,16 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
           for (uint32_t x = A; x < a4; ++x) L.oimg[x] = vs[x - A];
           for (uint32_t x = b4; x < Bv; ++x) L.oimg[x] = vs[x - A];
         }
+      }
+      if (k < n) {
+        const uint32_t sfx = kl - p;
         L.epos[k] = pos;
         L.vdst[k] = pos + 14 + sfx;
         L.vend[k] = pos + 14 + sfx + vl;
         L.vsrc[k] = vlead + vp;
+        // first image chunk whose start (16j - olead) is >= this value's start
+        const uint32_t j0 = (olead + pos + 14 + sfx + 15) >> 4;
+        if (j0 < ncs) atomicMax(&L.cent[j0], k);
       }
     }
     const uint32_t data_len = dc;
@@ -1277,40 +1397,56 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     // offsets table + entry count (u16 BE, `as u16`)
     for (uint32_t k = l; k < n; k += 64) lds_be(L.oimg + olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
     if (l == 0) lds_be(L.oimg + olead + data_len + 2 * n, n & 0xFFFF, 2);
+    if (has_next) {  // next block's staging loads overlap this block's bulk copy + flush
+      nxt_fast = is_fast(nxt);
+      if (nxt_fast) issue(nxt);
+    }
     // value bulk: 16-B image chunks; a chunk inside one value is one 16-B LDS read + one
     // ds_write_b128, otherwise its dwords that lie inside a value are copied one by one
     // (the remaining value bytes were written by the entry lanes above).
-    {
-      const uint32_t nc = (olead + uint32_t(size) + 15) >> 4;
-      for (uint32_t c = l; c < nc; c += 64) {
+    if (!(a.skip & 32)) {
+      // pass 1: chunks lying inside one value (others skipped: no divergence)
+      uint32_t carry = 0;
+      for (uint32_t c0 = 0; c0 < ncs; c0 += 64) {
+        const uint32_t c = c0 + l;
+        uint32_t k = wave_incl_max32(c < ncs ? L.cent[c] : 0u);
+        k = max(k, carry);
+        carry = __builtin_amdgcn_readlane(k, 63);
+        if (c >= ncs) continue;
         const int32_t x = int32_t(16 * c) - int32_t(olead);
-        const int32_t xc = x < 0 ? 0 : x;
-        uint32_t lo = 0, hi = n;  // largest k with vdst[k] <= xc
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (int32_t(L.vdst[mid]) <= xc) lo = mid; else hi = mid;
-        }
-        uint32_t k = lo;
         if (x >= int32_t(L.vdst[k]) && x + 16 <= int32_t(L.vend[k])) {
           uint32_t v[4];
           lds_read16(L.vimg, L.vsrc[k] + uint32_t(x - int32_t(L.vdst[k])), v);
           u32x4 q = {v[0], v[1], v[2], v[3]};
           *reinterpret_cast<u32x4*>(L.oimg + 16 * c) = q;
-        } else {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int32_t xd = x + 4 * d;
-            while (k + 1 < n && int32_t(L.vdst[k + 1]) <= xd) ++k;
-            if (xd >= int32_t(L.vdst[k]) && xd + 4 <= int32_t(L.vend[k]))
-              reinterpret_cast<uint32_t*>(L.oimg)[4 * c + d] =
-                  lds_dword_at(L.vimg, L.vsrc[k] + uint32_t(xd - int32_t(L.vdst[k])));
-          }
         }
+      }
+      // pass 2 (entry lanes): whole dwords of the value inside its first and last chunk when
+      // those chunks are not wholly inside the value
+      for (uint32_t k = l; k < n; k += 64) {
+        const uint32_t A = olead + L.vdst[k], Bv = olead + L.vend[k];  // image byte range
+        if (Bv <= A) continue;
+        const uint32_t src0 = L.vsrc[k];
+        const uint32_t a4 = (A + 3) & ~3u, b4 = Bv & ~3u;
+        if (a4 >= b4) continue;  // no whole dword
+        const uint32_t ja = A >> 4, jb = (Bv - 1) >> 4;
+        // dword ranges [a4, min(b4, 16(ja+1))) and [max(a4, 16 jb), b4), de-duplicated;
+        // chunks wholly inside the value were written by pass 1 (skip those dwords)
+        const bool a_full = (A & 15) == 0 && (A + 16 <= Bv);
+        const bool b_full = ((Bv & 15) == 0) && (Bv - 16 >= A);
+        uint32_t lo1 = a4, hi1 = min(b4, 16 * (ja + 1));
+        uint32_t lo2 = max(a4, max(16 * jb, hi1)), hi2 = b4;
+        if (a_full) hi1 = lo1;
+        if (b_full) hi2 = lo2;
+        for (uint32_t x = lo1; x < hi1; x += 4)
+          reinterpret_cast<uint32_t*>(L.oimg)[x >> 2] = lds_dword_at(L.vimg, src0 + (x - A));
+        for (uint32_t x = lo2; x < hi2; x += 4)
+          reinterpret_cast<uint32_t*>(L.oimg)[x >> 2] = lds_dword_at(L.vimg, src0 + (x - A));
       }
     }
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
-    {
+    if (!(a.skip & 64)) {
       uint8_t* gbase = a.out + (O - olead);
       const uint32_t nc = (olead + uint32_t(size) + 15) >> 4;
       const uint64_t room = a.out_cap - (O - olead);  // bytes of out from gbase on
@@ -1329,6 +1465,9 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       }
     }
     wave_sync();
+    if (!has_next) break;
+    cur = nxt;
+    cur_fast = nxt_fast;
   }
   raise_err(a.stats, err);
 }
@@ -1644,6 +1783,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   e.blk_cap = blk_cap;
   e.n = in->n;
   e.stats = stats;
+  e.skip = c->skip;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   const uint32_t grid = uint32_t(cus) * 3;
