@@ -406,6 +406,7 @@ __device__ __forceinline__ void store_region_chunk(uint8_t* base, uint64_t gb, i
 __device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead, uint32_t n, int32_t rb,
                                                  uint32_t V, uint32_t (&v)[4]) {
   uint32_t k = upper_entry(L.vout, n, rb < 0 ? 0u : uint32_t(rb));
+  uint32_t vbeg = L.vout[k], vend = L.vout[k + 1], vs = L.vsrc[k];  // register-cached cursor
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     uint32_t word = 0;
@@ -413,8 +414,13 @@ __device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead,
     for (int i = 0; i < 4; ++i) {
       const int32_t r = rb + 4 * d + i;
       if (r < 0 || r >= int32_t(V)) continue;
-      while (k + 1 < n && int32_t(L.vout[k + 1]) <= r) ++k;
-      word |= uint32_t(L.img[lead + L.vsrc[k] + (uint32_t(r) - L.vout[k])]) << (8 * i);
+      while (uint32_t(r) >= vend && k + 1 < n) {
+        ++k;
+        vbeg = vend;
+        vend = L.vout[k + 1];
+        vs = L.vsrc[k];
+      }
+      word |= uint32_t(L.img[lead + vs + (uint32_t(r) - vbeg)]) << (8 * i);
     }
     v[d] = word;
   }
@@ -476,29 +482,28 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
       if (j >= nc) continue;
       const int32_t rb = int32_t(16 * j) - int32_t(offK);
       if (!ktab) k = upper_entry(L.kout, n, rb < 0 ? 0u : uint32_t(rb));
+      // cursor state cached in registers; LDS table reads only when crossing into the next key
+      uint32_t kbeg = L.kout[k], kend = L.kout[k + 1], pk = L.pfx[k], ek = L.epos[k];
       uint32_t v[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const int32_t r0 = rb + 4 * d;
-        while (k + 1 < n && int32_t(L.kout[k + 1]) <= r0) ++k;
-        const int32_t t0 = r0 - int32_t(L.kout[k]);
-        const int32_t p = L.pfx[k];
-        if (r0 >= 0 && r0 + 4 <= int32_t(L.kout[k + 1]) && (t0 >= p || t0 + 4 <= p)) {
-          const uint32_t src = t0 >= p ? uint32_t(L.epos[k]) + 4 + uint32_t(t0 - p) : 4u + uint32_t(t0);
-          v[d] = lds_dword_at(img, lead + src);
-        } else {
-          uint32_t word = 0, kk = k;
+        uint32_t word = 0;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int32_t r = r0 + i;
-            if (r < 0 || r >= int32_t(K)) continue;
-            while (kk + 1 < n && int32_t(L.kout[kk + 1]) <= r) ++kk;
-            const uint32_t t = uint32_t(r) - L.kout[kk];
-            const uint32_t src = t < L.pfx[kk] ? 4 + t : uint32_t(L.epos[kk]) + 4 + t - L.pfx[kk];
-            word |= uint32_t(img[lead + src]) << (8 * i);
+        for (int i = 0; i < 4; ++i) {
+          const int32_t r = rb + 4 * d + i;
+          if (r < 0 || r >= int32_t(K)) continue;
+          while (uint32_t(r) >= kend && k + 1 < n) {
+            ++k;
+            kbeg = kend;
+            kend = L.kout[k + 1];
+            pk = L.pfx[k];
+            ek = L.epos[k];
           }
-          v[d] = word;
+          const uint32_t t = uint32_t(r) - kbeg;
+          const uint32_t src = t < pk ? 4 + t : ek + 4 + t - pk;
+          word |= uint32_t(img[lead + src]) << (8 * i);
         }
+        v[d] = word;
       }
       store_region_chunk(a.keys, gbase + 16 * j, rb, K, a.key_cap, v);
     }
@@ -553,6 +558,16 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
 __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   const uint32_t l = lane_id();
   uint32_t err = 0;
+  // output-base loads depend only on b: issue them first, they land during staging + parse
+  const uint64_t tb = b / kTile, jb = b % kTile;
+  uint32_t cn = 0, ck = 0, cv = 0;
+  if (l < jb) {
+    const uint64_t q = tb * kTile + l;
+    cn = a.agg[3 * q];
+    ck = a.agg[3 * q + 1];
+    cv = a.agg[3 * q + 2];
+  }
+  const uint64_t tp0 = a.tile_pre[3 * tb], tp1 = a.tile_pre[3 * tb + 1], tp2 = a.tile_pre[3 * tb + 2];
   const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
   uint32_t len = 0;
   if (end < start || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
@@ -633,21 +648,11 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   uint64_t agg[3] = {h.n, K, V};
   if (err) agg[0] = agg[1] = agg[2] = 0;
 
-  // output bases: tile prefix + this tile's earlier blocks (one coalesced load per lane)
+  // output bases: tile prefix + this tile's earlier blocks
   uint64_t excl[3];
-  {
-    const uint64_t t = b / kTile, j = b % kTile;
-    uint64_t cn = 0, ck = 0, cv = 0;
-    if (l < j) {
-      const uint64_t q = t * kTile + l;
-      cn = a.agg[3 * q];
-      ck = a.agg[3 * q + 1];
-      cv = a.agg[3 * q + 2];
-    }
-    excl[0] = a.tile_pre[3 * t] + wave_sum(cn);
-    excl[1] = a.tile_pre[3 * t + 1] + wave_sum(ck);
-    excl[2] = a.tile_pre[3 * t + 2] + wave_sum(cv);
-  }
+  excl[0] = tp0 + wave_sum(cn);
+  excl[1] = tp1 + wave_sum(ck);
+  excl[2] = tp2 + wave_sum(cv);
   wave_sync();
   const uint64_t E0 = excl[0], K0 = excl[1], V0 = excl[2];
   const uint64_t Et = E0 + agg[0], Kt = K0 + agg[1], Vt = V0 + agg[2];
@@ -957,12 +962,28 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
   K.llead = 0;
   uint32_t c0 = 0, c1 = 0;  // chunk covers entries [c0, c1) with offsets [c0, c1]
 
+  // all of a chunk's loads are issued before the first LDS write (<= 9 + 9 offset values and
+  // <= 9 key chunks per lane), so a reload costs one global round trip, not eighteen
   auto load_chunk = [&](uint32_t from) {
     c0 = from;
     c1 = (s1 - from) < kPlanW ? s1 : from + kPlanW;
-    for (uint32_t i = l; i <= c1 - c0; i += 64) {
-      L.koff[i] = a.key_off[c0 + i];
-      L.voff[i] = a.val_off[c0 + i];
+    const uint32_t cnt = c1 - c0 + 1;
+    uint32_t ko[9], vo[9];
+#pragma unroll
+    for (uint32_t i = 0; i < 9; ++i) {
+      const uint32_t j = l + 64 * i;
+      if (j < cnt) {
+        ko[i] = a.key_off[c0 + j];
+        vo[i] = a.val_off[c0 + j];
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 9; ++i) {
+      const uint32_t j = l + 64 * i;
+      if (j < cnt) {
+        L.koff[j] = ko[i];
+        L.voff[j] = vo[i];
+      }
     }
     wave_sync();
     const uint32_t kb0 = uni(L.koff[0]), kb1 = uni(L.koff[c1 - c0]);
@@ -970,8 +991,13 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     if (llead + (kb1 - kb0) + 8 <= kPlanKB + 32 - 8) {
       const rsrc_t R = K.gk;
       const uint32_t nchunk = (llead + (kb1 - kb0) + 15) >> 4;
-      for (uint32_t c = l; c < nchunk; c += 64)
-        *reinterpret_cast<u32x4*>(L.keys + c * 16) = __builtin_amdgcn_raw_buffer_load_b128(R, al + c * 16, 0, 0);
+      u32x4 q[9];
+#pragma unroll
+      for (uint32_t i = 0; i < 9; ++i)
+        if (l + 64 * i < nchunk) q[i] = __builtin_amdgcn_raw_buffer_load_b128(R, al + (l + 64 * i) * 16, 0, 0);
+#pragma unroll
+      for (uint32_t i = 0; i < 9; ++i)
+        if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.keys + (l + 64 * i) * 16) = q[i];
       K.lbase = kb0;
       K.llead = llead;
       K.lend = kb1;
@@ -1011,7 +1037,9 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         gr = uint64_t(klen) + vlen + 16 - p;  // data growth + 2-byte offset slot
         if (klen == 0) err |= LSMBLK_ERR_EMPTY_KEY;
       }
-      const uint64_t incl = wave_incl_scan<uint64_t>(gr);
+      // u32 DPP scan when every lane's growth is < 2^25 (sum fits), else the 64-bit scan
+      const uint64_t incl = __ballot(gr >= (1u << 25)) == 0 ? uint64_t(wave_incl_scan32(uint32_t(gr)))
+                                                             : wave_incl_scan<uint64_t>(gr);
       const uint64_t before = carry + incl - gr;  // estimated_size() before adding e
       // builder.rs:56-60: reject when est + raw_len + vlen + 6 > block_size (not first entry)
       const bool stop = !valid || (e != s && before + klen + 8 + vlen + 6 > bs);
