@@ -406,23 +406,46 @@ __device__ __forceinline__ void store_region_chunk(uint8_t* base, uint64_t gb, i
 __device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead, uint32_t n, int32_t rb,
                                                  uint32_t V, uint32_t (&v)[4]) {
   uint32_t k = upper_entry(L.vout, n, rb < 0 ? 0u : uint32_t(rb));
-  uint32_t vbeg = L.vout[k], vend = L.vout[k + 1], vs = L.vsrc[k];  // register-cached cursor
+  // register-cached cursor: value k = region bytes [vbeg, vend) at image offset lead + vs
+  uint32_t vbeg = L.vout[k], vend = L.vout[k + 1], vs = lead + L.vsrc[k];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    uint32_t word = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int32_t r = rb + 4 * d + i;
-      if (r < 0 || r >= int32_t(V)) continue;
-      while (uint32_t(r) >= vend && k + 1 < n) {
-        ++k;
-        vbeg = vend;
-        vend = L.vout[k + 1];
-        vs = L.vsrc[k];
-      }
-      word |= uint32_t(L.img[lead + vs + (uint32_t(r) - vbeg)]) << (8 * i);
+    const int32_t r0 = rb + 4 * d;
+    const uint32_t rc = r0 < 0 ? 0u : uint32_t(r0);
+    while (rc >= vend && k + 1 < n) {
+      ++k;
+      vbeg = vend;
+      vend = L.vout[k + 1];
+      vs = lead + L.vsrc[k];
     }
-    v[d] = word;
+    // bytes of this dword that precede the region (r0 < 0) or follow it are don't-care
+    const uint32_t w1 = lds_dword_at(L.img, uint32_t(int32_t(vs) + (r0 - int32_t(vbeg))));
+    if (r0 + 4 <= int32_t(vend) || k + 1 >= n) {
+      v[d] = w1;
+    } else {
+      const uint32_t vend2 = L.vout[k + 2], vs2 = lead + L.vsrc[k + 1];
+      if (r0 + 4 <= int32_t(vend2)) {  // straddles values k and k+1
+        const uint32_t w2 = lds_dword_at(L.img, uint32_t(int32_t(vs2) - (int32_t(vend) - r0)));
+        const uint32_t nb = vend - uint32_t(r0 < 0 ? 0 : r0) + uint32_t(r0 < 0 ? -r0 : 0);  // bytes from k
+        const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+        v[d] = (w1 & m) | (w2 & ~m);
+      } else {  // three or more (tiny) values: byte-wise
+        uint32_t word = 0, kk = k, b0 = vbeg, b1 = vend, ss = vs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int32_t r = r0 + i;
+          if (r < 0 || r >= int32_t(V)) continue;
+          while (uint32_t(r) >= b1 && kk + 1 < n) {
+            ++kk;
+            b0 = b1;
+            b1 = L.vout[kk + 1];
+            ss = lead + L.vsrc[kk];
+          }
+          word |= uint32_t(L.img[ss + (uint32_t(r) - b0)]) << (8 * i);
+        }
+        v[d] = word;
+      }
+    }
   }
 }
 
@@ -939,6 +962,21 @@ __device__ __forceinline__ uint32_t lcp_first(const PlanKeys& K, const uint32_t 
   return p;
 }
 
+// LCP beyond the first 16 bytes (both keys agree on bytes 0..15 and m > 16): dwords 4..7 of
+// the first key come from registers, further ones from memory.  Returns LCP - 16.
+__device__ __forceinline__ uint32_t lcp_first_tail(const PlanKeys& K, const uint32_t (&fkw)[8], uint32_t fp,
+                                                   uint32_t kp, uint32_t m) {
+  for (uint32_t c = 4; 4 * c < m; ++c) {
+    const uint32_t f = c < 8 ? fkw[c & 7] : K.dword(fp + 4 * c);
+    const uint32_t x = f ^ K.dword(kp + 4 * c);
+    if (x) {
+      const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
+      return (q < m ? q : m) - 16;
+    }
+  }
+  return m - 16;
+}
+
 __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
   __shared__ PlanLds lds[kPlanWaves];
   PlanLds& L = lds[threadIdx.x >> 6];
@@ -1011,13 +1049,22 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
   uint64_t bytes = 0;
   uint32_t s = s0;
   const uint64_t bs = a.block_size;
-  while (s < s1) {
-    if (!(s >= c0 && s < c1)) load_chunk(s);
-    // first key of the block (ts is irrelevant to the size rule)
-    const uint32_t fp = uni(L.koff[s - c0]), fl = uni(L.koff[s - c0 + 1]) - fp;
-    uint32_t fkw[8];
+  // First key of the block being packed: arena position, length and its first 32 bytes in
+  // wave-uniform registers.  After the first block it comes for free from the lane that
+  // rejected (readlane of that lane's own key dwords), so the only dependent LDS round trip
+  // per block is the next window's entry reads.
+  uint32_t fp = 0, fl = 0;
+  uint32_t fkw[8];
+  auto load_first = [&](uint32_t at) {
+    fp = uni(L.koff[at - c0]);
+    fl = uni(L.koff[at - c0 + 1]) - fp;
 #pragma unroll
     for (uint32_t c = 0; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
+  };
+  bool have_first = false;
+  while (s < s1) {
+    if (!(s >= c0 && s < c1)) load_chunk(s);
+    if (!have_first) load_first(s);
     uint64_t carry = 2;  // estimated_size() of an empty builder
     uint32_t j0 = s;
     for (;;) {
@@ -1027,16 +1074,37 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
       }
       const uint32_t e = j0 + l;
       const bool valid = e < s1;
-      uint64_t gr = 0;
-      uint32_t klen = 0, vlen = 0;
+      uint32_t klen = 0, vlen = 0, kp = 0, p = 0;
+      uint32_t kd[4] = {0, 0, 0, 0};
       if (valid) {
-        const uint32_t kp = L.koff[e - c0];
+        kp = L.koff[e - c0];
         klen = L.koff[e - c0 + 1] - kp;
         vlen = L.voff[e - c0 + 1] - L.voff[e - c0];
-        const uint32_t p = e == s ? 0u : lcp_first(K, fkw, fp, fl, kp, klen);
-        gr = uint64_t(klen) + vlen + 16 - p;  // data growth + 2-byte offset slot
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) kd[c] = K.dword(kp + 4 * c);
+        if (e != s) {
+          // LCP vs the first key: first 16 bytes from registers, the rest (long keys) byte-wise
+          const uint32_t m = fl < klen ? fl : klen;
+          p = m;
+          bool done = false;
+#pragma unroll
+          for (uint32_t c = 0; c < 4; ++c) {
+            if (!done && 4 * c < m) {
+              const uint32_t x = fkw[c] ^ kd[c];
+              if (x) {
+                const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
+                p = q < m ? q : m;
+                done = true;
+              }
+            } else {
+              done = true;
+            }
+          }
+          if (!done) p = 16 + lcp_first_tail(K, fkw, fp, kp, m);
+        }
         if (klen == 0) err |= LSMBLK_ERR_EMPTY_KEY;
       }
+      const uint64_t gr = valid ? uint64_t(klen) + vlen + 16 - p : 0;  // data growth + offset slot
       // u32 DPP scan when every lane's growth is < 2^25 (sum fits), else the 64-bit scan
       const uint64_t incl = __ballot(gr >= (1u << 25)) == 0 ? uint64_t(wave_incl_scan32(uint32_t(gr)))
                                                              : wave_incl_scan<uint64_t>(gr);
@@ -1046,7 +1114,8 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
       const uint64_t m = __ballot(stop);
       if (m) {
         const uint32_t f = uint32_t(__builtin_ctzll(m));
-        const uint64_t size = __shfl(before, f, 64);
+        const uint64_t size = (uint64_t(__builtin_amdgcn_readlane(uint32_t(before >> 32), f)) << 32) |
+                              __builtin_amdgcn_readlane(uint32_t(before), f);
         if (l == 0) {
           a.rec_first[s0 + nb] = s;
           a.rec_size[s0 + nb] = uint32_t(size);
@@ -1054,9 +1123,29 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         ++nb;
         bytes += size;
         s = j0 + f;
+        // the rejecting lane's key is the next block's first key
+        have_first = s < s1 && f < 64;
+        if (have_first) {
+          fp = __builtin_amdgcn_readlane(kp, f);
+          fl = __builtin_amdgcn_readlane(klen, f);
+#pragma unroll
+          for (uint32_t c = 0; c < 4; ++c) fkw[c] = __builtin_amdgcn_readlane(kd[c], f);
+          if (fl > 16) {
+#pragma unroll
+            for (uint32_t c = 4; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
+          } else {
+#pragma unroll
+            for (uint32_t c = 4; c < 8; ++c) fkw[c] = 0;
+          }
+          // dwords of the first key past its end must not take part in the compare
+#pragma unroll
+          for (uint32_t c = 0; c < 4; ++c)
+            if (4 * c >= fl) fkw[c] = 0;
+        }
         break;
       }
-      carry += __shfl(incl, 63, 64);
+      carry += (uint64_t(__builtin_amdgcn_readlane(uint32_t(incl >> 32), 63)) << 32) |
+               __builtin_amdgcn_readlane(uint32_t(incl), 63);
       j0 += 64;
     }
   }
