@@ -248,16 +248,33 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x
   return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
 }
 
-// Store 16 bytes (dst 16-aligned) or, for a partially covered chunk, only bytes whose
-// mask bit is set.
-__device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t mask) {
-  if (mask == 0xFFFF) {
+// Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
+// store when whole, else conditional whole-dword stores plus at most three bytes at each
+// end (closed-form; a wave pays ~10 stores for its partial lanes, not 16 byte stores).
+__device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t lo, uint32_t hi) {
+  if (lo == 0 && hi == 16) {
     u32x4 q = {v[0], v[1], v[2], v[3]};
     *reinterpret_cast<u32x4*>(dst) = q;
-  } else {
+    return;
+  }
+  const uint32_t lo4 = (lo + 3) >> 2, hi4 = hi >> 2;  // whole dwords [lo4, hi4)
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (mask & (1u << j)) dst[j] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
+  for (uint32_t d = 0; d < 4; ++d)
+    if (d >= lo4 && d < hi4) d32[d] = v[d];
+  // head bytes [lo, min(hi, 4 lo4)) and tail bytes [max(lo, 4 hi4), hi); when the range lies
+  // inside one dword both describe the same bytes: only the head copy writes them
+  const uint32_t he = min(hi, 4 * lo4), ts = max(max(lo, 4 * hi4), he);
+  const uint32_t hw = v[min(lo >> 2, 3u)], tw = v[min(hi4, 3u)];
+#pragma unroll
+  for (uint32_t i = 0; i < 3; ++i) {
+    const uint32_t x = lo + i;
+    if (x < he) dst[x] = uint8_t(hw >> (8 * (x & 3)));
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < 3; ++i) {
+    const uint32_t x = ts + i;
+    if (x < hi) dst[x] = uint8_t(tw >> (8 * (x & 3)));
   }
 }
 
@@ -388,18 +405,16 @@ __device__ void dec_simple_outputs(const DecodeArgs& a, const Img& im, const Blo
 }
 
 // Store 16 output bytes of a region chunk (region byte rb .. rb+15 at global address gb),
-// masking bytes outside [0, size) or beyond the capacity.
+// dropping bytes outside [0, size) or beyond the capacity.
 __device__ __forceinline__ void store_region_chunk(uint8_t* base, uint64_t gb, int32_t rb, uint32_t size,
                                                    uint64_t cap, const uint32_t (&v)[4]) {
-  uint32_t mask = 0xFFFF;
-  if (rb < 0 || rb + 16 > int32_t(size) || gb + 16 > cap) {
-    mask = 0;
-    for (int i = 0; i < 16; ++i) {
-      const int32_t r = rb + i;
-      if (r >= 0 && r < int32_t(size) && gb + i < cap) mask |= 1u << i;
-    }
-  }
-  store_chunk(base + gb, v, mask);
+  const int32_t lo = rb < 0 ? -rb : 0;
+  int64_t hi = int64_t(size) - rb;
+  if (hi > 16) hi = 16;
+  const int64_t room = int64_t(cap) - int64_t(gb);
+  if (room < hi) hi = room;
+  if (hi <= lo) return;
+  store_chunk(base + gb, v, uint32_t(lo), uint32_t(hi));
 }
 
 // Byte-wise value chunk (region boundary or edge chunks).
@@ -505,28 +520,51 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
       if (j >= nc) continue;
       const int32_t rb = int32_t(16 * j) - int32_t(offK);
       if (!ktab) k = upper_entry(L.kout, n, rb < 0 ? 0u : uint32_t(rb));
-      // cursor state cached in registers; LDS table reads only when crossing into the next key
-      uint32_t kbeg = L.kout[k], kend = L.kout[k + 1], pk = L.pfx[k], ek = L.epos[k];
+      // Piece cursor: the key region is the concatenation of pieces (prefix of key k = image
+      // bytes 4.., then its suffix = image bytes epos+4..); psrc is the image byte of region
+      // byte pbeg.  A dword is one unaligned LDS read of the piece holding its first byte,
+      // merged under a byte mask with the following piece(s) when it crosses a boundary.
+      uint32_t ke = L.kout[k + 1];
+      uint32_t pbeg = L.kout[k], pend = pbeg + L.pfx[k], psrc = lead + 4;
+      bool pre = true;
+      auto advance = [&]() -> bool {
+        do {
+          if (pre) {
+            pre = false;
+            pbeg = pend;
+            pend = ke;
+            psrc = lead + L.epos[k] + 4;
+          } else {
+            if (k + 1 >= n) return false;
+            ++k;
+            pre = true;
+            pbeg = ke;
+            ke = L.kout[k + 1];
+            pend = pbeg + L.pfx[k];
+            psrc = lead + 4;
+          }
+        } while (pend == pbeg);
+        return true;
+      };
+      if (pend == pbeg) advance();  // empty prefix (keys themselves are never empty)
       uint32_t v[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        uint32_t word = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int32_t r = rb + 4 * d + i;
-          if (r < 0 || r >= int32_t(K)) continue;
-          while (uint32_t(r) >= kend && k + 1 < n) {
-            ++k;
-            kbeg = kend;
-            kend = L.kout[k + 1];
-            pk = L.pfx[k];
-            ek = L.epos[k];
-          }
-          const uint32_t t = uint32_t(r) - kbeg;
-          const uint32_t src = t < pk ? 4 + t : ek + 4 + t - pk;
-          word |= uint32_t(img[lead + src]) << (8 * i);
+        const int32_t r0 = rb + 4 * d;
+        v[d] = 0;
+        if (r0 >= int32_t(K)) continue;
+        while (r0 >= int32_t(pend) && advance()) {
         }
-        v[d] = word;
+        // r0 < 0 only in the first chunk (pbeg == 0): bytes before the region are don't-care
+        uint32_t w = lds_dword_at(img, uint32_t(int32_t(psrc) + (r0 - int32_t(pbeg))));
+        int32_t cov = int32_t(pend) - r0;
+        while (cov < 4 && advance()) {
+          const uint32_t w2 = lds_dword_at(img, psrc - uint32_t(cov));
+          const uint32_t m = (1u << (8 * cov)) - 1;
+          w = (w & m) | (w2 & ~m);
+          cov = int32_t(pend) - r0;
+        }
+        v[d] = w;
       }
       store_region_chunk(a.keys, gbase + 16 * j, rb, K, a.key_cap, v);
     }
@@ -1570,15 +1608,11 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       for (uint32_t c = l; c < nc; c += 64) {
         const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + c * 16);
         const uint32_t v[4] = {q.x, q.y, q.z, q.w};
-        uint32_t mask = 0xFFFF;
-        if (16 * c < olead || 16 * c + 16 > olead + size || 16 * c + 16 > room) {
-          mask = 0;
-          for (int j = 0; j < 16; ++j) {
-            const uint32_t xj = c * 16 + j;
-            if (xj >= olead && xj < olead + size && xj < room) mask |= 1u << j;
-          }
-        }
-        store_chunk(gbase + c * 16, v, mask);
+        const uint32_t lo = 16 * c < olead ? olead - 16 * c : 0u;
+        uint64_t hi = olead + size - 16ull * c;
+        if (hi > 16) hi = 16;
+        if (room < 16ull * c + hi) hi = room > 16ull * c ? room - 16ull * c : 0;
+        if (hi > lo) store_chunk(gbase + c * 16, v, lo, uint32_t(hi));
       }
     }
     wave_sync();

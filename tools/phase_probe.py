@@ -1,0 +1,38 @@
+"""GPU-box probe for per-phase PMC counts: runs encode (or decode) of the U workload a few
+times with one ablation mask (lsmblk_debug_set key 1) so that a rocprofv3 --pmc pass sees
+dispatches of a single configuration.
+
+usage: python3 tools/phase_probe.py {encode|decode} MASK [entries]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from lsm_amd import batch, synth  # noqa: E402
+from lsm_amd._lib import check, lib  # noqa: E402
+
+
+def main():
+    which, mask = sys.argv[1], int(sys.argv[2])
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else 8 << 20
+    keys, key_off, vals, val_off, ts = synth.gen_uniform(n)
+    kv = batch.KVStream.from_numpy(keys, key_off, vals, val_off, ts, device="cuda")
+    seg = synth.segments_by_bytes(key_off, val_off)
+    blocks, blk_off = batch.encode_kv(kv, seg, synth.BLOCK_SIZE["U"])
+    ctx = batch._ctx(0)
+    check(lib().lsmblk_debug_set(ctx, 1, mask))
+    for _ in range(3):
+        if which == "encode":
+            batch.encode_kv(kv, seg, synth.BLOCK_SIZE["U"])
+        else:
+            batch.decode_blocks(blocks, blk_off)
+    torch.cuda.synchronize()
+    check(lib().lsmblk_debug_set(ctx, 1, 0))
+    print(which, mask, "blocks", blk_off.numel() - 1)
+
+
+if __name__ == "__main__":
+    main()
