@@ -293,7 +293,7 @@ struct DecodeArgs {
   const uint32_t* agg;        // per-block (entries, key bytes, value bytes), from dec_count_kernel
   const uint64_t* tile_pre;   // per-tile exclusive prefix (entries, key bytes, value bytes)
   uint32_t skip;  // ablation mask (lsmblk_debug_set, timing experiments only): 2 keys,
-                  // 4 values, 8 per-entry metadata
+                  // 4 values, 8 per-entry metadata, 16 value pass 2, 32 value pass 1
 };
 
 constexpr uint32_t kTile = 64;  // blocks per count tile
@@ -405,22 +405,21 @@ __device__ void dec_simple_outputs(const DecodeArgs& a, const Img& im, const Blo
 }
 
 // Store 16 output bytes of a region chunk (region byte rb .. rb+15 at global address gb),
-// dropping bytes outside [0, size) or beyond the capacity.
+// dropping bytes outside [0, size).  Capacity is checked per block before any output is
+// written (a block that does not fit writes nothing and raises CAPACITY).
 __device__ __forceinline__ void store_region_chunk(uint8_t* base, uint64_t gb, int32_t rb, uint32_t size,
-                                                   uint64_t cap, const uint32_t (&v)[4]) {
+                                                   const uint32_t (&v)[4]) {
   const int32_t lo = rb < 0 ? -rb : 0;
-  int64_t hi = int64_t(size) - rb;
-  if (hi > 16) hi = 16;
-  const int64_t room = int64_t(cap) - int64_t(gb);
-  if (room < hi) hi = room;
-  if (hi <= lo) return;
-  store_chunk(base + gb, v, uint32_t(lo), uint32_t(hi));
+  const int32_t rem = int32_t(size) - rb;
+  const int32_t hi = rem < 16 ? rem : 16;
+  if (hi > lo) store_chunk(base + gb, v, uint32_t(lo), uint32_t(hi));
 }
 
 // Byte-wise value chunk (region boundary or edge chunks).
+// k0: the entry holding region byte max(rb, 0), or ~0u to search for it.
 __device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead, uint32_t n, int32_t rb,
-                                                 uint32_t V, uint32_t (&v)[4]) {
-  uint32_t k = upper_entry(L.vout, n, rb < 0 ? 0u : uint32_t(rb));
+                                                 uint32_t V, uint32_t k0, uint32_t (&v)[4]) {
+  uint32_t k = k0 != ~0u ? k0 : upper_entry(L.vout, n, rb < 0 ? 0u : uint32_t(rb));
   // register-cached cursor: value k = region bytes [vbeg, vend) at image offset lead + vs
   uint32_t vbeg = L.vout[k], vend = L.vout[k + 1], vs = lead + L.vsrc[k];
 #pragma unroll
@@ -566,7 +565,7 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
         }
         v[d] = w;
       }
-      store_region_chunk(a.keys, gbase + 16 * j, rb, K, a.key_cap, v);
+      store_region_chunk(a.keys, gbase + 16 * j, rb, K, v);
     }
   }
   // values, pass 1: chunks lying inside one value (no divergence: others are skipped)
@@ -579,20 +578,22 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
       const uint32_t j = j0 + l;
       const uint32_t k = max(wave_incl_max32(j < nc ? L.vcent[j] : 0u), carry);
       carry = __builtin_amdgcn_readlane(k, 63);
-      if (j >= nc) continue;
+      if (j >= nc || (skip & 32)) continue;
       const int32_t rb = int32_t(16 * j) - int32_t(offV);
       if (rb < 0 || rb + 16 > int32_t(V)) continue;
       if (rb < int32_t(L.vout[k]) || rb + 16 > int32_t(L.vout[k + 1])) continue;
       uint32_t v[4];
       lds_read16(img, lead + L.vsrc[k] + uint32_t(rb) - L.vout[k], v);
-      store_region_chunk(a.vals, gbase + 16 * j, rb, V, a.val_cap, v);
+      store_region_chunk(a.vals, gbase + 16 * j, rb, V, v);
     }
     // pass 2: the chunk holding each in-chunk value boundary (owned by its first boundary)
     // and the two partial edge chunks, byte-wise.
     const uint32_t jlast = (offV + V - 1) >> 4;
-    for (uint32_t c = 0; c < n + 64; c += 64) {
+    // lanes k = n and n + 1 (after the entry lanes) take the first and last (partial) chunks
+    for (uint32_t c = 0; c < n + 2 && !(skip & 16); c += 64) {
       const uint32_t k = c + l;
       int32_t j = -1;
+      uint32_t k0 = ~0u;
       if (k >= 1 && k < n) {
         const uint32_t bk = L.vout[k] + offV;
         if ((bk & 15) != 0 && L.vout[k] > 0 && L.vout[k] < V) {
@@ -600,18 +601,22 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
           const uint32_t bp = L.vout[k - 1] + offV;
           const bool prev_same = k >= 2 && (bp & 15) != 0 && L.vout[k - 1] > 0 && (bp >> 4) == jb;
           const bool edge = (jb == 0 && offV != 0) || (jb == jlast && ((offV + V) & 15) != 0);
-          if (!prev_same && !edge) j = int32_t(jb);
+          // owner = first boundary in the chunk: the chunk's first byte is in value k-1
+          if (!prev_same && !edge) {
+            j = int32_t(jb);
+            k0 = k - 1;
+          }
         }
-      } else if (c == 0 && l == 62 && offV != 0) {
+      } else if (k == n && offV != 0) {
         j = 0;
-      } else if (c == 0 && l == 63 && ((offV + V) & 15) != 0 && !(jlast == 0 && offV != 0)) {
+      } else if (k == n + 1 && ((offV + V) & 15) != 0 && !(jlast == 0 && offV != 0)) {
         j = int32_t(jlast);
       }
       if (j < 0) continue;
       const int32_t rb = 16 * j - int32_t(offV);
       uint32_t v[4];
-      value_chunk_slow(L, lead, n, rb, V, v);
-      store_region_chunk(a.vals, gbase + 16 * uint32_t(j), rb, V, a.val_cap, v);
+      value_chunk_slow(L, lead, n, rb, V, k0, v);
+      store_region_chunk(a.vals, gbase + 16 * uint32_t(j), rb, V, v);
     }
   }
 }
@@ -720,7 +725,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   if (Kt > 0xFFFFFFFFull || Vt > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
   if (Et > a.entry_cap || Kt > a.key_cap || Vt > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
 
-  if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW)) && h.n) {
+  if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
     if (fast) {
       dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
     } else if (fits) {
@@ -1601,18 +1606,17 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     }
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
-    if (!(a.skip & 64)) {
+    // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
+    if (!(a.skip & 64) && O + size <= a.out_cap) {
       uint8_t* gbase = a.out + (O - olead);
-      const uint32_t nc = (olead + uint32_t(size) + 15) >> 4;
-      const uint64_t room = a.out_cap - (O - olead);  // bytes of out from gbase on
+      const uint32_t end = olead + uint32_t(size);
+      const uint32_t nc = (end + 15) >> 4;
       for (uint32_t c = l; c < nc; c += 64) {
         const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + c * 16);
         const uint32_t v[4] = {q.x, q.y, q.z, q.w};
         const uint32_t lo = 16 * c < olead ? olead - 16 * c : 0u;
-        uint64_t hi = olead + size - 16ull * c;
-        if (hi > 16) hi = 16;
-        if (room < 16ull * c + hi) hi = room > 16ull * c ? room - 16ull * c : 0;
-        if (hi > lo) store_chunk(gbase + c * 16, v, lo, uint32_t(hi));
+        const uint32_t hi = min(end - 16 * c, 16u);
+        store_chunk(gbase + c * 16, v, lo, hi);
       }
     }
     wave_sync();

@@ -135,6 +135,26 @@ def test_many_tiny_entries_per_block():
     assert (np.diff(off) > 0).all()
 
 
+@pytest.mark.parametrize("value_len,shift", [(8, 0), (8, 5), (12, 3)])
+def test_fast_path_blocks_with_64_to_128_entries(value_len, shift):
+    # 16-B keys + small values: ~100 entries per 4 KiB block, i.e. more entries than lanes
+    # in a wave but still on the LDS-table (fast) paths of encode and decode
+    kv = O.KV(*synth.gen_uniform(20000, seed=12 + value_len, value_len=value_len))
+    _, off = roundtrip_check(kv, [0, kv.n], 4096, shift=shift)
+    per_block = kv.n / (len(off) - 1)
+    assert 64 < per_block <= 128
+
+
+def test_small_random_values_mixed_entry_counts():
+    rng = np.random.default_rng(13)
+    kv0 = O.KV(*synth.gen_uniform(15000, seed=13))
+    keys = [bytes(kv0.keys[16 * i:16 * i + 16]) for i in range(kv0.n)]
+    ents = [(k, int(kv0.ts[i]), bytes(rng.integers(0, 256, int(rng.integers(0, 24)), dtype=np.uint8)))
+            for i, k in enumerate(keys)]
+    kv = O.KV.from_entries(ents)
+    roundtrip_check(kv, [0, kv.n], 4096, shift=7)
+
+
 def test_long_keys_and_shared_prefixes():
     rng = np.random.default_rng(2)
     base = bytes(rng.integers(0, 256, 90, dtype=np.uint8))
