@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU-box: parity tests -> full bench (cpu baseline + pcie) -> rocprof stats -> PMC traffic passes.
+# usage: tools/round_gpu.sh TAG
+set -o pipefail
+TAG=$1; shift
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/tests_$TAG.log; exit 1; }
+tail -2 gpurun_out/tests_$TAG.log
+timeout -k 10 300 python3 bench.py --pcie > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -f csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || { echo "rocprof failed"; exit 1; }
+head -6 gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -d, -f1-4
+if [ "$1" != "--no-pmc" ]; then
+  bash tools/traffic.sh gpurun_out/traffic_$TAG.json || exit 1
+  cat gpurun_out/traffic_$TAG.json
+fi
