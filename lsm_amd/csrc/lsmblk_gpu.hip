@@ -215,14 +215,22 @@ __device__ __forceinline__ void raise_err(uint64_t* stats, uint32_t err) {
 // ---------------------------------------------------------------- byte sources
 // An "image" is a block's bytes addressed block-relative; LdsImg reads the LDS staging copy,
 // GlbImg reads global memory through a bounds-checked buffer descriptor (OOB reads = 0).
+// LDS image swizzle (decode block image, emit output image): 16-B granule g of 128-B row r
+// is stored at granule g ^ (r & 7).  U-config entries are exactly 128 B apart (16-B keys,
+// p = 2, 100-B values), so without it per-entry-lane accesses at one field offset all hit
+// one bank (32-way conflicts); with it they spread over 8 granules.  Granules stay whole, so
+// b128 staging writes / flush reads and 8-B aligned b64 reads are unaffected.
+__device__ __forceinline__ uint32_t swz(uint32_t x) { return x ^ ((x >> 3) & 0x70u); }
+
 struct LdsImg {
-  const uint8_t* p;  // LDS address of block byte 0
-  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
-  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (uint32_t(p[i]) << 8) | p[i + 1]; }
+  const uint8_t* base;  // swizzled LDS image; block byte 0 is image byte lead
+  uint32_t lead;
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return base[swz(lead + i)]; }
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
   __device__ __forceinline__ uint64_t u64(uint32_t i) const {
     uint64_t v = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v = (v << 8) | p[i + j];
+    for (int j = 0; j < 8; ++j) v = (v << 8) | u8(i + j);
     return v;
   }
 };
@@ -246,6 +254,14 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x
   const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
   const uint32_t i = x >> 2;
   return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
+}
+
+// 4 bytes starting at byte offset x of a swizzled LDS image.
+__device__ __forceinline__ uint32_t sw_dword_at(const uint8_t* base, uint32_t x) {
+  const uint32_t x4 = x & ~3u;
+  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(base + swz(x4));
+  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(base + swz(x4 + 4));
+  return __builtin_amdgcn_alignbyte(w1, w0, x & 3);
 }
 
 // Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
@@ -326,6 +342,22 @@ __device__ __forceinline__ uint32_t upper_entry(const uint32_t* tab, uint32_t n,
 __device__ __forceinline__ void lds_read16(const uint8_t* base, uint32_t x, uint32_t (&v)[4]) {
   const uint2* q = reinterpret_cast<const uint2*>(base + (x & ~7u));
   const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
+  const uint32_t sh = x & 3;
+  const bool hi = (x & 4) != 0;
+  const uint32_t w0 = hi ? q0.y : q0.x, w1 = hi ? q1.x : q0.y, w2 = hi ? q1.y : q1.x;
+  const uint32_t w3 = hi ? q2.x : q1.y, w4 = hi ? q2.y : q2.x;
+  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+}
+
+// lds_read16 on a swizzled image (8-B pieces never straddle a 16-B granule)
+__device__ __forceinline__ void sw_read16(const uint8_t* base, uint32_t x, uint32_t (&v)[4]) {
+  const uint32_t x8 = x & ~7u;
+  const uint2 q0 = *reinterpret_cast<const uint2*>(base + swz(x8));
+  const uint2 q1 = *reinterpret_cast<const uint2*>(base + swz(x8 + 8));
+  const uint2 q2 = *reinterpret_cast<const uint2*>(base + swz(x8 + 16));
   const uint32_t sh = x & 3;
   const bool hi = (x & 4) != 0;
   const uint32_t w0 = hi ? q0.y : q0.x, w1 = hi ? q1.x : q0.y, w2 = hi ? q1.y : q1.x;
@@ -433,13 +465,13 @@ __device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead,
       vs = lead + L.vsrc[k];
     }
     // bytes of this dword that precede the region (r0 < 0) or follow it are don't-care
-    const uint32_t w1 = lds_dword_at(L.img, uint32_t(int32_t(vs) + (r0 - int32_t(vbeg))));
+    const uint32_t w1 = sw_dword_at(L.img, uint32_t(int32_t(vs) + (r0 - int32_t(vbeg))));
     if (r0 + 4 <= int32_t(vend) || k + 1 >= n) {
       v[d] = w1;
     } else {
       const uint32_t vend2 = L.vout[k + 2], vs2 = lead + L.vsrc[k + 1];
       if (r0 + 4 <= int32_t(vend2)) {  // straddles values k and k+1
-        const uint32_t w2 = lds_dword_at(L.img, uint32_t(int32_t(vs2) - (int32_t(vend) - r0)));
+        const uint32_t w2 = sw_dword_at(L.img, uint32_t(int32_t(vs2) - (int32_t(vend) - r0)));
         const uint32_t nb = vend - uint32_t(r0 < 0 ? 0 : r0) + uint32_t(r0 < 0 ? -r0 : 0);  // bytes from k
         const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
         v[d] = (w1 & m) | (w2 & ~m);
@@ -455,7 +487,7 @@ __device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead,
             b1 = L.vout[kk + 1];
             ss = lead + L.vsrc[kk];
           }
-          word |= uint32_t(L.img[ss + (uint32_t(r) - b0)]) << (8 * i);
+          word |= uint32_t(L.img[swz(ss + (uint32_t(r) - b0))]) << (8 * i);
         }
         v[d] = word;
       }
@@ -475,9 +507,7 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
       const uint64_t e = E0 + k;
       if (e < a.entry_cap) {
         const uint32_t x = lead + L.epos[k] + 4 + L.sfx[k];  // big-endian u64 ts after the suffix
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(img) + (x >> 2);
-        const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], x & 3);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(w[2], w[1], x & 3);
+        const uint32_t lo = sw_dword_at(img, x), hi = sw_dword_at(img, x + 4);
         a.ts[e] = __builtin_bswap64((uint64_t(hi) << 32) | lo);
         a.key_off[e] = uint32_t(K0 + L.kout[k]);
         a.val_off[e] = uint32_t(V0 + L.vout[k]);
@@ -555,10 +585,10 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
         while (r0 >= int32_t(pend) && advance()) {
         }
         // r0 < 0 only in the first chunk (pbeg == 0): bytes before the region are don't-care
-        uint32_t w = lds_dword_at(img, uint32_t(int32_t(psrc) + (r0 - int32_t(pbeg))));
+        uint32_t w = sw_dword_at(img, uint32_t(int32_t(psrc) + (r0 - int32_t(pbeg))));
         int32_t cov = int32_t(pend) - r0;
         while (cov < 4 && advance()) {
-          const uint32_t w2 = lds_dword_at(img, psrc - uint32_t(cov));
+          const uint32_t w2 = sw_dword_at(img, psrc - uint32_t(cov));
           const uint32_t m = (1u << (8 * cov)) - 1;
           w = (w & m) | (w2 & ~m);
           cov = int32_t(pend) - r0;
@@ -583,7 +613,7 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
       if (rb < 0 || rb + 16 > int32_t(V)) continue;
       if (rb < int32_t(L.vout[k]) || rb + 16 > int32_t(L.vout[k + 1])) continue;
       uint32_t v[4];
-      lds_read16(img, lead + L.vsrc[k] + uint32_t(rb) - L.vout[k], v);
+      sw_read16(img, lead + L.vsrc[k] + uint32_t(rb) - L.vout[k], v);
       store_region_chunk(a.vals, gbase + 16 * j, rb, V, v);
     }
     // pass 2: the chunk holding each in-chunk value boundary (owned by its first boundary)
@@ -654,25 +684,20 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
       if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
+      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + swz((l + 64 * i) * 16)) = v[i];
     wave_sync();
-    h = parse_hdr(LdsImg{L.img + lead}, len);
+    h = parse_hdr(LdsImg{L.img, lead}, len);
   } else {
     h = parse_hdr(GlbImg{R, lead}, len);
   }
   if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
   const bool fast = fits && h.n <= kDecMaxE;
-#ifdef LSMBLK_DEVICE_DEBUG
-  if (l == 0) printf("dec b=%llu start=%llu end=%llu len=%u lead=%u fits=%d n=%u data_end=%u fks=%u ok=%d err=%u img0=%02x %02x %02x %02x last=%02x %02x\n",
-                     (unsigned long long)b, (unsigned long long)start, (unsigned long long)end, len, lead, (int)fits, h.n, h.data_end, h.fks, (int)h.ok, err,
-                     L.img[lead], L.img[lead + 1], L.img[lead + 2], L.img[lead + 3], L.img[lead + len - 2], L.img[lead + len - 1]);
-#endif
 
   // phase 1: parse entries, block aggregates (entries, key bytes, value bytes)
   uint64_t K = 0, V = 0;
   bool bad = false;
   if (fast) {
-    const LdsImg im{L.img + lead};
+    const LdsImg im{L.img, lead};
     for (uint32_t c = 0; c < h.n; c += 64) {
       const uint32_t k = c + l;
       uint32_t off = 0, p = 0, s = 0, vl = 0;
@@ -702,7 +727,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
       uint32_t off = 0, p = 0, s = 0, vl = 0;
       bool ok = true;
       if (k < h.n) {
-        if (fits) ok = parse_entry(LdsImg{L.img + lead}, h, k, off, p, s, vl);
+        if (fits) ok = parse_entry(LdsImg{L.img, lead}, h, k, off, p, s, vl);
         else ok = parse_entry(GlbImg{R, lead}, h, k, off, p, s, vl);
       }
       bad = bad || !ok;
@@ -729,16 +754,11 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
     if (fast) {
       dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
     } else if (fits) {
-      dec_simple_outputs(a, LdsImg{L.img + lead}, h, E0, K0, V0);
+      dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
     } else {
       dec_simple_outputs(a, GlbImg{R, lead}, h, E0, K0, V0);
     }
   }
-#ifdef LSMBLK_DEVICE_DEBUG
-  if (l == 0) printf("dec b=%llu agg=%llu %llu %llu excl=%llu %llu %llu err=%u\n", (unsigned long long)b,
-                     (unsigned long long)agg[0], (unsigned long long)agg[1], (unsigned long long)agg[2],
-                     (unsigned long long)E0, (unsigned long long)K0, (unsigned long long)V0, err);
-#endif
   raise_err(a.stats, err);
 }
 
@@ -1270,8 +1290,9 @@ struct alignas(16) EmitLds {
   uint32_t vsrc[kEmitMaxE];
 };
 
-__device__ __forceinline__ void lds_be(uint8_t* p, uint64_t v, int nbytes) {
-  for (int i = 0; i < nbytes; ++i) p[i] = uint8_t(v >> (8 * (nbytes - 1 - i)));
+// big-endian field of nbytes at byte x of a swizzled LDS image
+__device__ __forceinline__ void sw_be(uint8_t* base, uint32_t x, uint64_t v, int nbytes) {
+  for (int i = 0; i < nbytes; ++i) base[swz(x + i)] = uint8_t(v >> (8 * (nbytes - 1 - i)));
 }
 
 // Global byte readers for the simple path.
@@ -1467,7 +1488,8 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     if (has_next) meta2(nxt);  // level-2 of the next block
     wave_sync();
     // entry lanes: prefix, positions, non-value bytes and value edge bytes into oimg
-    const uint32_t fl = uni(a.key_off[s + 1]) - kb0;  // first key is at kimg[klead]
+    // first key is at kimg[klead]; its end offset key_off[s + 1] is lane 0's prefetched pf_ko1
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf_ko1) - kb0;
     const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of this block
     for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
     uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
@@ -1523,21 +1545,22 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       dc += __shfl(incl, 63, 64);
       if (k < n && !(a.skip & 16)) {
         const uint32_t sfx = kl - p;
-        uint8_t* o = L.oimg + olead + pos;
-        lds_be(o, p & 0xFFFF, 2);
-        lds_be(o + 2, sfx & 0xFFFF, 2);
+        uint8_t* o = L.oimg;
+        const uint32_t ox = olead + pos;
+        sw_be(o, ox, p & 0xFFFF, 2);
+        sw_be(o, ox + 2, sfx & 0xFFFF, 2);
         const uint8_t* ks = L.kimg + klead + kp + p;
-        for (uint32_t t = 0; t < sfx; ++t) o[4 + t] = ks[t];
-        lds_be(o + 4 + sfx, tsv, 8);
-        lds_be(o + 12 + sfx, vl & 0xFFFF, 2);
+        for (uint32_t t = 0; t < sfx; ++t) o[swz(ox + 4 + t)] = ks[t];
+        sw_be(o, ox + 4 + sfx, tsv, 8);
+        sw_be(o, ox + 12 + sfx, vl & 0xFFFF, 2);
         const uint32_t A = olead + pos + 14 + sfx, Bv = A + vl;
         const uint32_t a4 = (A + 3) & ~3u, b4 = Bv & ~3u;
         const uint8_t* vs = L.vimg + vlead + vp;
         if (a4 >= b4) {
-          for (uint32_t t = 0; t < vl; ++t) L.oimg[A + t] = vs[t];
+          for (uint32_t t = 0; t < vl; ++t) o[swz(A + t)] = vs[t];
         } else {
-          for (uint32_t x = A; x < a4; ++x) L.oimg[x] = vs[x - A];
-          for (uint32_t x = b4; x < Bv; ++x) L.oimg[x] = vs[x - A];
+          for (uint32_t x = A; x < a4; ++x) o[swz(x)] = vs[x - A];
+          for (uint32_t x = b4; x < Bv; ++x) o[swz(x)] = vs[x - A];
         }
       }
       if (k < n) {
@@ -1555,8 +1578,8 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
     wave_sync();
     // offsets table + entry count (u16 BE, `as u16`)
-    for (uint32_t k = l; k < n; k += 64) lds_be(L.oimg + olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
-    if (l == 0) lds_be(L.oimg + olead + data_len + 2 * n, n & 0xFFFF, 2);
+    for (uint32_t k = l; k < n; k += 64) sw_be(L.oimg, olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
+    if (l == 0) sw_be(L.oimg, olead + data_len + 2 * n, n & 0xFFFF, 2);
     if (has_next) {  // next block's staging loads overlap this block's bulk copy + flush
       nxt_fast = is_fast(nxt);
       if (nxt_fast) issue(nxt);
@@ -1578,7 +1601,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
           uint32_t v[4];
           lds_read16(L.vimg, L.vsrc[k] + uint32_t(x - int32_t(L.vdst[k])), v);
           u32x4 q = {v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<u32x4*>(L.oimg + 16 * c) = q;
+          *reinterpret_cast<u32x4*>(L.oimg + swz(16 * c)) = q;
         }
       }
       // pass 2 (entry lanes): whole dwords of the value inside its first and last chunk when
@@ -1599,9 +1622,9 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         if (a_full) hi1 = lo1;
         if (b_full) hi2 = lo2;
         for (uint32_t x = lo1; x < hi1; x += 4)
-          reinterpret_cast<uint32_t*>(L.oimg)[x >> 2] = lds_dword_at(L.vimg, src0 + (x - A));
+          *reinterpret_cast<uint32_t*>(L.oimg + swz(x)) = lds_dword_at(L.vimg, src0 + (x - A));
         for (uint32_t x = lo2; x < hi2; x += 4)
-          reinterpret_cast<uint32_t*>(L.oimg)[x >> 2] = lds_dword_at(L.vimg, src0 + (x - A));
+          *reinterpret_cast<uint32_t*>(L.oimg + swz(x)) = lds_dword_at(L.vimg, src0 + (x - A));
       }
     }
     wave_sync();
@@ -1612,7 +1635,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       const uint32_t end = olead + uint32_t(size);
       const uint32_t nc = (end + 15) >> 4;
       for (uint32_t c = l; c < nc; c += 64) {
-        const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + c * 16);
+        const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + swz(c * 16));
         const uint32_t v[4] = {q.x, q.y, q.z, q.w};
         const uint32_t lo = 16 * c < olead ? olead - 16 * c : 0u;
         const uint32_t hi = min(end - 16 * c, 16u);
