@@ -36,6 +36,7 @@
 namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr uint32_t kSpinLimit = 1u << 22;  // look-back bound (~seconds); never reached when correct
@@ -318,24 +319,12 @@ constexpr uint32_t kDecWaves = 4;
 constexpr uint32_t kDecImg = 4352;  // staged block bytes per wave (4 KiB blocks + lead + slack)
 constexpr uint32_t kDecMaxE = 128;  // entries with LDS tables (fast path)
 
-constexpr uint32_t kDecChunks = kDecImg / 16 + 2;  // 16-B output chunks of a region (V, K <= len)
 
 struct alignas(16) DecLds {
   uint8_t img[kDecImg];
   uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE], vsrc[kDecMaxE];
   uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
-  uint32_t kcent[kDecChunks], vcent[kDecChunks];  // region chunk -> last entry starting at/before it
 };
-
-// largest k in [0, n) with tab[k] <= r (tab[0] == 0 <= r)
-__device__ __forceinline__ uint32_t upper_entry(const uint32_t* tab, uint32_t n, uint32_t r) {
-  uint32_t lo = 0, hi = n;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (tab[mid] <= r) lo = mid; else hi = mid;
-  }
-  return lo;
-}
 
 // 16 bytes at LDS byte offset x (any alignment) via three 8-B reads: ds_read_b64 at a 16-B
 // lane stride is bank-conflict free, ds_read_b32 at that stride is a 4-way conflict.
@@ -436,217 +425,86 @@ __device__ void dec_simple_outputs(const DecodeArgs& a, const Img& im, const Blo
   }
 }
 
-// Store 16 output bytes of a region chunk (region byte rb .. rb+15 at global address gb),
-// dropping bytes outside [0, size).  Capacity is checked per block before any output is
-// written (a block that does not fit writes nothing and raises CAPACITY).
-__device__ __forceinline__ void store_region_chunk(uint8_t* base, uint64_t gb, int32_t rb, uint32_t size,
-                                                   const uint32_t (&v)[4]) {
-  const int32_t lo = rb < 0 ? -rb : 0;
-  const int32_t rem = int32_t(size) - rb;
-  const int32_t hi = rem < 16 ? rem : 16;
-  if (hi > lo) store_chunk(base + gb, v, uint32_t(lo), uint32_t(hi));
+// Unaligned 16-B / 8-B / 4-B / 1-B stores through a buffer descriptor whose base is 16-B
+// aligned (the gfx9 unaligned access mode: a dword store needs only byte alignment).
+__device__ __forceinline__ void st16(const rsrc_t& R, uint32_t off, const uint32_t (&v)[4]) {
+  const u32x4 q = {v[0], v[1], v[2], v[3]};
+  __builtin_amdgcn_raw_buffer_store_b128(q, R, off, 0, 0);
 }
 
-// Byte-wise value chunk (region boundary or edge chunks).
-// k0: the entry holding region byte max(rb, 0), or ~0u to search for it.
-__device__ __forceinline__ void value_chunk_slow(const DecLds& L, uint32_t lead, uint32_t n, int32_t rb,
-                                                 uint32_t V, uint32_t k0, uint32_t (&v)[4]) {
-  uint32_t k = k0 != ~0u ? k0 : upper_entry(L.vout, n, rb < 0 ? 0u : uint32_t(rb));
-  // register-cached cursor: value k = region bytes [vbeg, vend) at image offset lead + vs
-  uint32_t vbeg = L.vout[k], vend = L.vout[k + 1], vs = lead + L.vsrc[k];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int32_t r0 = rb + 4 * d;
-    const uint32_t rc = r0 < 0 ? 0u : uint32_t(r0);
-    while (rc >= vend && k + 1 < n) {
-      ++k;
-      vbeg = vend;
-      vend = L.vout[k + 1];
-      vs = lead + L.vsrc[k];
-    }
-    // bytes of this dword that precede the region (r0 < 0) or follow it are don't-care
-    const uint32_t w1 = sw_dword_at(L.img, uint32_t(int32_t(vs) + (r0 - int32_t(vbeg))));
-    if (r0 + 4 <= int32_t(vend) || k + 1 >= n) {
-      v[d] = w1;
-    } else {
-      const uint32_t vend2 = L.vout[k + 2], vs2 = lead + L.vsrc[k + 1];
-      if (r0 + 4 <= int32_t(vend2)) {  // straddles values k and k+1
-        const uint32_t w2 = sw_dword_at(L.img, uint32_t(int32_t(vs2) - (int32_t(vend) - r0)));
-        const uint32_t nb = vend - uint32_t(r0 < 0 ? 0 : r0) + uint32_t(r0 < 0 ? -r0 : 0);  // bytes from k
-        const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
-        v[d] = (w1 & m) | (w2 & ~m);
-      } else {  // three or more (tiny) values: byte-wise
-        uint32_t word = 0, kk = k, b0 = vbeg, b1 = vend, ss = vs;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int32_t r = r0 + i;
-          if (r < 0 || r >= int32_t(V)) continue;
-          while (uint32_t(r) >= b1 && kk + 1 < n) {
-            ++kk;
-            b0 = b1;
-            b1 = L.vout[kk + 1];
-            ss = lead + L.vsrc[kk];
-          }
-          word |= uint32_t(L.img[swz(ss + (uint32_t(r) - b0))]) << (8 * i);
-        }
-        v[d] = word;
-      }
-    }
+// Store bytes [0, len) of a run (len < 16) whose first 16 bytes are v: overlapping stores of
+// the widest size that fits (8+8, 4+4, or single bytes), never past len.
+__device__ __forceinline__ void st_short(const rsrc_t& R, uint32_t off, uint32_t len, const uint32_t (&v)[4]) {
+  if (len >= 8) {
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, R, off, 0, 0);
+    // bytes [len - 8, len)
+    const uint32_t x = len - 8, sh = x & 3;
+    const uint32_t w0 = x < 4 ? v[0] : v[1], w1 = x < 4 ? v[1] : v[2], w2 = x < 4 ? v[2] : v[3];
+    __builtin_amdgcn_raw_buffer_store_b64(
+        u32x2{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh)}, R, off + x, 0, 0);
+  } else if (len >= 4) {
+    __builtin_amdgcn_raw_buffer_store_b32(v[0], R, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(v[1], v[0], len - 4), R, off + len - 4, 0, 0);
+  } else {
+    for (uint32_t i = 0; i < len; ++i)
+      __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v[0] >> (8 * i)), R, off + i, 0, 0);
   }
 }
 
-// Fast path: LDS image + LDS tables, coalesced aligned stores.
+// Fast path, lane per entry: every entry lane writes its own key and value as contiguous
+// runs with unaligned 16-B stores (the last piece overlaps the previous one), so runs of
+// adjacent entries abut without read-modify-write and no lane needs a chunk -> entry search.
 __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
                                  uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V, uint32_t skip) {
   const uint32_t l = lane_id();
   const uint8_t* img = L.img;
   const uint32_t n = h.n;
-  // per-entry metadata (entry lanes)
-  if (!(skip & 8)) {
-    for (uint32_t k = l; k < n; k += 64) {
-      const uint64_t e = E0 + k;
-      if (e < a.entry_cap) {
-        const uint32_t x = lead + L.epos[k] + 4 + L.sfx[k];  // big-endian u64 ts after the suffix
-        const uint32_t lo = sw_dword_at(img, x), hi = sw_dword_at(img, x + 4);
-        a.ts[e] = __builtin_bswap64((uint64_t(hi) << 32) | lo);
-        a.key_off[e] = uint32_t(K0 + L.kout[k]);
-        a.val_off[e] = uint32_t(V0 + L.vout[k]);
-      }
-    }
-  }
-  // chunk -> entry tables: entry k marks the first region chunk starting at or after its
-  // first byte; a wave max-scan over the chunk lanes then yields, for every chunk, the last
-  // entry starting at or before it (no per-chunk binary search)
-  const uint32_t offKc = uint32_t(K0 & 15), offVc = uint32_t(V0 & 15);
-  const uint32_t nck = (offKc + K + 15) >> 4, ncv = (offVc + V + 15) >> 4;
-  const bool ktab = nck <= kDecChunks;
-  for (uint32_t j = l; j < ncv; j += 64) L.vcent[j] = 0;
-  if (ktab)
-    for (uint32_t j = l; j < nck; j += 64) L.kcent[j] = 0;
-  wave_sync();
+  // descriptors over this block's output runs, bases aligned down to 16 B
+  const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
+  const rsrc_t RK = make_rsrc(a.keys + (K0 - kb), kb + K);
+  const rsrc_t RV = make_rsrc(a.vals + (V0 - vb), vb + V);
+  const uint32_t fk = lead + 4;  // image byte of the first key
   for (uint32_t k = l; k < n; k += 64) {
-    const uint32_t jv = (L.vout[k] + offVc + 15) >> 4;
-    if (jv < ncv && L.vout[k + 1] > L.vout[k]) atomicMax(&L.vcent[jv], k);
-    const uint32_t jk = (L.kout[k] + offKc + 15) >> 4;
-    if (ktab && jk < nck) atomicMax(&L.kcent[jk], k);
-  }
-  wave_sync();
-  // keys: 16-B chunks covering [K0, K0+K).  A key is two pieces, first-key prefix (image
-  // byte 4 + t) and own suffix (image byte epos + 4 + t - p); a dword inside one piece is
-  // one unaligned LDS read, anything else is resolved byte by byte.
-  if (!(skip & 2)) {
-    const uint32_t offK = uint32_t(K0 & 15);
-    const uint64_t gbase = K0 - offK;
-    const uint32_t nc = (offK + K + 15) >> 4;
-    uint32_t carry = 0;
-    for (uint32_t j0 = 0; j0 < nc; j0 += 64) {
-      const uint32_t j = j0 + l;
-      uint32_t k;
-      if (ktab) {
-        k = max(wave_incl_max32(j < nc ? L.kcent[j] : 0u), carry);
-        carry = __builtin_amdgcn_readlane(k, 63);
-      }
-      if (j >= nc) continue;
-      const int32_t rb = int32_t(16 * j) - int32_t(offK);
-      if (!ktab) k = upper_entry(L.kout, n, rb < 0 ? 0u : uint32_t(rb));
-      // Piece cursor: the key region is the concatenation of pieces (prefix of key k = image
-      // bytes 4.., then its suffix = image bytes epos+4..); psrc is the image byte of region
-      // byte pbeg.  A dword is one unaligned LDS read of the piece holding its first byte,
-      // merged under a byte mask with the following piece(s) when it crosses a boundary.
-      uint32_t ke = L.kout[k + 1];
-      uint32_t pbeg = L.kout[k], pend = pbeg + L.pfx[k], psrc = lead + 4;
-      bool pre = true;
-      auto advance = [&]() -> bool {
-        do {
-          if (pre) {
-            pre = false;
-            pbeg = pend;
-            pend = ke;
-            psrc = lead + L.epos[k] + 4;
-          } else {
-            if (k + 1 >= n) return false;
-            ++k;
-            pre = true;
-            pbeg = ke;
-            ke = L.kout[k + 1];
-            pend = pbeg + L.pfx[k];
-            psrc = lead + 4;
-          }
-        } while (pend == pbeg);
-        return true;
+    const uint32_t epos = L.epos[k], p = L.pfx[k], s = L.sfx[k];
+    const uint32_t kout = L.kout[k], vout = L.vout[k], vl = L.vout[k + 1] - vout;
+    const uint32_t sb = lead + epos + 4;  // image byte of the suffix
+    if (!(skip & 8)) {
+      const uint64_t e = E0 + k;
+      const uint32_t lo = sw_dword_at(img, sb + s), hi = sw_dword_at(img, sb + s + 4);
+      a.ts[e] = __builtin_bswap64((uint64_t(hi) << 32) | lo);
+      a.key_off[e] = uint32_t(K0 + kout);
+      a.val_off[e] = uint32_t(V0 + vout);
+    }
+    if (!(skip & 2)) {
+      // key byte x = first key byte x (x < p) or suffix byte x - p; a dword straddling p
+      // merges the two under a byte mask
+      const uint32_t kl = p + s;
+      auto kdw = [&](uint32_t x) -> uint32_t {
+        const uint32_t sw = sw_dword_at(img, sb + x - p);
+        if (x >= p) return sw;
+        const uint32_t fw = sw_dword_at(img, fk + x);
+        if (x + 4 <= p) return fw;
+        const uint32_t m = (1u << (8 * (p - x))) - 1;
+        return (fw & m) | (sw & ~m);
       };
-      if (pend == pbeg) advance();  // empty prefix (keys themselves are never empty)
-      uint32_t v[4];
+      for (uint32_t t = 0; t < kl; t += 16) {
+        const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
+        uint32_t v[4];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int32_t r0 = rb + 4 * d;
-        v[d] = 0;
-        if (r0 >= int32_t(K)) continue;
-        while (r0 >= int32_t(pend) && advance()) {
-        }
-        // r0 < 0 only in the first chunk (pbeg == 0): bytes before the region are don't-care
-        uint32_t w = sw_dword_at(img, uint32_t(int32_t(psrc) + (r0 - int32_t(pbeg))));
-        int32_t cov = int32_t(pend) - r0;
-        while (cov < 4 && advance()) {
-          const uint32_t w2 = sw_dword_at(img, psrc - uint32_t(cov));
-          const uint32_t m = (1u << (8 * cov)) - 1;
-          w = (w & m) | (w2 & ~m);
-          cov = int32_t(pend) - r0;
-        }
-        v[d] = w;
+        for (uint32_t d = 0; d < 4; ++d) v[d] = kdw(o + 4 * d);
+        if (kl >= 16) st16(RK, kb + kout + o, v);
+        else st_short(RK, kb + kout, kl, v);
       }
-      store_region_chunk(a.keys, gbase + 16 * j, rb, K, v);
     }
-  }
-  // values, pass 1: chunks lying inside one value (no divergence: others are skipped)
-  if (!(skip & 4)) {
-    const uint32_t offV = uint32_t(V0 & 15);
-    const uint64_t gbase = V0 - offV;
-    const uint32_t nc = (offV + V + 15) >> 4;
-    uint32_t carry = 0;
-    for (uint32_t j0 = 0; j0 < nc; j0 += 64) {
-      const uint32_t j = j0 + l;
-      const uint32_t k = max(wave_incl_max32(j < nc ? L.vcent[j] : 0u), carry);
-      carry = __builtin_amdgcn_readlane(k, 63);
-      if (j >= nc || (skip & 32)) continue;
-      const int32_t rb = int32_t(16 * j) - int32_t(offV);
-      if (rb < 0 || rb + 16 > int32_t(V)) continue;
-      if (rb < int32_t(L.vout[k]) || rb + 16 > int32_t(L.vout[k + 1])) continue;
-      uint32_t v[4];
-      sw_read16(img, lead + L.vsrc[k] + uint32_t(rb) - L.vout[k], v);
-      store_region_chunk(a.vals, gbase + 16 * j, rb, V, v);
-    }
-    // pass 2: the chunk holding each in-chunk value boundary (owned by its first boundary)
-    // and the two partial edge chunks, byte-wise.
-    const uint32_t jlast = (offV + V - 1) >> 4;
-    // lanes k = n and n + 1 (after the entry lanes) take the first and last (partial) chunks
-    for (uint32_t c = 0; c < n + 2 && !(skip & 16); c += 64) {
-      const uint32_t k = c + l;
-      int32_t j = -1;
-      uint32_t k0 = ~0u;
-      if (k >= 1 && k < n) {
-        const uint32_t bk = L.vout[k] + offV;
-        if ((bk & 15) != 0 && L.vout[k] > 0 && L.vout[k] < V) {
-          const uint32_t jb = bk >> 4;
-          const uint32_t bp = L.vout[k - 1] + offV;
-          const bool prev_same = k >= 2 && (bp & 15) != 0 && L.vout[k - 1] > 0 && (bp >> 4) == jb;
-          const bool edge = (jb == 0 && offV != 0) || (jb == jlast && ((offV + V) & 15) != 0);
-          // owner = first boundary in the chunk: the chunk's first byte is in value k-1
-          if (!prev_same && !edge) {
-            j = int32_t(jb);
-            k0 = k - 1;
-          }
-        }
-      } else if (k == n && offV != 0) {
-        j = 0;
-      } else if (k == n + 1 && ((offV + V) & 15) != 0 && !(jlast == 0 && offV != 0)) {
-        j = int32_t(jlast);
+    if (!(skip & 4)) {
+      const uint32_t src = sb + s + 10;  // image byte of the value
+      for (uint32_t t = 0; t < vl; t += 16) {
+        const uint32_t o = vl >= 16 ? min(t, vl - 16) : 0u;
+        uint32_t v[4];
+        sw_read16(img, src + o, v);
+        if (vl >= 16) st16(RV, vb + vout + o, v);
+        else st_short(RV, vb + vout, vl, v);
       }
-      if (j < 0) continue;
-      const int32_t rb = 16 * j - int32_t(offV);
-      uint32_t v[4];
-      value_chunk_slow(L, lead, n, rb, V, k0, v);
-      store_region_chunk(a.vals, gbase + 16 * uint32_t(j), rb, V, v);
     }
   }
 }
