@@ -104,6 +104,10 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p16, uint32_t nbytes) {
   const uint32_t n = nbytes >= 0xFFFFFFF0u ? 0xFFFFFFFFu : (nbytes + 15) & ~15u;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p16), (short)0, (int)n, 0x00020000);
 }
+// Store descriptor with an exact byte bound: an access reaching past nbytes is dropped.
+__device__ __forceinline__ rsrc_t make_rsrc_exact(void* p16, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p16, (short)0, (int)nbytes, 0x00020000);
+}
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF); }
 
 // ---------------------------------------------------------------- look-back granules
@@ -315,15 +319,16 @@ struct DecodeArgs {
 
 constexpr uint32_t kTile = 64;  // blocks per count tile
 
-constexpr uint32_t kDecWaves = 4;
 constexpr uint32_t kDecImg = 4352;  // staged block bytes per wave (4 KiB blocks + lead + slack)
 constexpr uint32_t kDecMaxE = 128;  // entries with LDS tables (fast path)
+constexpr uint32_t kDecOut = 4096;  // LDS output image (keys + values) of a fast-path block
 
 
 struct alignas(16) DecLds {
   uint8_t img[kDecImg];
   uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE], vsrc[kDecMaxE];
   uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
+  uint8_t out[kDecOut];  // decoded key run, then (16-B aligned) value run
 };
 
 // 16 bytes at LDS byte offset x (any alignment) via three 8-B reads: ds_read_b64 at a 16-B
@@ -451,18 +456,52 @@ __device__ __forceinline__ void st_short(const rsrc_t& R, uint32_t off, uint32_t
   }
 }
 
+// Output sinks of the lane-per-entry decode: unaligned runs either go straight to global
+// memory (GlbSink, buffer stores) or are composed in the wave's LDS output image (LdsSink)
+// that is then flushed with aligned, coalesced 16-B stores (one HBM write request per 64-B
+// line instead of one per lane).
+struct GlbSink {
+  rsrc_t RK, RV;
+  uint32_t kb, vb;  // byte of the first key / value in its descriptor (16-B aligned base)
+  __device__ __forceinline__ void put16(bool val, uint32_t off, const uint32_t (&v)[4]) const {
+    st16(val ? RV : RK, (val ? vb : kb) + off, v);
+  }
+  __device__ __forceinline__ void put_short(bool val, uint32_t off, uint32_t len, const uint32_t (&v)[4]) const {
+    st_short(val ? RV : RK, (val ? vb : kb) + off, len, v);
+  }
+};
+struct LdsSink {
+  uint8_t* out;
+  uint32_t kb, vb;  // LDS byte of the first key / value
+  __device__ __forceinline__ void put16(bool val, uint32_t off, const uint32_t (&v)[4]) const {
+    *reinterpret_cast<u32x4*>(out + (val ? vb : kb) + off) = u32x4{v[0], v[1], v[2], v[3]};
+  }
+  __device__ __forceinline__ void put_short(bool val, uint32_t off, uint32_t len, const uint32_t (&v)[4]) const {
+    uint8_t* p = out + (val ? vb : kb) + off;
+    if (len >= 8) {
+      const uint32_t x = len - 8, sh = x & 3;
+      const uint32_t w0 = x < 4 ? v[0] : v[1], w1 = x < 4 ? v[1] : v[2], w2 = x < 4 ? v[2] : v[3];
+      *reinterpret_cast<u32x2*>(p) = u32x2{v[0], v[1]};
+      *reinterpret_cast<u32x2*>(p + x) =
+          u32x2{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh)};
+    } else if (len >= 4) {
+      *reinterpret_cast<uint32_t*>(p) = v[0];
+      *reinterpret_cast<uint32_t*>(p + len - 4) = __builtin_amdgcn_alignbyte(v[1], v[0], len - 4);
+    } else {
+      for (uint32_t i = 0; i < len; ++i) p[i] = uint8_t(v[0] >> (8 * i));
+    }
+  }
+};
+
 // Fast path, lane per entry: every entry lane writes its own key and value as contiguous
-// runs with unaligned 16-B stores (the last piece overlaps the previous one), so runs of
-// adjacent entries abut without read-modify-write and no lane needs a chunk -> entry search.
-__device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
-                                 uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V, uint32_t skip) {
+// runs of 16-B pieces (the last piece overlaps the previous one), so runs of adjacent
+// entries abut and no lane needs a chunk -> entry search.
+template <class Sink>
+__device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, uint32_t lead, uint32_t n,
+                                               uint64_t E0, uint64_t K0, uint64_t V0, const Sink& out,
+                                               uint32_t skip) {
   const uint32_t l = lane_id();
   const uint8_t* img = L.img;
-  const uint32_t n = h.n;
-  // descriptors over this block's output runs, bases aligned down to 16 B
-  const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
-  const rsrc_t RK = make_rsrc(a.keys + (K0 - kb), kb + K);
-  const rsrc_t RV = make_rsrc(a.vals + (V0 - vb), vb + V);
   const uint32_t fk = lead + 4;  // image byte of the first key
   for (uint32_t k = l; k < n; k += 64) {
     const uint32_t epos = L.epos[k], p = L.pfx[k], s = L.sfx[k];
@@ -492,8 +531,8 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
         uint32_t v[4];
 #pragma unroll
         for (uint32_t d = 0; d < 4; ++d) v[d] = kdw(o + 4 * d);
-        if (kl >= 16) st16(RK, kb + kout + o, v);
-        else st_short(RK, kb + kout, kl, v);
+        if (kl >= 16) out.put16(false, kout + o, v);
+        else out.put_short(false, kout, kl, v);
       }
     }
     if (!(skip & 4)) {
@@ -502,10 +541,39 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
         const uint32_t o = vl >= 16 ? min(t, vl - 16) : 0u;
         uint32_t v[4];
         sw_read16(img, src + o, v);
-        if (vl >= 16) st16(RV, vb + vout + o, v);
-        else st_short(RV, vb + vout, vl, v);
+        if (vl >= 16) out.put16(true, vout + o, v);
+        else out.put_short(true, vout, vl, v);
       }
     }
+  }
+}
+
+// Aligned flush of an LDS output run: LDS bytes [lo, lo + len) -> global bytes at gdst, with
+// lo == gdst & 15 (the LDS run mirrors the global 16-B alignment).  Interior chunks are one
+// b128 store; the two edge chunks store only their own bytes.
+__device__ __forceinline__ void flush_run(uint8_t* gdst_aligned, const uint8_t* lds, uint32_t lo, uint32_t len) {
+  const uint32_t end = lo + len, nc = (end + 15) >> 4;
+  for (uint32_t c = lane_id(); c < nc; c += 64) {
+    const u32x4 q = *reinterpret_cast<const u32x4*>(lds + 16 * c);
+    const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+    const uint32_t a0 = 16 * c < lo ? lo - 16 * c : 0u;
+    const uint32_t a1 = min(end - 16 * c, 16u);
+    store_chunk(gdst_aligned + 16 * c, v, a0, a1);
+  }
+}
+
+__device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
+                                 uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V, uint32_t skip) {
+  const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
+  const uint32_t vrun = (kb + K + 15) & ~15u;  // LDS start of the value run's first chunk
+  if (vrun + vb + V + 16 <= kDecOut) {
+    dec_entry_runs(a, L, lead, h.n, E0, K0, V0, LdsSink{L.out, kb, vrun + vb}, skip);
+    wave_sync();
+    flush_run(a.keys + (K0 - kb), L.out, kb, K);
+    flush_run(a.vals + (V0 - vb), L.out + vrun, vb, V);
+  } else {
+    const GlbSink g{make_rsrc_exact(a.keys + (K0 - kb), kb + K), make_rsrc_exact(a.vals + (V0 - vb), vb + V), kb, vb};
+    dec_entry_runs(a, L, lead, h.n, E0, K0, V0, g, skip);
   }
 }
 
@@ -621,10 +689,12 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
 }
 
 // One wave per block, no inter-wave waiting: the bases come from the count + scan passes.
-__global__ __launch_bounds__(256) void decode_kernel(DecodeArgs a) {
-  __shared__ DecLds lds[kDecWaves];
-  const uint64_t b = uint64_t(blockIdx.x) * kDecWaves + (threadIdx.x >> 6);
-  if (b < a.nblk) decode_block(a, lds[threadIdx.x >> 6], b);
+// One single-wave workgroup per block (LDS, not waves, bounds the residency: single-wave
+// workgroups pack the CU's LDS best).  No inter-wave waiting: the output bases come from the
+// count + scan passes.
+__global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
+  __shared__ DecLds lds;
+  decode_block(a, lds, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- decode pass 1: count
@@ -1756,8 +1826,7 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   a.agg = c->dec_agg;
   a.tile_pre = c->tile_pre;
   a.skip = c->skip;
-  const uint64_t grid = (nblk + kDecWaves - 1) / kDecWaves;
-  hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(grid)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(nblk)), dim3(64), 0, st, a);
   if (c->timing) (void)hipEventRecord(c->ev[3], st);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
