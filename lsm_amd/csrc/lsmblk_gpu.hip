@@ -73,6 +73,10 @@ __device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
   v = max(v, LSM_DPP(v, 0x143, 0xC));
   return v;
 }
+// Inclusive min-scan of values <= 0x7FFFFFFF as the max-scan of 0x7FFFFFFF - v: DPP lanes
+// shifted in from outside a row read 0, the max identity.  (Measured on gfx950: an
+// update_dpp "old" of 0xFFFFFFFF does not reach those lanes, and ~max(~v) was folded away.)
+__device__ __forceinline__ uint32_t wave_incl_min31(uint32_t v) { return 0x7FFFFFFFu - wave_incl_max32(0x7FFFFFFFu - v); }
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   return __builtin_amdgcn_readlane(wave_incl_scan32(v), 63);
 }
@@ -901,6 +905,8 @@ struct alignas(16) PlanLds {
   uint8_t keys[kPlanKB + 32];
   uint32_t koff[kPlanW + 1];
   uint32_t voff[kPlanW + 1];
+  uint32_t rec[kPlanW];   // klen + vlen
+  uint32_t alcp[kPlanW];  // LCP with the predecessor key | out-of-order flag << 31
 };
 
 // Key bytes of the batch, served from the LDS chunk when it holds them.
@@ -991,8 +997,12 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
   K.llead = 0;
   uint32_t c0 = 0, c1 = 0;  // chunk covers entries [c0, c1) with offsets [c0, c1]
 
-  // all of a chunk's loads are issued before the first LDS write (<= 9 + 9 offset values and
-  // <= 9 key chunks per lane), so a reload costs one global round trip, not eighteen
+  // A chunk = offsets, key bytes and the per-entry walk inputs of up to kPlanW entries.  All of
+  // its global loads are issued before the first LDS write (<= 9 + 9 offset values and <= 9
+  // key chunks per lane).  Then, all lanes in parallel: rec = klen + vlen and alcp = LCP of
+  // the key with its predecessor in the segment, bit 31 set when the pair is out of order.
+  // For keys in non-decreasing order LCP(first, key_e) = min of alcp over (first, e], which
+  // turns the serial block walk into two wave scans over LDS words.
   auto load_chunk = [&](uint32_t from) {
     c0 = from;
     c1 = (s1 - from) < kPlanW ? s1 : from + kPlanW;
@@ -1006,6 +1016,8 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         vo[i] = a.val_off[c0 + j];
       }
     }
+    // predecessor of the chunk's first entry (its key is outside the chunk)
+    const uint32_t kprev = c0 > s0 ? uni(a.key_off[c0 - 1]) : 0u;
 #pragma unroll
     for (uint32_t i = 0; i < 9; ++i) {
       const uint32_t j = l + 64 * i;
@@ -1034,74 +1046,88 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
       K.lbase = K.lend = 0;  // keys from global
     }
     wave_sync();
+    for (uint32_t j = l; j < c1 - c0; j += 64) {
+      const uint32_t e = c0 + j;
+      const uint32_t kp = L.koff[j], kl = L.koff[j + 1] - kp;
+      uint32_t alcp = 0;
+      if (e > s0) {
+        const uint32_t pp = j ? L.koff[j - 1] : kprev, pl = kp - pp;
+        const uint32_t m = pl < kl ? pl : kl;
+        uint32_t lcp = m, w0 = 0, w1 = 0;
+        for (uint32_t d = 0; 4 * d < m; ++d) {
+          const uint32_t x0 = K.dword(pp + 4 * d), x1 = K.dword(kp + 4 * d);
+          if (x0 != x1) {
+            const uint32_t z = 4 * d + (__builtin_ctz(x0 ^ x1) >> 3);
+            if (z < m) {
+              lcp = z;
+              w0 = x0;
+              w1 = x1;
+            }
+            break;
+          }
+        }
+        const uint32_t sh = 8 * (lcp & 3);
+        const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
+        alcp = lcp | (sorted ? 0u : 0x80000000u);
+        if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
+      } else if (kl == 0) {
+        err |= LSMBLK_ERR_EMPTY_KEY;
+      }
+      L.rec[j] = kl + (L.voff[j + 1] - L.voff[j]);
+      L.alcp[j] = alcp;
+    }
+    wave_sync();
   };
 
   uint32_t nb = 0;
   uint64_t bytes = 0;
   uint32_t s = s0;
   const uint64_t bs = a.block_size;
-  // First key of the block being packed: arena position, length and its first 32 bytes in
-  // wave-uniform registers.  After the first block it comes for free from the lane that
-  // rejected (readlane of that lane's own key dwords), so the only dependent LDS round trip
-  // per block is the next window's entry reads.
-  uint32_t fp = 0, fl = 0;
-  uint32_t fkw[8];
-  auto load_first = [&](uint32_t at) {
-    fp = uni(L.koff[at - c0]);
-    fl = uni(L.koff[at - c0 + 1]) - fp;
-#pragma unroll
-    for (uint32_t c = 0; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
-  };
-  bool have_first = false;
   while (s < s1) {
     if (!(s >= c0 && s < c1)) load_chunk(s);
-    if (!have_first) load_first(s);
-    uint64_t carry = 2;  // estimated_size() of an empty builder
+    // first key of this block (used only by the direct-LCP fallback for unsorted windows)
+    const uint32_t fp = uni(L.koff[s - c0]), fl = uni(L.koff[s - c0 + 1]) - fp;
+    bool have_fkw = false, direct = false;
+    uint32_t fkw[8];
+    uint64_t carry = 2;         // estimated_size() of an empty builder
+    uint32_t pmin = 0x7FFFFFFFu;  // running min of alcp over (s, window start)
     uint32_t j0 = s;
     for (;;) {
       const uint32_t wend = (s1 - j0) < 64 ? s1 : j0 + 64;
-      if (!(j0 >= c0 && wend <= c1)) {
-        load_chunk(j0);
-      }
+      if (!(j0 >= c0 && wend <= c1)) load_chunk(j0);
       const uint32_t e = j0 + l;
       const bool valid = e < s1;
-      uint32_t klen = 0, vlen = 0, kp = 0, p = 0;
-      uint32_t kd[4] = {0, 0, 0, 0};
+      uint32_t rec = 0, al = 0x7FFFFFFFu;
       if (valid) {
-        kp = L.koff[e - c0];
-        klen = L.koff[e - c0 + 1] - kp;
-        vlen = L.voff[e - c0 + 1] - L.voff[e - c0];
-#pragma unroll
-        for (uint32_t c = 0; c < 4; ++c) kd[c] = K.dword(kp + 4 * c);
-        if (e != s) {
-          // LCP vs the first key: first 16 bytes from registers, the rest (long keys) byte-wise
-          const uint32_t m = fl < klen ? fl : klen;
-          p = m;
-          bool done = false;
-#pragma unroll
-          for (uint32_t c = 0; c < 4; ++c) {
-            if (!done && 4 * c < m) {
-              const uint32_t x = fkw[c] ^ kd[c];
-              if (x) {
-                const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
-                p = q < m ? q : m;
-                done = true;
-              }
-            } else {
-              done = true;
-            }
-          }
-          if (!done) p = 16 + lcp_first_tail(K, fkw, fp, kp, m);
-        }
-        if (klen == 0) err |= LSMBLK_ERR_EMPTY_KEY;
+        rec = L.rec[e - c0];
+        if (e != s) al = L.alcp[e - c0];
       }
-      const uint64_t gr = valid ? uint64_t(klen) + vlen + 16 - p : 0;  // data growth + offset slot
+      direct = direct || __ballot(al >> 31) != 0;  // an out-of-order pair inside this block
+      uint32_t p = 0;
+      if (!direct) {
+        p = min(pmin, wave_incl_min31(al));
+        if (e == s) p = 0;
+      } else {
+        if (!have_fkw) {
+#pragma unroll
+          for (uint32_t c = 0; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
+          have_fkw = true;
+        }
+        if (valid && e != s) {
+          const uint32_t kp = L.koff[e - c0], kl = L.koff[e - c0 + 1] - kp;
+          p = lcp_first(K, fkw, fp, fl, kp, kl);
+        }
+      }
+#ifdef LSMBLK_PLAN_DEBUG
+      if (g == 0 && valid) printf("e=%u s=%u al=%x p=%u rec=%u direct=%d pmin=%u\n", e, s, al, p, rec, (int)direct, pmin);
+#endif
+      const uint64_t gr = valid ? uint64_t(rec) + 16 - p : 0;  // data growth + offset slot
       // u32 DPP scan when every lane's growth is < 2^25 (sum fits), else the 64-bit scan
       const uint64_t incl = __ballot(gr >= (1u << 25)) == 0 ? uint64_t(wave_incl_scan32(uint32_t(gr)))
                                                              : wave_incl_scan<uint64_t>(gr);
       const uint64_t before = carry + incl - gr;  // estimated_size() before adding e
       // builder.rs:56-60: reject when est + raw_len + vlen + 6 > block_size (not first entry)
-      const bool stop = !valid || (e != s && before + klen + 8 + vlen + 6 > bs);
+      const bool stop = !valid || (e != s && before + rec + 14 > bs);
       const uint64_t m = __ballot(stop);
       if (m) {
         const uint32_t f = uint32_t(__builtin_ctzll(m));
@@ -1114,29 +1140,11 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         ++nb;
         bytes += size;
         s = j0 + f;
-        // the rejecting lane's key is the next block's first key
-        have_first = s < s1 && f < 64;
-        if (have_first) {
-          fp = __builtin_amdgcn_readlane(kp, f);
-          fl = __builtin_amdgcn_readlane(klen, f);
-#pragma unroll
-          for (uint32_t c = 0; c < 4; ++c) fkw[c] = __builtin_amdgcn_readlane(kd[c], f);
-          if (fl > 16) {
-#pragma unroll
-            for (uint32_t c = 4; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
-          } else {
-#pragma unroll
-            for (uint32_t c = 4; c < 8; ++c) fkw[c] = 0;
-          }
-          // dwords of the first key past its end must not take part in the compare
-#pragma unroll
-          for (uint32_t c = 0; c < 4; ++c)
-            if (4 * c >= fl) fkw[c] = 0;
-        }
         break;
       }
       carry += (uint64_t(__builtin_amdgcn_readlane(uint32_t(incl >> 32), 63)) << 32) |
                __builtin_amdgcn_readlane(uint32_t(incl), 63);
+      pmin = __builtin_amdgcn_readlane(p, 63);
       j0 += 64;
     }
   }

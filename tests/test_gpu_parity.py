@@ -246,3 +246,29 @@ def test_roundtrip_properties_large(cfg, n, target):
     assert rc == 0
     np.testing.assert_array_equal(blk_off.cpu().numpy().view(np.uint64), ro)
     np.testing.assert_array_equal(blocks.cpu().numpy(), rb)
+
+
+@pytest.mark.parametrize("order", ["shuffled", "one_inversion", "descending", "dup_runs"])
+def test_key_order_adjacent_lcp_and_direct_fallback(order):
+    # The plan walk derives LCP(first key, key) as the running min of adjacent-pair LCPs,
+    # valid only for non-decreasing keys; windows holding an out-of-order pair must fall back
+    # to the direct first-key compare (builder.rs:19-33 compares against the first key only).
+    rng = np.random.default_rng(21)
+    n = 6000
+    pre = [bytes(rng.integers(0, 256, int(rng.integers(0, 6)), dtype=np.uint8)) for _ in range(8)]
+    keys = sorted({pre[int(rng.integers(0, 8))] + bytes(rng.integers(0, 256, int(rng.integers(1, 20)), dtype=np.uint8))
+                   for _ in range(n)})
+    if order == "shuffled":
+        keys = [keys[i] for i in rng.permutation(len(keys))]
+    elif order == "one_inversion":
+        i = len(keys) // 2
+        keys[i], keys[i + 1] = keys[i + 1], keys[i]
+    elif order == "descending":
+        keys = keys[::-1]
+    else:  # long runs of one key (multi-version), lcp == full length
+        keys = [k for k in keys[:600] for _ in range(int(rng.integers(1, 12)))]
+    ents = [(k, i, bytes(rng.integers(0, 256, int(rng.integers(0, 160)), dtype=np.uint8)))
+            for i, k in enumerate(keys)]
+    kv = O.KV.from_entries(ents)
+    roundtrip_check(kv, [0, kv.n], 4096)
+    roundtrip_check(kv, [0, kv.n // 3, kv.n], 512)
