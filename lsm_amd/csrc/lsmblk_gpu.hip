@@ -1211,19 +1211,16 @@ struct EmitArgs {
 
 constexpr uint32_t kEmitWaves = 4;
 constexpr uint32_t kEmitKCap = 1088;
-constexpr uint32_t kEmitVCap = 4160;
-constexpr uint32_t kEmitOCap = 4160;
+constexpr uint32_t kEmitICap = 4224;  // block image: staged values, then the encoded block (33 swizzle rows)
 constexpr uint32_t kEmitMaxE = 128;
 
 struct alignas(16) EmitLds {
   uint8_t kimg[kEmitKCap];
-  uint8_t vimg[kEmitVCap];
-  uint8_t oimg[kEmitOCap];
-  uint32_t cent[kEmitOCap / 16 + 1];  // image chunk -> last entry whose value starts at or before it
-  uint32_t epos[kEmitMaxE];
-  uint32_t vdst[kEmitMaxE + 1];
-  uint32_t vend[kEmitMaxE];
-  uint32_t vsrc[kEmitMaxE];
+  uint8_t img[kEmitICap];
+  uint32_t cent[kEmitICap / 16 + 1];  // chunk -> last entry whose value starts at/before it, then its source
+  uint16_t epos[kEmitMaxE], pfx[kEmitMaxE], ksrc[kEmitMaxE];  // record start, prefix, suffix in kimg
+  uint16_t vdst[kEmitMaxE], vsrc[kEmitMaxE], vlen[kEmitMaxE];  // value start (block), staged start, length
+  uint64_t ts[kEmitMaxE];
 };
 
 // big-endian field of nbytes at byte x of a swizzled LDS image
@@ -1323,7 +1320,7 @@ struct EmitMeta {
 // metadata, the key/value staging loads and the first 64 entries' offsets/ts of block i+1
 // are already in flight (the wave is latency-bound otherwise: ~3 dependent global round
 // trips per block).  LDS caps occupancy at 3 waves/SIMD, so the prefetch registers are free.
-__global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void emit_kernel(EmitArgs a) {
   __shared__ EmitLds lds[kEmitWaves];
   EmitLds& L = lds[threadIdx.x >> 6];
   const uint32_t l = lane_id();
@@ -1349,8 +1346,9 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
   };
   auto is_fast = [&](const EmitMeta& m) {
     const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
+    // the staged values and the encoded block share the image (24 B of read slack)
     return m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
-           vlead + (m.vb1 - m.vb0) + 8 <= kEmitVCap && uint32_t(m.O & 15) + m.size + 8 <= kEmitOCap;
+           vlead + (m.vb1 - m.vb0) + 24 <= kEmitICap && uint32_t(m.O & 15) + m.size + 8 <= kEmitICap;
   };
   u32x4 kq[2], vq[5];
   uint32_t pf_ko0 = 0, pf_ko1 = 0, pf_vo0 = 0, pf_vo1 = 0;
@@ -1411,7 +1409,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       cur_fast = nxt_fast;
       continue;
     }
-    {  // land the staged keys / values of the current block
+    {  // land the staged keys (plain) and values (swizzled block image at vlead)
       const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
       const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
 #pragma unroll
@@ -1419,30 +1417,36 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         if (l + 64 * i < nk) *reinterpret_cast<u32x4*>(L.kimg + (l + 64 * i) * 16) = kq[i];
 #pragma unroll
       for (uint32_t i = 0; i < 5; ++i)
-        if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.vimg + (l + 64 * i) * 16) = vq[i];
+        if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + swz((l + 64 * i) * 16)) = vq[i];
     }
     if (has_next) meta2(nxt);  // level-2 of the next block
     wave_sync();
-    // entry lanes: prefix, positions, non-value bytes and value edge bytes into oimg
-    // first key is at kimg[klead]; its end offset key_off[s + 1] is lane 0's prefetched pf_ko1
-    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf_ko1) - kb0;
-    const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of this block
+    // Phase 1, entry lanes: LCP against the first key, record positions (wave scan), tables,
+    // and the value bytes of each value's two partial edge chunks (captured in registers: the
+    // in-place move below overwrites the staged values).
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf_ko1) - kb0;  // first key at kimg[klead]
+    const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
     for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
     uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
 #pragma unroll
     for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
     uint32_t dc = 0;
-    for (uint32_t c = 0; c < n; c += 64) {
+    uint32_t eh[2][4], et[2][4];  // first / last 16 bytes of the value of entries l, l + 64
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+      const uint32_t c = 64 * it;
+      if (c >= n) break;
       const uint32_t k = c + l;
       uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
-      uint64_t tsv = 0;
       if (k < n) {
         uint32_t ko0, ko1, vo0, vo1;
-        if (c == 0) {  // prefetched one block ahead
-          ko0 = pf_ko0; ko1 = pf_ko1; vo0 = pf_vo0; vo1 = pf_vo1; tsv = pf_ts;
+        if (it == 0) {  // prefetched one block ahead
+          ko0 = pf_ko0; ko1 = pf_ko1; vo0 = pf_vo0; vo1 = pf_vo1;
+          L.ts[k] = pf_ts;
         } else {
           ko0 = a.key_off[s + k]; ko1 = a.key_off[s + k + 1];
-          vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1]; tsv = a.ts[s + k];
+          vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1];
+          L.ts[k] = a.ts[s + k];
         }
         kp = ko0 - kb0;
         kl = ko1 - ko0;
@@ -1474,57 +1478,37 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
             }
           }
         }
+        const uint32_t vs = vlead + vp;
+        sw_read16(L.img, vs, eh[it]);
+        sw_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
       }
       const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
       const uint32_t incl = wave_incl_scan<uint32_t>(dg);
       const uint32_t pos = dc + incl - dg;
       dc += __shfl(incl, 63, 64);
-      if (k < n && !(a.skip & 16)) {
-        const uint32_t sfx = kl - p;
-        uint8_t* o = L.oimg;
-        const uint32_t ox = olead + pos;
-        sw_be(o, ox, p & 0xFFFF, 2);
-        sw_be(o, ox + 2, sfx & 0xFFFF, 2);
-        const uint8_t* ks = L.kimg + klead + kp + p;
-        for (uint32_t t = 0; t < sfx; ++t) o[swz(ox + 4 + t)] = ks[t];
-        sw_be(o, ox + 4 + sfx, tsv, 8);
-        sw_be(o, ox + 12 + sfx, vl & 0xFFFF, 2);
-        const uint32_t A = olead + pos + 14 + sfx, Bv = A + vl;
-        const uint32_t a4 = (A + 3) & ~3u, b4 = Bv & ~3u;
-        const uint8_t* vs = L.vimg + vlead + vp;
-        if (a4 >= b4) {
-          for (uint32_t t = 0; t < vl; ++t) o[swz(A + t)] = vs[t];
-        } else {
-          for (uint32_t x = A; x < a4; ++x) o[swz(x)] = vs[x - A];
-          for (uint32_t x = b4; x < Bv; ++x) o[swz(x)] = vs[x - A];
-        }
-      }
       if (k < n) {
         const uint32_t sfx = kl - p;
-        L.epos[k] = pos;
-        L.vdst[k] = pos + 14 + sfx;
-        L.vend[k] = pos + 14 + sfx + vl;
-        L.vsrc[k] = vlead + vp;
-        // first image chunk whose start (16j - olead) is >= this value's start
+        L.epos[k] = uint16_t(pos);
+        L.pfx[k] = uint16_t(p);
+        L.ksrc[k] = uint16_t(klead + kp + p);
+        L.vdst[k] = uint16_t(pos + 14 + sfx);
+        L.vsrc[k] = uint16_t(vlead + vp);
+        L.vlen[k] = uint16_t(vl);
+        // first image chunk whose start is at or after this value's start
         const uint32_t j0 = (olead + pos + 14 + sfx + 15) >> 4;
-        if (j0 < ncs) atomicMax(&L.cent[j0], k);
+        if (j0 < ncs && vl) atomicMax(&L.cent[j0], k);
       }
     }
     const uint32_t data_len = dc;
     if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
-    wave_sync();
-    // offsets table + entry count (u16 BE, `as u16`)
-    for (uint32_t k = l; k < n; k += 64) sw_be(L.oimg, olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
-    if (l == 0) sw_be(L.oimg, olead + data_len + 2 * n, n & 0xFFFF, 2);
-    if (has_next) {  // next block's staging loads overlap this block's bulk copy + flush
+    if (has_next) {  // next block's staging loads overlap the rest of this block
       nxt_fast = is_fast(nxt);
       if (nxt_fast) issue(nxt);
     }
-    // value bulk: 16-B image chunks; a chunk inside one value is one 16-B LDS read + one
-    // ds_write_b128, otherwise its dwords that lie inside a value are copied one by one
-    // (the remaining value bytes were written by the entry lanes above).
-    if (!(a.skip & 32)) {
-      // pass 1: chunks lying inside one value (others skipped: no divergence)
+    wave_sync();
+    // Phase 2a (ascending): image chunk -> source byte of a chunk lying wholly inside one
+    // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
+    {
       uint32_t carry = 0;
       for (uint32_t c0 = 0; c0 < ncs; c0 += 64) {
         const uint32_t c = c0 + l;
@@ -1532,37 +1516,69 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         k = max(k, carry);
         carry = __builtin_amdgcn_readlane(k, 63);
         if (c >= ncs) continue;
-        const int32_t x = int32_t(16 * c) - int32_t(olead);
-        if (x >= int32_t(L.vdst[k]) && x + 16 <= int32_t(L.vend[k])) {
-          uint32_t v[4];
-          lds_read16(L.vimg, L.vsrc[k] + uint32_t(x - int32_t(L.vdst[k])), v);
-          u32x4 q = {v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<u32x4*>(L.oimg + swz(16 * c)) = q;
-        }
-      }
-      // pass 2 (entry lanes): whole dwords of the value inside its first and last chunk when
-      // those chunks are not wholly inside the value
-      for (uint32_t k = l; k < n; k += 64) {
-        const uint32_t A = olead + L.vdst[k], Bv = olead + L.vend[k];  // image byte range
-        if (Bv <= A) continue;
-        const uint32_t src0 = L.vsrc[k];
-        const uint32_t a4 = (A + 3) & ~3u, b4 = Bv & ~3u;
-        if (a4 >= b4) continue;  // no whole dword
-        const uint32_t ja = A >> 4, jb = (Bv - 1) >> 4;
-        // dword ranges [a4, min(b4, 16(ja+1))) and [max(a4, 16 jb), b4), de-duplicated;
-        // chunks wholly inside the value were written by pass 1 (skip those dwords)
-        const bool a_full = (A & 15) == 0 && (A + 16 <= Bv);
-        const bool b_full = ((Bv & 15) == 0) && (Bv - 16 >= A);
-        uint32_t lo1 = a4, hi1 = min(b4, 16 * (ja + 1));
-        uint32_t lo2 = max(a4, max(16 * jb, hi1)), hi2 = b4;
-        if (a_full) hi1 = lo1;
-        if (b_full) hi2 = lo2;
-        for (uint32_t x = lo1; x < hi1; x += 4)
-          *reinterpret_cast<uint32_t*>(L.oimg + swz(x)) = lds_dword_at(L.vimg, src0 + (x - A));
-        for (uint32_t x = lo2; x < hi2; x += 4)
-          *reinterpret_cast<uint32_t*>(L.oimg + swz(x)) = lds_dword_at(L.vimg, src0 + (x - A));
+        const int32_t x = int32_t(16 * c) - int32_t(olead);  // block byte of the chunk
+        const int32_t vd = int32_t(L.vdst[k]), ve = vd + int32_t(L.vlen[k]);
+        L.cent[c] = (k < n && x >= vd && x + 16 <= ve) ? uint32_t(L.vsrc[k]) + uint32_t(x - vd) : ~0u;
       }
     }
+    wave_sync();
+    // Phase 2b (descending): move whole-value chunks to their place in the encoded block.
+    // A value only moves up (its destination follows its own header and every earlier
+    // record), so walking the chunks from the top never overwrites a source still unread.
+    if (!(a.skip & 32)) {
+      const uint32_t top = (ncs + 63) & ~63u;
+      for (uint32_t c0 = top; c0 > 0; c0 -= 64) {
+        const uint32_t c = c0 - 64 + l;
+        const uint32_t src = c < ncs ? L.cent[c] : ~0u;
+        uint32_t v[4];
+        if (src != ~0u) sw_read16(L.img, src, v);
+        if (src != ~0u) *reinterpret_cast<u32x4*>(L.img + swz(16 * c)) = u32x4{v[0], v[1], v[2], v[3]};
+      }
+    }
+    wave_sync();
+    // Phase 3, entry lanes: header, key suffix, ts, value_len, and the value bytes of the
+    // partial edge chunks (from the registers captured in phase 1).
+    if (!(a.skip & 16)) {
+#pragma unroll
+      for (uint32_t it = 0; it < 2; ++it) {
+        const uint32_t k = 64 * it + l;
+        if (64 * it >= n) break;
+        if (k >= n) continue;
+        const uint32_t pos = L.epos[k], p = L.pfx[k], ks = L.ksrc[k], vd = L.vdst[k], vl = L.vlen[k];
+        const uint32_t sfx = vd - pos - 14;
+        const uint64_t tsv = L.ts[k];
+        uint8_t* o = L.img;
+        const uint32_t ox = olead + pos;
+        sw_be(o, ox, p & 0xFFFF, 2);
+        sw_be(o, ox + 2, sfx & 0xFFFF, 2);
+        for (uint32_t t = 0; t < sfx; ++t) o[swz(ox + 4 + t)] = L.kimg[ks + t];
+        sw_be(o, ox + 4 + sfx, tsv, 8);
+        sw_be(o, ox + 12 + sfx, vl & 0xFFFF, 2);
+        // value bytes outside whole chunks: [A, min(H, B)) and [max(T, H), B)
+        const uint32_t A = olead + vd, B = A + vl;
+        const uint32_t H = (A + 15) & ~15u, T = B & ~15u;
+        const uint32_t h_end = min(H, B), t_beg = max(T, H);
+        for (uint32_t x = A; x < h_end; ++x) {
+          const uint32_t u = x - A;  // < 16
+          o[swz(x)] = uint8_t(eh[it][u >> 2] >> (8 * (u & 3)));
+        }
+        if (vl >= 16) {
+          for (uint32_t x = t_beg; x < B; ++x) {
+            const uint32_t u = x + 16 - B;  // byte of the value's last 16
+            o[swz(x)] = uint8_t(et[it][u >> 2] >> (8 * (u & 3)));
+          }
+        } else {
+          for (uint32_t x = t_beg; x < B; ++x) {
+            const uint32_t u = x - A;  // a short value is wholly in its first 16 bytes
+            o[swz(x)] = uint8_t(eh[it][u >> 2] >> (8 * (u & 3)));
+          }
+        }
+      }
+    }
+    wave_sync();
+    // offsets table + entry count (u16 BE, `as u16`)
+    for (uint32_t k = l; k < n; k += 64) sw_be(L.img, olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
+    if (l == 0) sw_be(L.img, olead + data_len + 2 * n, n & 0xFFFF, 2);
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
     // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
@@ -1571,7 +1587,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
       const uint32_t end = olead + uint32_t(size);
       const uint32_t nc = (end + 15) >> 4;
       for (uint32_t c = l; c < nc; c += 64) {
-        const u32x4 q = *reinterpret_cast<const u32x4*>(L.oimg + swz(c * 16));
+        const u32x4 q = *reinterpret_cast<const u32x4*>(L.img + swz(c * 16));
         const uint32_t v[4] = {q.x, q.y, q.z, q.w};
         const uint32_t lo = 16 * c < olead ? olead - 16 * c : 0u;
         const uint32_t hi = min(end - 16 * c, 16u);
@@ -1899,7 +1915,10 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   e.skip = c->skip;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const uint32_t grid = uint32_t(cus) * 3;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
+    per_cu = 3;
+  const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
   hipLaunchKernelGGL(emit_kernel, dim3(grid), dim3(256), 0, st, e);
   if (c->timing) (void)hipEventRecord(c->ev[6], st);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
