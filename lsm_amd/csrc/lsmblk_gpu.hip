@@ -725,7 +725,7 @@ __global__ __launch_bounds__(256) void dec_count_kernel(CountArgs a) {
   const uint64_t tile = blockIdx.x;
   uint64_t tn = 0, tk = 0, tv = 0;
   uint32_t err = 0;
-#pragma unroll 1
+#pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
     const uint64_t b = tile * kTile + w * 16 + r * 4 + grp;
     uint32_t n = 0;
