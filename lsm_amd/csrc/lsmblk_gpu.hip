@@ -876,6 +876,16 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
 }
 
 // ================================================================ encode: plan
+// The greedy block walk of SsTableBuilder (table/builder.rs:48-65 over BlockBuilder::add,
+// block/builder.rs:54-73) in two passes:
+//   plan_adj_kernel   all entries in parallel: rec = klen + vlen, alcp = LCP with the
+//                     predecessor key, bit 31 set when the pair is out of order.
+//   plan_walk_kernel  one wave per segment walks the blocks over LDS chunks of (rec, alcp):
+//                     for non-decreasing keys LCP(first key, key_e) = min of alcp over
+//                     (first, e], so each block boundary is a min-scan, a sum-scan and a
+//                     ballot over 64 candidate entries; a block holding an out-of-order pair
+//                     compares with its first key directly.  Segment totals by decoupled
+//                     look-back, then the dense block tables.
 struct PlanArgs {
   const uint8_t* keys;
   const uint32_t* key_off;
@@ -884,8 +894,10 @@ struct PlanArgs {
   const uint32_t* seg_start;
   uint32_t nseg;
   uint32_t block_size;
+  uint32_t* rec;        // n: klen + vlen
+  uint32_t* alcp;       // n: see above
+  uint32_t* sz;         // scratch, n+1: encoded size per (segment-local) block
   uint32_t* rec_first;  // scratch, n+1
-  uint32_t* rec_size;   // scratch, n+1
   uint32_t* blk_first;  // dense, n+1
   uint64_t* blk_off;    // user, blk_cap
   uint64_t blk_cap, out_cap;
@@ -897,28 +909,14 @@ struct PlanArgs {
   uint32_t poll;
 };
 
-constexpr uint32_t kPlanWaves = 4;
-constexpr uint32_t kPlanW = 512;    // entries per LDS chunk
-constexpr uint32_t kPlanKB = 8192;  // key bytes per LDS chunk
+constexpr uint32_t kAlcpUnsorted = 0x80000000u;
+constexpr uint32_t kAlcpLcp = 0x7FFFFFFFu;
 
-struct alignas(16) PlanLds {
-  uint8_t keys[kPlanKB + 32];
-  uint32_t koff[kPlanW + 1];
-  uint32_t voff[kPlanW + 1];
-  uint32_t rec[kPlanW];   // klen + vlen
-  uint32_t alcp[kPlanW];  // LCP with the predecessor key | out-of-order flag << 31
-};
-
-// Key bytes of the batch, served from the LDS chunk when it holds them.
+// Key bytes of the batch through one descriptor over the whole key arena.
 struct PlanKeys {
-  rsrc_t gk;          // whole key arena, base aligned down to 4
-  uint32_t glead;     // keys pointer & 15 (descriptor base is 16-B aligned)
-  const uint8_t* lk;  // LDS chunk (16-aligned)
-  uint32_t lbase;     // arena offset of lk[llead]
-  uint32_t llead;
-  uint32_t lend;      // arena offset one past the chunk's last byte; 0-length if keys not staged
+  rsrc_t gk;       // whole key arena, base aligned down to 16
+  uint32_t glead;  // keys pointer & 15
   __device__ __forceinline__ uint32_t dword(uint32_t pos) const {  // 4 bytes at arena pos
-    if (pos >= lbase && pos + 4 <= lend) return lds_dword_at(lk, llead + (pos - lbase));
     const uint32_t x = glead + pos, al = x & ~3u;
     const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(gk, al, 0, 0);
     const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(gk, al + 4, 0, 0);
@@ -926,57 +924,63 @@ struct PlanKeys {
   }
 };
 
-// LCP of the key at arena position kp (length kl) against the first key (fp, fl), whose
-// first 32 bytes are held in wave-uniform registers fkw[].
-__device__ __forceinline__ uint32_t lcp_first(const PlanKeys& K, const uint32_t (&fkw)[8], uint32_t fp,
-                                              uint32_t fl, uint32_t kp, uint32_t kl) {
-  const uint32_t m = fl < kl ? fl : kl;
-  uint32_t p = m;
-  bool done = false;
-#pragma unroll
-  for (uint32_t c = 0; c < 8; ++c) {
-    if (!done && 4 * c < m) {
-      const uint32_t x = fkw[c] ^ K.dword(kp + 4 * c);
-      if (x) {
-        const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
-        p = q < m ? q : m;
-        done = true;
-      }
-    } else {
-      done = true;
-    }
-  }
-  if (!done) {
-    for (uint32_t c = 8; 4 * c < m; ++c) {
-      const uint32_t x = K.dword(fp + 4 * c) ^ K.dword(kp + 4 * c);
-      if (x) {
-        const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
-        p = q < m ? q : m;
-        break;
-      }
-    }
-  }
-  return p;
+__device__ __forceinline__ PlanKeys plan_keys(const PlanArgs& a) {
+  PlanKeys K;
+  K.glead = uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15);
+  K.gk = make_rsrc(a.keys - K.glead, K.glead + uni(a.key_off[a.n]));
+  return K;
 }
 
-// LCP beyond the first 16 bytes (both keys agree on bytes 0..15 and m > 16): dwords 4..7 of
-// the first key come from registers, further ones from memory.  Returns LCP - 16.
-__device__ __forceinline__ uint32_t lcp_first_tail(const PlanKeys& K, const uint32_t (&fkw)[8], uint32_t fp,
-                                                   uint32_t kp, uint32_t m) {
-  for (uint32_t c = 4; 4 * c < m; ++c) {
-    const uint32_t f = c < 8 ? fkw[c & 7] : K.dword(fp + 4 * c);
-    const uint32_t x = f ^ K.dword(kp + 4 * c);
-    if (x) {
-      const uint32_t q = 4 * c + (__builtin_ctz(x) >> 3);
-      return (q < m ? q : m) - 16;
+// LCP of keys (pp, pl) and (kp, kl); *w0 / *w1 = the dwords holding the first difference.
+__device__ __forceinline__ uint32_t key_lcp(const PlanKeys& K, uint32_t pp, uint32_t pl, uint32_t kp, uint32_t kl,
+                                            uint32_t& w0, uint32_t& w1) {
+  const uint32_t m = pl < kl ? pl : kl;
+  uint32_t lcp = m;
+  w0 = w1 = 0;
+  for (uint32_t d = 0; 4 * d < m; ++d) {
+    const uint32_t x0 = K.dword(pp + 4 * d), x1 = K.dword(kp + 4 * d);
+    if (x0 != x1) {
+      const uint32_t z = 4 * d + (__builtin_ctz(x0 ^ x1) >> 3);
+      if (z < m) {
+        lcp = z;
+        w0 = x0;
+        w1 = x1;
+      }
+      break;
     }
   }
-  return m - 16;
+  return lcp;
 }
 
-__global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
-  __shared__ PlanLds lds[kPlanWaves];
-  PlanLds& L = lds[threadIdx.x >> 6];
+__global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a) {
+  const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  uint32_t err = 0;
+  const PlanKeys K = plan_keys(a);
+  if (e < a.n) {
+    const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
+    a.rec[e] = kl + (a.val_off[e + 1] - a.val_off[e]);
+    uint32_t al = 0;
+    if (e > 0) {
+      const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
+      uint32_t w0, w1;
+      const uint32_t lcp = key_lcp(K, pp, pl, kp, kl, w0, w1);
+      const uint32_t m = pl < kl ? pl : kl, sh = 8 * (lcp & 3);
+      const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
+      al = (lcp < kAlcpLcp ? lcp : kAlcpLcp) | (sorted ? 0u : kAlcpUnsorted);
+    }
+    a.alcp[e] = al;
+    if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
+  }
+  err = __ballot(err != 0) ? LSMBLK_ERR_EMPTY_KEY : 0u;
+  raise_err(a.stats, err);
+}
+
+constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
+
+__global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a) {
+  __shared__ uint32_t crec[4][kWalk], calcp[4][kWalk];
+  uint32_t* CR = crec[threadIdx.x >> 6];
+  uint32_t* CA = calcp[threadIdx.x >> 6];
   const uint32_t l = lane_id();
   const uint32_t g = take_ticket(a.ticket);
   if (g >= a.nseg) return;
@@ -987,147 +991,71 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     s1 = s0 = (s0 > a.n ? uint32_t(a.n) : s0);
     if (s1 < s0) s1 = s0;
   }
-  const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys);
-  PlanKeys K;
-  K.glead = uint32_t(kaddr & 15);
-  const uint32_t ktotal = uni(a.key_off[a.n]);
-  K.gk = make_rsrc(a.keys - K.glead, K.glead + ktotal);
-  K.lk = L.keys;
-  K.lbase = K.lend = 0;
-  K.llead = 0;
-  uint32_t c0 = 0, c1 = 0;  // chunk covers entries [c0, c1) with offsets [c0, c1]
-
-  // A chunk = offsets, key bytes and the per-entry walk inputs of up to kPlanW entries.  All of
-  // its global loads are issued before the first LDS write (<= 9 + 9 offset values and <= 9
-  // key chunks per lane).  Then, all lanes in parallel: rec = klen + vlen and alcp = LCP of
-  // the key with its predecessor in the segment, bit 31 set when the pair is out of order.
-  // For keys in non-decreasing order LCP(first, key_e) = min of alcp over (first, e], which
-  // turns the serial block walk into two wave scans over LDS words.
+  const PlanKeys K = plan_keys(a);
+  uint32_t c0 = 0, c1 = 0;  // LDS chunk = entries [c0, c1)
   auto load_chunk = [&](uint32_t from) {
     c0 = from;
-    c1 = (s1 - from) < kPlanW ? s1 : from + kPlanW;
-    const uint32_t cnt = c1 - c0 + 1;
-    uint32_t ko[9], vo[9];
+    c1 = s1 - from < kWalk ? s1 : from + kWalk;
+    uint32_t r[kWalk / 64], q[kWalk / 64];
 #pragma unroll
-    for (uint32_t i = 0; i < 9; ++i) {
-      const uint32_t j = l + 64 * i;
-      if (j < cnt) {
-        ko[i] = a.key_off[c0 + j];
-        vo[i] = a.val_off[c0 + j];
-      }
-    }
-    // predecessor of the chunk's first entry (its key is outside the chunk)
-    const uint32_t kprev = c0 > s0 ? uni(a.key_off[c0 - 1]) : 0u;
-#pragma unroll
-    for (uint32_t i = 0; i < 9; ++i) {
-      const uint32_t j = l + 64 * i;
-      if (j < cnt) {
-        L.koff[j] = ko[i];
-        L.voff[j] = vo[i];
+    for (uint32_t i = 0; i < kWalk / 64; ++i) {
+      const uint32_t j = c0 + 64 * i + l;
+      if (j < c1) {
+        r[i] = a.rec[j];
+        q[i] = a.alcp[j];
       }
     }
     wave_sync();
-    const uint32_t kb0 = uni(L.koff[0]), kb1 = uni(L.koff[c1 - c0]);
-    const uint32_t al = (K.glead + kb0) & ~15u, llead = (K.glead + kb0) & 15u;
-    if (llead + (kb1 - kb0) + 8 <= kPlanKB + 32 - 8) {
-      const rsrc_t R = K.gk;
-      const uint32_t nchunk = (llead + (kb1 - kb0) + 15) >> 4;
-      u32x4 q[9];
 #pragma unroll
-      for (uint32_t i = 0; i < 9; ++i)
-        if (l + 64 * i < nchunk) q[i] = __builtin_amdgcn_raw_buffer_load_b128(R, al + (l + 64 * i) * 16, 0, 0);
-#pragma unroll
-      for (uint32_t i = 0; i < 9; ++i)
-        if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.keys + (l + 64 * i) * 16) = q[i];
-      K.lbase = kb0;
-      K.llead = llead;
-      K.lend = kb1;
-    } else {
-      K.lbase = K.lend = 0;  // keys from global
-    }
-    wave_sync();
-    for (uint32_t j = l; j < c1 - c0; j += 64) {
-      const uint32_t e = c0 + j;
-      const uint32_t kp = L.koff[j], kl = L.koff[j + 1] - kp;
-      uint32_t alcp = 0;
-      if (e > s0) {
-        const uint32_t pp = j ? L.koff[j - 1] : kprev, pl = kp - pp;
-        const uint32_t m = pl < kl ? pl : kl;
-        uint32_t lcp = m, w0 = 0, w1 = 0;
-        for (uint32_t d = 0; 4 * d < m; ++d) {
-          const uint32_t x0 = K.dword(pp + 4 * d), x1 = K.dword(kp + 4 * d);
-          if (x0 != x1) {
-            const uint32_t z = 4 * d + (__builtin_ctz(x0 ^ x1) >> 3);
-            if (z < m) {
-              lcp = z;
-              w0 = x0;
-              w1 = x1;
-            }
-            break;
-          }
-        }
-        const uint32_t sh = 8 * (lcp & 3);
-        const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
-        alcp = lcp | (sorted ? 0u : 0x80000000u);
-        if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
-      } else if (kl == 0) {
-        err |= LSMBLK_ERR_EMPTY_KEY;
+    for (uint32_t i = 0; i < kWalk / 64; ++i) {
+      const uint32_t j = 64 * i + l;
+      if (c0 + j < c1) {
+        CR[j] = r[i];
+        CA[j] = q[i];
       }
-      L.rec[j] = kl + (L.voff[j + 1] - L.voff[j]);
-      L.alcp[j] = alcp;
     }
     wave_sync();
   };
-
   uint32_t nb = 0;
   uint64_t bytes = 0;
-  uint32_t s = s0;
   const uint64_t bs = a.block_size;
-  while (s < s1) {
-    if (!(s >= c0 && s < c1)) load_chunk(s);
-    // first key of this block (used only by the direct-LCP fallback for unsorted windows)
-    const uint32_t fp = uni(L.koff[s - c0]), fl = uni(L.koff[s - c0 + 1]) - fp;
-    bool have_fkw = false, direct = false;
-    uint32_t fkw[8];
-    uint64_t carry = 2;         // estimated_size() of an empty builder
-    uint32_t pmin = 0x7FFFFFFFu;  // running min of alcp over (s, window start)
-    uint32_t j0 = s;
-    for (;;) {
-      const uint32_t wend = (s1 - j0) < 64 ? s1 : j0 + 64;
+  for (uint32_t s = s0; s < s1;) {
+    uint64_t carry = 2;           // estimated_size() of an empty builder
+    uint32_t pmin = kAlcpLcp;     // running min of alcp over (s, window start)
+    bool direct = false;
+    uint32_t sp = 0, sl = 0;      // key_s (direct compares only)
+    for (uint32_t j0 = s;; j0 += 64) {
+      const uint32_t wend = s1 - j0 < 64 ? s1 : j0 + 64;
       if (!(j0 >= c0 && wend <= c1)) load_chunk(j0);
       const uint32_t e = j0 + l;
       const bool valid = e < s1;
-      uint32_t rec = 0, al = 0x7FFFFFFFu;
+      uint32_t r = 0, al = kAlcpLcp;
       if (valid) {
-        rec = L.rec[e - c0];
-        if (e != s) al = L.alcp[e - c0];
+        r = CR[e - c0];
+        if (e != s) al = CA[e - c0];
       }
-      direct = direct || __ballot(al >> 31) != 0;  // an out-of-order pair inside this block
+      if (!direct && __ballot(al & kAlcpUnsorted)) {  // an out-of-order pair inside this block
+        direct = true;
+        sp = a.key_off[s];
+        sl = a.key_off[s + 1] - sp;
+      }
       uint32_t p = 0;
       if (!direct) {
-        p = min(pmin, wave_incl_min31(al));
-        if (e == s) p = 0;
-      } else {
-        if (!have_fkw) {
-#pragma unroll
-          for (uint32_t c = 0; c < 8; ++c) fkw[c] = 4 * c < fl ? uni(K.dword(fp + 4 * c)) : 0u;
-          have_fkw = true;
-        }
-        if (valid && e != s) {
-          const uint32_t kp = L.koff[e - c0], kl = L.koff[e - c0 + 1] - kp;
-          p = lcp_first(K, fkw, fp, fl, kp, kl);
-        }
+        p = min(pmin, wave_incl_min31(al & kAlcpLcp));
+        pmin = __builtin_amdgcn_readlane(p, 63);
+      } else if (valid && e != s) {
+        const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
+        uint32_t w0, w1;
+        p = key_lcp(K, sp, sl, kp, kl, w0, w1);
       }
-#ifdef LSMBLK_PLAN_DEBUG
-      if (g == 0 && valid) printf("e=%u s=%u al=%x p=%u rec=%u direct=%d pmin=%u\n", e, s, al, p, rec, (int)direct, pmin);
-#endif
-      const uint64_t gr = valid ? uint64_t(rec) + 16 - p : 0;  // data growth + offset slot
+      if (e == s) p = 0;
+      const uint64_t gr = valid ? uint64_t(r) + 16 - p : 0;  // data growth + offset slot
       // u32 DPP scan when every lane's growth is < 2^25 (sum fits), else the 64-bit scan
       const uint64_t incl = __ballot(gr >= (1u << 25)) == 0 ? uint64_t(wave_incl_scan32(uint32_t(gr)))
                                                              : wave_incl_scan<uint64_t>(gr);
       const uint64_t before = carry + incl - gr;  // estimated_size() before adding e
       // builder.rs:56-60: reject when est + raw_len + vlen + 6 > block_size (not first entry)
-      const bool stop = !valid || (e != s && before + rec + 14 > bs);
+      const bool stop = !valid || (e != s && before + r + 14 > bs);
       const uint64_t m = __ballot(stop);
       if (m) {
         const uint32_t f = uint32_t(__builtin_ctzll(m));
@@ -1135,7 +1063,7 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
                               __builtin_amdgcn_readlane(uint32_t(before), f);
         if (l == 0) {
           a.rec_first[s0 + nb] = s;
-          a.rec_size[s0 + nb] = uint32_t(size);
+          a.sz[s0 + nb] = uint32_t(size);
         }
         ++nb;
         bytes += size;
@@ -1144,11 +1072,12 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
       }
       carry += (uint64_t(__builtin_amdgcn_readlane(uint32_t(incl >> 32), 63)) << 32) |
                __builtin_amdgcn_readlane(uint32_t(incl), 63);
-      pmin = __builtin_amdgcn_readlane(p, 63);
-      j0 += 64;
     }
   }
-
+  // make this wave's record stores visible to its own later loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // segment totals -> dense block numbering and output offsets
   uint64_t agg[2] = {nb, bytes};
   uint64_t excl[2] = {0, 0};
@@ -1160,18 +1089,14 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     const uint64_t inc[2] = {excl[0] + agg[0], excl[1] + agg[1]};
     publish<2>(a.inc, g, inc, a.tag, 2, a.poll);
   }
-  // make this wave's record stores visible to its own later loads
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const uint64_t B0 = excl[0], O0 = excl[1];
   uint64_t oc = O0;
   for (uint32_t c = 0; c < nb; c += 64) {
     const uint32_t i = c + l;
     uint32_t sz = 0, first = 0;
     if (i < nb) {
-      sz = a.rec_size[s0 + i];
       first = a.rec_first[s0 + i];
+      sz = a.sz[s0 + i];
     }
     const uint64_t incl = wave_incl_scan<uint64_t>(sz);
     if (i < nb) {
@@ -1625,8 +1550,8 @@ struct lsmblk_ctx {
   uint64_t* seg_inc = nullptr;
   uint64_t seg_cap = 0;
   uint32_t* rec_first = nullptr; // n+1
-  uint32_t* rec_size = nullptr;
   uint32_t* blk_first = nullptr;
+  uint32_t* ent = nullptr;       // 3 per entry: rec, alcp, block sizes (plan passes)
   uint64_t rec_cap = 0;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
@@ -1690,9 +1615,9 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
     cap = c->rec_cap;
     if ((rc = grow(&c->rec_first, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
-    if ((rc = grow(&c->rec_size, &cap, entries + 1, 1))) return rc;
-    cap = c->rec_cap;
     if ((rc = grow(&c->blk_first, &cap, entries + 1, 1))) return rc;
+    cap = c->rec_cap;
+    if ((rc = grow(&c->ent, &cap, entries + 1, 3))) return rc;
     c->rec_cap = cap;
   }
   return LSMBLK_OK;
@@ -1744,7 +1669,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->seg_agg);
   (void)hipFree(c->seg_inc);
   (void)hipFree(c->rec_first);
-  (void)hipFree(c->rec_size);
+  (void)hipFree(c->ent);
   (void)hipFree(c->blk_first);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1882,8 +1807,11 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   p.seg_start = seg_start;
   p.nseg = nseg;
   p.block_size = block_size;
+  const uint64_t ecap = c->rec_cap;  // rows of the per-entry plan arrays
+  p.rec = c->ent;
+  p.alcp = c->ent + ecap;
+  p.sz = c->ent + 2 * ecap;
   p.rec_first = c->rec_first;
-  p.rec_size = c->rec_size;
   p.blk_first = c->blk_first;
   p.blk_off = blk_off;
   p.blk_cap = blk_cap;
@@ -1896,7 +1824,11 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   p.poll = c->poll;
   c->enc_timed = c->timing;
   if (c->timing) (void)hipEventRecord(c->ev[4], st);
-  hipLaunchKernelGGL(plan_kernel, dim3((nseg + kPlanWaves - 1) / kPlanWaves), dim3(256), 0, st, p);
+  if (in->n) {
+    const uint32_t eg = uint32_t((in->n + 255) / 256);
+    hipLaunchKernelGGL(plan_adj_kernel, dim3(eg), dim3(256), 0, st, p);
+  }
+  hipLaunchKernelGGL(plan_walk_kernel, dim3((nseg + 3) / 4), dim3(256), 0, st, p);
   if (c->timing) (void)hipEventRecord(c->ev[5], st);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   EmitArgs e;
