@@ -1148,9 +1148,20 @@ struct alignas(16) EmitLds {
   uint64_t ts[kEmitMaxE];
 };
 
-// big-endian field of nbytes at byte x of a swizzled LDS image
-__device__ __forceinline__ void sw_be(uint8_t* base, uint32_t x, uint64_t v, int nbytes) {
-  for (int i = 0; i < nbytes; ++i) base[swz(x + i)] = uint8_t(v >> (8 * (nbytes - 1 - i)));
+// bytes [0, len) (len < 16) of v at an unaligned LDS address: overlapping stores of the widest
+// size that fits (8 + 8, 4 + 4, or single bytes)
+__device__ __forceinline__ void lds_st_short(uint8_t* p, uint32_t len, const uint32_t (&v)[4]) {
+  if (len >= 8) {
+    const uint32_t x = len - 8, sh = x & 3;
+    const uint32_t w0 = x < 4 ? v[0] : v[1], w1 = x < 4 ? v[1] : v[2], w2 = x < 4 ? v[2] : v[3];
+    *reinterpret_cast<u32x2*>(p) = u32x2{v[0], v[1]};
+    *reinterpret_cast<u32x2*>(p + x) = u32x2{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh)};
+  } else if (len >= 4) {
+    *reinterpret_cast<uint32_t*>(p) = v[0];
+    *reinterpret_cast<uint32_t*>(p + len - 4) = __builtin_amdgcn_alignbyte(v[1], v[0], len - 4);
+  } else {
+    for (uint32_t i = 0; i < len; ++i) p[i] = uint8_t(v[0] >> (8 * i));
+  }
 }
 
 // Global byte readers for the simple path.
@@ -1342,7 +1353,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         if (l + 64 * i < nk) *reinterpret_cast<u32x4*>(L.kimg + (l + 64 * i) * 16) = kq[i];
 #pragma unroll
       for (uint32_t i = 0; i < 5; ++i)
-        if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + swz((l + 64 * i) * 16)) = vq[i];
+        if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = vq[i];
     }
     if (has_next) meta2(nxt);  // level-2 of the next block
     wave_sync();
@@ -1404,8 +1415,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
           }
         }
         const uint32_t vs = vlead + vp;
-        sw_read16(L.img, vs, eh[it]);
-        sw_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
+        lds_read16(L.img, vs, eh[it]);
+        lds_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
       }
       const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
       const uint32_t incl = wave_incl_scan<uint32_t>(dg);
@@ -1456,8 +1467,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         const uint32_t c = c0 - 64 + l;
         const uint32_t src = c < ncs ? L.cent[c] : ~0u;
         uint32_t v[4];
-        if (src != ~0u) sw_read16(L.img, src, v);
-        if (src != ~0u) *reinterpret_cast<u32x4*>(L.img + swz(16 * c)) = u32x4{v[0], v[1], v[2], v[3]};
+        if (src != ~0u) lds_read16(L.img, src, v);
+        if (src != ~0u) *reinterpret_cast<u32x4*>(L.img + 16 * c) = u32x4{v[0], v[1], v[2], v[3]};
       }
     }
     wave_sync();
@@ -1472,38 +1483,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         const uint32_t pos = L.epos[k], p = L.pfx[k], ks = L.ksrc[k], vd = L.vdst[k], vl = L.vlen[k];
         const uint32_t sfx = vd - pos - 14;
         const uint64_t tsv = L.ts[k];
+        // unaligned LDS stores (the image is not swizzled): every field is one or two stores
         uint8_t* o = L.img;
         const uint32_t ox = olead + pos;
-        sw_be(o, ox, p & 0xFFFF, 2);
-        sw_be(o, ox + 2, sfx & 0xFFFF, 2);
-        for (uint32_t t = 0; t < sfx; ++t) o[swz(ox + 4 + t)] = L.kimg[ks + t];
-        sw_be(o, ox + 4 + sfx, tsv, 8);
-        sw_be(o, ox + 12 + sfx, vl & 0xFFFF, 2);
-        // value bytes outside whole chunks: [A, min(H, B)) and [max(T, H), B)
-        const uint32_t A = olead + vd, B = A + vl;
-        const uint32_t H = (A + 15) & ~15u, T = B & ~15u;
-        const uint32_t h_end = min(H, B), t_beg = max(T, H);
-        for (uint32_t x = A; x < h_end; ++x) {
-          const uint32_t u = x - A;  // < 16
-          o[swz(x)] = uint8_t(eh[it][u >> 2] >> (8 * (u & 3)));
+        *reinterpret_cast<uint32_t*>(o + ox) = bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16);
+        for (uint32_t t = 0; t < sfx; t += 16) {
+          const uint32_t o2 = sfx >= 16 ? min(t, sfx - 16) : 0u;
+          uint32_t v[4];
+          lds_read16(L.kimg, ks + o2, v);
+          if (sfx >= 16) *reinterpret_cast<u32x4*>(o + ox + 4 + o2) = u32x4{v[0], v[1], v[2], v[3]};
+          else lds_st_short(o + ox + 4, sfx, v);
         }
+        const uint64_t tbe = __builtin_bswap64(tsv);
+        *reinterpret_cast<u32x2*>(o + ox + 4 + sfx) = u32x2{uint32_t(tbe), uint32_t(tbe >> 32)};
+        *reinterpret_cast<uint16_t*>(o + ox + 12 + sfx) = uint16_t(bswap16(vl & 0xFFFF));
+        // value bytes outside whole chunks: a value of >= 16 bytes rewrites its first and last
+        // 16 (the bytes inside whole chunks are rewritten with what the move put there)
+        const uint32_t A = olead + vd;
         if (vl >= 16) {
-          for (uint32_t x = t_beg; x < B; ++x) {
-            const uint32_t u = x + 16 - B;  // byte of the value's last 16
-            o[swz(x)] = uint8_t(et[it][u >> 2] >> (8 * (u & 3)));
-          }
-        } else {
-          for (uint32_t x = t_beg; x < B; ++x) {
-            const uint32_t u = x - A;  // a short value is wholly in its first 16 bytes
-            o[swz(x)] = uint8_t(eh[it][u >> 2] >> (8 * (u & 3)));
-          }
+          *reinterpret_cast<u32x4*>(o + A) = u32x4{eh[it][0], eh[it][1], eh[it][2], eh[it][3]};
+          *reinterpret_cast<u32x4*>(o + A + vl - 16) = u32x4{et[it][0], et[it][1], et[it][2], et[it][3]};
+        } else if (vl) {
+          lds_st_short(o + A, vl, eh[it]);
         }
       }
     }
     wave_sync();
     // offsets table + entry count (u16 BE, `as u16`)
-    for (uint32_t k = l; k < n; k += 64) sw_be(L.img, olead + data_len + 2 * k, L.epos[k] & 0xFFFF, 2);
-    if (l == 0) sw_be(L.img, olead + data_len + 2 * n, n & 0xFFFF, 2);
+    for (uint32_t k = l; k < n; k += 64)
+      *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.epos[k] & 0xFFFF));
+    if (l == 0) *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * n) = uint16_t(bswap16(n & 0xFFFF));
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
     // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
@@ -1512,7 +1521,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       const uint32_t end = olead + uint32_t(size);
       const uint32_t nc = (end + 15) >> 4;
       for (uint32_t c = l; c < nc; c += 64) {
-        const u32x4 q = *reinterpret_cast<const u32x4*>(L.img + swz(c * 16));
+        const u32x4 q = *reinterpret_cast<const u32x4*>(L.img + c * 16);
         const uint32_t v[4] = {q.x, q.y, q.z, q.w};
         const uint32_t lo = 16 * c < olead ? olead - 16 * c : 0u;
         const uint32_t hi = min(end - 16 * c, 16u);
