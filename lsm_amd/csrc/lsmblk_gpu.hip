@@ -224,23 +224,21 @@ __device__ __forceinline__ void raise_err(uint64_t* stats, uint32_t err) {
 // ---------------------------------------------------------------- byte sources
 // An "image" is a block's bytes addressed block-relative; LdsImg reads the LDS staging copy,
 // GlbImg reads global memory through a bounds-checked buffer descriptor (OOB reads = 0).
-// LDS image swizzle (decode block image, emit output image): 16-B granule g of 128-B row r
-// is stored at granule g ^ (r & 7).  U-config entries are exactly 128 B apart (16-B keys,
-// p = 2, 100-B values), so without it per-entry-lane accesses at one field offset all hit
-// one bank (32-way conflicts); with it they spread over 8 granules.  Granules stay whole, so
-// b128 staging writes / flush reads and 8-B aligned b64 reads are unaffected.
-__device__ __forceinline__ uint32_t swz(uint32_t x) { return x ^ ((x >> 3) & 0x70u); }
-
+// Decode reads the (unswizzled) LDS image with unaligned ds_read_u16/b32/b64/b128 (the gfx9
+// unaligned access mode): one instruction per field instead of one per byte.
 struct LdsImg {
-  const uint8_t* base;  // swizzled LDS image; block byte 0 is image byte lead
+  const uint8_t* base;  // LDS image; block byte 0 is image byte lead
   uint32_t lead;
-  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return base[swz(lead + i)]; }
-  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return base[lead + i]; }
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const {
+    return bswap16(*reinterpret_cast<const uint16_t*>(base + lead + i));
+  }
+  __device__ __forceinline__ uint32_t le32(uint32_t i) const {
+    return *reinterpret_cast<const uint32_t*>(base + lead + i);
+  }
   __device__ __forceinline__ uint64_t u64(uint32_t i) const {
-    uint64_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v = (v << 8) | u8(i + j);
-    return v;
+    const u32x2 q = *reinterpret_cast<const u32x2*>(base + lead + i);
+    return __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
   }
 };
 struct GlbImg {
@@ -250,6 +248,9 @@ struct GlbImg {
     return __builtin_amdgcn_raw_buffer_load_b8(r, lead + i, 0, 0);
   }
   __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
+  __device__ __forceinline__ uint32_t le32(uint32_t i) const {
+    return u8(i) | (u8(i + 1) << 8) | (u8(i + 2) << 16) | (u8(i + 3) << 24);
+  }
   __device__ __forceinline__ uint64_t u64(uint32_t i) const {
     uint64_t v = 0;
 #pragma unroll
@@ -263,14 +264,6 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x
   const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
   const uint32_t i = x >> 2;
   return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
-}
-
-// 4 bytes starting at byte offset x of a swizzled LDS image.
-__device__ __forceinline__ uint32_t sw_dword_at(const uint8_t* base, uint32_t x) {
-  const uint32_t x4 = x & ~3u;
-  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(base + swz(x4));
-  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(base + swz(x4 + 4));
-  return __builtin_amdgcn_alignbyte(w1, w0, x & 3);
 }
 
 // Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
@@ -350,22 +343,6 @@ __device__ __forceinline__ void lds_read16(const uint8_t* base, uint32_t x, uint
   v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
 }
 
-// lds_read16 on a swizzled image (8-B pieces never straddle a 16-B granule)
-__device__ __forceinline__ void sw_read16(const uint8_t* base, uint32_t x, uint32_t (&v)[4]) {
-  const uint32_t x8 = x & ~7u;
-  const uint2 q0 = *reinterpret_cast<const uint2*>(base + swz(x8));
-  const uint2 q1 = *reinterpret_cast<const uint2*>(base + swz(x8 + 8));
-  const uint2 q2 = *reinterpret_cast<const uint2*>(base + swz(x8 + 16));
-  const uint32_t sh = x & 3;
-  const bool hi = (x & 4) != 0;
-  const uint32_t w0 = hi ? q0.y : q0.x, w1 = hi ? q1.x : q0.y, w2 = hi ? q1.y : q1.x;
-  const uint32_t w3 = hi ? q2.x : q1.y, w4 = hi ? q2.y : q2.x;
-  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
-  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
-}
-
 struct BlockHdr {
   uint32_t len, n, data_end, fks;
   bool ok;
@@ -393,8 +370,9 @@ __device__ __forceinline__ bool parse_entry(const Img& im, const BlockHdr& h, ui
                                             uint32_t& off, uint32_t& p, uint32_t& s, uint32_t& vl) {
   off = im.u16(h.data_end + 2 * k);
   bool ok = off + 4 <= h.data_end;
-  p = im.u16(off);
-  s = im.u16(off + 2);
+  const uint32_t w = im.le32(off);  // BE16 p | BE16 s
+  p = bswap16(w & 0xFFFF);
+  s = bswap16(w >> 16);
   ok = ok && (off + 4 + s + 10 <= h.data_end) && (p <= h.fks) && (p + s > 0);
   vl = im.u16(off + 12 + s);
   ok = ok && (off + 14 + s + vl <= h.data_end);
@@ -513,28 +491,39 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
     const uint32_t sb = lead + epos + 4;  // image byte of the suffix
     if (!(skip & 8)) {
       const uint64_t e = E0 + k;
-      const uint32_t lo = sw_dword_at(img, sb + s), hi = sw_dword_at(img, sb + s + 4);
-      a.ts[e] = __builtin_bswap64((uint64_t(hi) << 32) | lo);
+      const u32x2 q = *reinterpret_cast<const u32x2*>(img + sb + s);
+      a.ts[e] = __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
       a.key_off[e] = uint32_t(K0 + kout);
       a.val_off[e] = uint32_t(V0 + vout);
     }
     if (!(skip & 2)) {
-      // key byte x = first key byte x (x < p) or suffix byte x - p; a dword straddling p
-      // merges the two under a byte mask
+      // key byte x = first key byte x (x < p) or suffix byte x - p: a 16-B piece is one
+      // unaligned read of each, merged under a per-dword byte mask
       const uint32_t kl = p + s;
-      auto kdw = [&](uint32_t x) -> uint32_t {
-        const uint32_t sw = sw_dword_at(img, sb + x - p);
-        if (x >= p) return sw;
-        const uint32_t fw = sw_dword_at(img, fk + x);
-        if (x + 4 <= p) return fw;
-        const uint32_t m = (1u << (8 * (p - x))) - 1;
-        return (fw & m) | (sw & ~m);
-      };
       for (uint32_t t = 0; t < kl; t += 16) {
         const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
         uint32_t v[4];
+        if (sb + o >= p) {
+          const u32x4 sq = *reinterpret_cast<const u32x4*>(img + sb + o - p);
+          const u32x4 fq = *reinterpret_cast<const u32x4*>(img + fk + o);
+          const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w}, fv[4] = {fq.x, fq.y, fq.z, fq.w};
 #pragma unroll
-        for (uint32_t d = 0; d < 4; ++d) v[d] = kdw(o + 4 * d);
+          for (uint32_t d = 0; d < 4; ++d) {
+            const int32_t nf = int32_t(p) - int32_t(o + 4 * d);  // leading bytes from the first key
+            const uint32_t m = nf <= 0 ? 0u : nf >= 4 ? ~0u : (1u << (8 * nf)) - 1;
+            v[d] = (fv[d] & m) | (sv[d] & ~m);
+          }
+        } else {  // suffix before the image start (a prefix longer than the entry offset)
+#pragma unroll
+          for (uint32_t d = 0; d < 4; ++d) {
+            uint32_t wd = 0;
+            for (uint32_t i = 0; i < 4; ++i) {
+              const uint32_t x = o + 4 * d + i;
+              wd |= uint32_t(x < p ? img[fk + x] : img[sb + x - p]) << (8 * i);
+            }
+            v[d] = wd;
+          }
+        }
         if (kl >= 16) out.put16(false, kout + o, v);
         else out.put_short(false, kout, kl, v);
       }
@@ -543,8 +532,8 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
       const uint32_t src = sb + s + 10;  // image byte of the value
       for (uint32_t t = 0; t < vl; t += 16) {
         const uint32_t o = vl >= 16 ? min(t, vl - 16) : 0u;
-        uint32_t v[4];
-        sw_read16(img, src + o, v);
+        const u32x4 q = *reinterpret_cast<const u32x4*>(img + src + o);
+        const uint32_t v[4] = {q.x, q.y, q.z, q.w};
         if (vl >= 16) out.put16(true, vout + o, v);
         else out.put_short(true, vout, vl, v);
       }
@@ -614,7 +603,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
       if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + swz((l + 64 * i) * 16)) = v[i];
+      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
     wave_sync();
     h = parse_hdr(LdsImg{L.img, lead}, len);
   } else {
