@@ -47,6 +47,11 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_re
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return (uint64_t(uni(uint32_t(x >> 32))) << 32) | uni(uint32_t(x));
 }
+// lane j's x (readlane returns int: both halves go through uint32_t, no sign extension)
+__device__ __forceinline__ uint64_t lane64(uint64_t x, uint32_t j) {
+  return (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), j))) << 32) |
+         uint32_t(__builtin_amdgcn_readlane(uint32_t(x), j));
+}
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1048,8 +1053,7 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a) {
       const uint64_t m = __ballot(stop);
       if (m) {
         const uint32_t f = uint32_t(__builtin_ctzll(m));
-        const uint64_t size = (uint64_t(__builtin_amdgcn_readlane(uint32_t(before >> 32), f)) << 32) |
-                              __builtin_amdgcn_readlane(uint32_t(before), f);
+        const uint64_t size = lane64(before, f);
         if (l == 0) {
           a.rec_first[s0 + nb] = s;
           a.sz[s0 + nb] = uint32_t(size);
@@ -1059,8 +1063,7 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a) {
         s = j0 + f;
         break;
       }
-      carry += (uint64_t(__builtin_amdgcn_readlane(uint32_t(incl >> 32), 63)) << 32) |
-               __builtin_amdgcn_readlane(uint32_t(incl), 63);
+      carry += lane64(incl, 63);
     }
   }
   // make this wave's record stores visible to its own later loads

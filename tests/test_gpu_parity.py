@@ -111,6 +111,24 @@ def test_unaligned_block_stream():
     roundtrip_check(kv, [0, kv.n], 4096, shift=3)
 
 
+def test_block_offsets_beyond_2gib_and_4gib():
+    """blk_off values past 2**31 and 2**32: byte offsets are u64 end to end (a readlane of
+    the low half into a u64 once sign-extended bit 31 in an experimental decode)."""
+    kv = O.KV(*synth.gen_uniform(20000, seed=5))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 256 << 10)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, 4096)
+    assert rc == 0
+    rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
+    assert rc == 0
+    for base in ((1 << 31) - 5000, (1 << 32) + 3):
+        buf = torch.zeros(base + len(ref_blocks) + 16, dtype=torch.uint8, device="cuda")
+        buf[base:base + len(ref_blocks)] = torch.from_numpy(ref_blocks).cuda()
+        off = torch.from_numpy((ref_off.astype(np.uint64) + np.uint64(base)).view(np.int64)).cuda()
+        assert_kv_equal(batch.decode_blocks(buf, off), ref_kv)
+        del buf, off
+        torch.cuda.empty_cache()
+
+
 def test_unaligned_key_and_value_arenas():
     kv = O.KV(*synth.gen_zipf(5000, seed=5))
     rc, ref_blocks, ref_off = O.encode_segments(kv, [0, kv.n], 4096)
