@@ -175,6 +175,16 @@ int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint3
                         uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
                         uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, void* stream);
 
+/* SST block framing (SURVEY.md §8 f, row 1): crc[b] = crc32fast::hash(block b) for block
+ * b = blocks[blk_off[b] .. blk_off[b+1]) -- the checksum SsTableBuilder::finish_block appends
+ * after every encoded block as a big-endian u32 (src/table/builder.rs:120-122) and
+ * SsTable::read_block verifies before Block::decode (src/table.rs:219-230).  CRC-32/ISO-HDLC
+ * (reflected 0xEDB88320, init and xorout 0xFFFFFFFF); an empty block's CRC is 0.
+ * stats: [0] blocks [1] bytes [3] error flags (LSMBLK_ERR_MALFORMED: a block's offsets are
+ * decreasing or it exceeds 2 GiB; its crc is then 0).  Asynchronous like the calls above. */
+int lsmblk_crc32_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off,
+                       uint64_t nblk, uint32_t* crc, uint64_t* stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,6 +4,8 @@
                  batch of blocks (reference src/table.rs:213-233, src/table/iterator.rs:86-97)
   encode_kv      replaces SsTableBuilder::add -> BlockBuilder::add / finish_block over a batch
                  of segments (reference src/table/builder.rs:48-65,112-123)
+  crc32_blocks   the per-block SST framing checksum (crc32fast::hash, reference
+                 src/table/builder.rs:120-122, verified at src/table.rs:226-230)
 
 Tensors live on a ROCm device (torch is only the allocator / stream provider).  The work
 is done by liblsmblk.so; there is no CPU path here.
@@ -171,3 +173,26 @@ def encode_kv(kv: KVStream, seg_start, block_size: int, stream=None):
         raise LsmBlkError(st, "encode_kv")
     nblk, nbytes = stats[0].item(), stats[1].item()
     return out[:nbytes], blk_off[:nblk + 1]
+
+
+def crc32_into(blocks: torch.Tensor, blk_off: torch.Tensor, nblk: int, crc: torch.Tensor, stats, stream=None):
+    """Asynchronous per-block CRC-32 into a preallocated int32 tensor (no host sync)."""
+    dev = _dev_index(blk_off)
+    check(lib().lsmblk_crc32_batch(_ctx(dev), _ptr(blocks), blk_off.data_ptr(), nblk, _ptr(crc),
+                                   stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_crc32_batch")
+
+
+def crc32_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None) -> torch.Tensor:
+    """crc32fast::hash of every block -- the SST framing checksum SsTableBuilder::finish_block
+    appends (reference src/table/builder.rs:120-122) and SsTable::read_block verifies
+    (src/table.rs:226-230).  Returns an int32 tensor[nblk] holding the u32 CRCs."""
+    dev = torch.device("cuda", _dev_index(blk_off))
+    nblk = blk_off.numel() - 1
+    crc = torch.zeros(max(nblk, 1), dtype=torch.int32, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    crc32_into(blocks, blk_off, nblk, crc, stats, stream)
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "crc32_blocks")
+    return crc[:nblk]

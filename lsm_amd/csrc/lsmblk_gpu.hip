@@ -1535,7 +1535,174 @@ __global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64
   }
 }
 
+// ================================================================ CRC-32 (SST block framing)
+// crc32fast::hash of every block: the checksum SsTableBuilder::finish_block appends
+// (src/table/builder.rs:120-122) and SsTable::read_block verifies (src/table.rs:226-230).
+// CRC-32/ISO-HDLC: reflected polynomial 0xEDB88320, init and xorout 0xFFFFFFFF.
+//
+// CRC is a serial recurrence per block, so a wave splits each 4-KiB chunk into 64 segments
+// of 64 B, one per lane, and recombines them by linearity.  With R_x(M) the CRC register
+// after feeding M from state x and Z(x, n) = R_x(n zero bytes) (linear in x):
+//   R_x(A || B) = Z(R_x(A), |B|) ^ R_0(B).
+// The chunk is right-aligned on the lanes -- its one short segment (sz mod 64) is the
+// first -- so the segment of lane l is followed by exactly 63 - l full segments and
+// contributes Z(R(seg_l), 64 (63 - l)): the binary digits of 63 - l select up to six of the
+// precomputed maps Z(., 64 << j).  The block's init 0xFFFFFFFF rides in its first segment;
+// chunk after chunk, acc = Z(acc, 4096) ^ R_0(chunk).  Every map is a 32x32 GF(2) matrix
+// applied as four 256-entry byte tables in LDS; segments fold 4 bytes per step with the
+// slicing-by-4 tables.  HBM-bound by design: the per-byte work is LDS lookups.
+constexpr uint32_t kCrcChunk = 4096;
+constexpr uint32_t kCrcMats = 7;  // Z(., 64 << j), j = 0..5, and j = 6: a whole chunk
+constexpr uint32_t kCrcStage = kCrcChunk + 32;
+struct alignas(16) CrcTabs {
+  uint32_t slice[4][256];
+  uint32_t shift[kCrcMats][4][256];
+};
+
+struct CrcArgs {
+  const uint8_t* blocks;
+  const uint64_t* blk_off;
+  uint64_t nblk;
+  uint32_t* crc;
+  const CrcTabs* tabs;
+  uint64_t* stats;
+};
+
+__device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[4][256], uint32_t x) {
+  return m[0][x & 0xFF] ^ m[1][(x >> 8) & 0xFF] ^ m[2][(x >> 16) & 0xFF] ^ m[3][x >> 24];
+}
+
+// R over the chunk bytes p[0, sz) (LDS), 0 < sz <= kCrcChunk; the block's first chunk
+// starts from the CRC init.  Every lane returns the chunk's register.
+__device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p, uint32_t sz, bool first) {
+  const uint32_t l = lane_id();
+  const uint32_t nseg = (sz + 63) >> 6, l0 = 64 - nseg, r = sz - 64 * (nseg - 1);
+  uint32_t crc = 0;
+  if (l >= l0) {
+    const uint32_t so = l == l0 ? 0u : r + 64 * (l - l0 - 1), sn = l == l0 ? r : 64u;
+    crc = first && l == l0 ? 0xFFFFFFFFu : 0u;
+    const uint8_t* q = p + so;
+    const uint32_t nb = sn & 3;
+    for (uint32_t i = 0; i < nb; ++i) crc = T.slice[0][(crc ^ q[i]) & 0xFF] ^ (crc >> 8);
+#pragma unroll 4
+    for (uint32_t i = nb; i < sn; i += 4) {
+      crc ^= *reinterpret_cast<const uint32_t*>(q + i);  // unaligned LDS read
+      crc = T.slice[3][crc & 0xFF] ^ T.slice[2][(crc >> 8) & 0xFF] ^ T.slice[1][(crc >> 16) & 0xFF] ^
+            T.slice[0][crc >> 24];
+    }
+    const uint32_t m = 63 - l;  // full segments after this one
+#pragma unroll
+    for (uint32_t j = 0; j < 6; ++j)
+      if ((m >> j) & 1) crc = crc_apply(T.shift[j], crc);
+  }
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) crc ^= __shfl_xor(crc, d, 64);
+  return crc;
+}
+
+// Persistent waves, one block at a time, the next chunk's loads in flight while the current
+// one is folded.  A block of len bytes has ceil(len / 4096) chunks; the first holds the
+// len mod 4096 remainder (or a full 4096), so every later chunk is full.
+__global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
+  __shared__ CrcTabs T;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4][kCrcStage];
+  const uint32_t t = threadIdx.x, w = t >> 6, l = lane_id();
+  for (uint32_t i = t; i < sizeof(CrcTabs) / 16; i += 256)
+    reinterpret_cast<u32x4*>(&T)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
+  if (blockIdx.x == 0 && t == 0) {
+    a.stats[0] = a.nblk;
+    a.stats[1] = a.blk_off[a.nblk] - a.blk_off[0];
+  }
+  __syncthreads();
+  uint8_t* S = stage[w];
+  const uint64_t stride = uint64_t(gridDim.x) * 4;
+  uint64_t b = uint64_t(blockIdx.x) * 4 + w;
+  if (b >= a.nblk) return;
+  uint32_t err = 0;
+  auto meta = [&](uint64_t bi, uint64_t& st, uint32_t& len) {
+    const uint64_t s0 = uni64(a.blk_off[bi]), e0 = uni64(a.blk_off[bi + 1]);
+    const bool ok = e0 >= s0 && e0 - s0 <= 0x7FFFFFF0ull;
+    if (!ok) err |= LSMBLK_ERR_MALFORMED;
+    st = s0;
+    len = ok ? uint32_t(e0 - s0) : 0u;
+  };
+  u32x4 q[5];
+  uint32_t qlead = 0;
+  auto issue = [&](uint64_t cs, uint32_t sz) {  // loads of block bytes [cs, cs + sz)
+    const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(a.blocks + cs) & 15));
+    const rsrc_t R = make_rsrc(a.blocks + cs - lead, lead + sz);
+    const uint32_t n16 = (lead + sz + 15) >> 4;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < n16) q[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
+    qlead = lead;
+  };
+  uint64_t st;
+  uint32_t len;
+  meta(b, st, len);
+  uint32_t nch = (len + kCrcChunk - 1) / kCrcChunk;
+  if (nch) issue(st, len - kCrcChunk * (nch - 1));
+  for (;;) {
+    const uint64_t bn = b + stride;
+    const bool has_next = bn < a.nblk;
+    uint64_t stn = 0;
+    uint32_t lenn = 0;
+    if (has_next) meta(bn, stn, lenn);  // in flight while this block is folded
+    const uint32_t nchn = (lenn + kCrcChunk - 1) / kCrcChunk;
+    const uint32_t h = len - kCrcChunk * (nch ? nch - 1 : 0u);  // first chunk's size
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c < nch; ++c) {
+      const uint32_t sz = c == 0 ? h : kCrcChunk, lead = qlead;
+      const uint32_t n16 = (lead + sz + 15) >> 4;
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i)
+        if (l + 64 * i < n16) *reinterpret_cast<u32x4*>(S + 16 * (l + 64 * i)) = q[i];
+      wave_sync();
+      if (c + 1 < nch) issue(st + h + uint64_t(kCrcChunk) * c, kCrcChunk);
+      else if (has_next && nchn) issue(stn, lenn - kCrcChunk * (nchn - 1));
+      const uint32_t part = crc_chunk(T, S + lead, sz, c == 0);
+      acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
+      wave_sync();  // the next landing overwrites S
+    }
+    if (nch == 0 && has_next && nchn) issue(stn, lenn - kCrcChunk * (nchn - 1));  // empty block
+    if (l == 0) a.crc[b] = nch ? ~acc : 0u;
+    if (!has_next) break;
+    b = bn;
+    st = stn;
+    len = lenn;
+    nch = nchn;
+  }
+  raise_err(a.stats, err);
+}
+
 }  // namespace
+
+// CRC tables (host): slicing-by-4 and the zero-extension maps Z(., 64 << j) as byte tables.
+static void crc_host_tables(CrcTabs& T) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? 0xEDB88320u : 0u);
+    T.slice[0][i] = c;
+  }
+  for (int k = 1; k < 4; ++k)
+    for (uint32_t i = 0; i < 256; ++i) T.slice[k][i] = (T.slice[k - 1][i] >> 8) ^ T.slice[0][T.slice[k - 1][i] & 0xFF];
+  for (uint32_t j = 0; j < kCrcMats; ++j) {
+    const uint32_t n = 64u << j;
+    uint32_t col[32];
+    for (uint32_t bit = 0; bit < 32; ++bit) {
+      uint32_t x = 1u << bit;
+      for (uint32_t z = 0; z < n; ++z) x = T.slice[0][x & 0xFF] ^ (x >> 8);
+      col[bit] = x;
+    }
+    for (uint32_t k = 0; k < 4; ++k)
+      for (uint32_t v = 0; v < 256; ++v) {
+        uint32_t y = 0;
+        for (uint32_t bit = 0; bit < 8; ++bit)
+          if ((v >> bit) & 1) y ^= col[8 * k + bit];
+        T.shift[j][k][v] = y;
+      }
+  }
+}
 
 // ================================================================ host side
 struct lsmblk_ctx {
@@ -1544,6 +1711,7 @@ struct lsmblk_ctx {
   uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket
   uint32_t* dec_agg = nullptr;   // (entries, key bytes, value bytes) per block
   uint64_t dec_cap = 0;
+  CrcTabs* crc_tabs = nullptr;   // CRC-32 slicing + zero-extension tables (first CRC call)
   uint64_t* tile_sum = nullptr;  // 3 per 64-block tile
   uint64_t* tile_pre = nullptr;
   uint64_t tile_cap = 0;
@@ -1672,6 +1840,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->rec_first);
   (void)hipFree(c->ent);
   (void)hipFree(c->blk_first);
+  (void)hipFree(c->crc_tabs);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -1854,6 +2023,38 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
   hipLaunchKernelGGL(emit_kernel, dim3(grid), dim3(256), 0, st, e);
   if (c->timing) (void)hipEventRecord(c->ev[6], st);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t* crc,
+                       uint64_t* stats, void* stream) {
+  if (!c || !blk_off || !stats || (nblk && !crc)) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  if (!c->crc_tabs) {
+    CrcTabs h;
+    crc_host_tables(h);
+    if (hipMalloc(reinterpret_cast<void**>(&c->crc_tabs), sizeof(CrcTabs)) != hipSuccess) {
+      c->crc_tabs = nullptr;
+      return LSMBLK_E_NOMEM;
+    }
+    if (hipMemcpy(c->crc_tabs, &h, sizeof(CrcTabs), hipMemcpyHostToDevice) != hipSuccess) return LSMBLK_E_HIP;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (nblk == 0) return LSMBLK_OK;
+  CrcArgs a;
+  a.blocks = blocks;
+  a.blk_off = blk_off;
+  a.nblk = nblk;
+  a.crc = crc;
+  a.tabs = c->crc_tabs;
+  a.stats = stats;
+  // 32 KiB of tables + 4 x 4 KiB staging per workgroup: three workgroups per CU
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const uint64_t want = (nblk + 3) / 4, cap = uint64_t(cus > 0 ? cus : 256) * 3;
+  hipLaunchKernelGGL(crc_kernel, dim3(uint32_t(want < cap ? want : cap)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
