@@ -1548,15 +1548,20 @@ __global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64
 // first -- so the segment of lane l is followed by exactly 63 - l full segments and
 // contributes Z(R(seg_l), 64 (63 - l)): the binary digits of 63 - l select up to six of the
 // precomputed maps Z(., 64 << j).  The block's init 0xFFFFFFFF rides in its first segment;
-// chunk after chunk, acc = Z(acc, 4096) ^ R_0(chunk).  Every map is a 32x32 GF(2) matrix
-// applied as four 256-entry byte tables in LDS; segments fold 4 bytes per step with the
-// slicing-by-4 tables.  HBM-bound by design: the per-byte work is LDS lookups.
+// chunk after chunk, acc = Z(acc, 4096) ^ R_0(chunk).
+//
+// Every linear map (the 4-byte fold step and each Z) is applied as eight 16-entry NIBBLE
+// tables in LDS: all 64 lanes of one lookup instruction then address 16 dwords in 16
+// distinct banks (repeats broadcast), so lookups are conflict-free.  256-entry byte tables
+// put 64 random lanes on 32 banks and measured 1.6 TB/s; 4 KiB of nibble tables also leave
+// room for more resident workgroups.
 constexpr uint32_t kCrcChunk = 4096;
 constexpr uint32_t kCrcMats = 7;  // Z(., 64 << j), j = 0..5, and j = 6: a whole chunk
-constexpr uint32_t kCrcStage = kCrcChunk + 32;
+constexpr uint32_t kCrcStage = 5 * 1024;  // five 1-KiB load pieces (lead + chunk <= 4111 B)
 struct alignas(16) CrcTabs {
-  uint32_t slice[4][256];
-  uint32_t shift[kCrcMats][4][256];
+  uint32_t fold[8][16];              // R_0 after xoring a dword into the register: by nibble
+  uint32_t shift[kCrcMats][8][16];   // Z(., 64 << j) by nibble of the register
+  uint32_t nib[16];                  // one 4-bit step (leading odd bytes of a segment)
 };
 
 struct CrcArgs {
@@ -1568,8 +1573,9 @@ struct CrcArgs {
   uint64_t* stats;
 };
 
-__device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[4][256], uint32_t x) {
-  return m[0][x & 0xFF] ^ m[1][(x >> 8) & 0xFF] ^ m[2][(x >> 16) & 0xFF] ^ m[3][x >> 24];
+__device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[8][16], uint32_t x) {
+  return (m[0][x & 15] ^ m[1][(x >> 4) & 15]) ^ (m[2][(x >> 8) & 15] ^ m[3][(x >> 12) & 15]) ^
+         (m[4][(x >> 16) & 15] ^ m[5][(x >> 20) & 15]) ^ (m[6][(x >> 24) & 15] ^ m[7][x >> 28]);
 }
 
 // R over the chunk bytes p[0, sz) (LDS), 0 < sz <= kCrcChunk; the block's first chunk
@@ -1583,13 +1589,13 @@ __device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p
     crc = first && l == l0 ? 0xFFFFFFFFu : 0u;
     const uint8_t* q = p + so;
     const uint32_t nb = sn & 3;
-    for (uint32_t i = 0; i < nb; ++i) crc = T.slice[0][(crc ^ q[i]) & 0xFF] ^ (crc >> 8);
-#pragma unroll 4
-    for (uint32_t i = nb; i < sn; i += 4) {
-      crc ^= *reinterpret_cast<const uint32_t*>(q + i);  // unaligned LDS read
-      crc = T.slice[3][crc & 0xFF] ^ T.slice[2][(crc >> 8) & 0xFF] ^ T.slice[1][(crc >> 16) & 0xFF] ^
-            T.slice[0][crc >> 24];
+    for (uint32_t i = 0; i < nb; ++i) {
+      crc ^= q[i];
+      crc = T.nib[crc & 15] ^ (crc >> 4);
+      crc = T.nib[crc & 15] ^ (crc >> 4);
     }
+#pragma unroll 4
+    for (uint32_t i = nb; i < sn; i += 4) crc = crc_apply(T.fold, crc ^ *reinterpret_cast<const uint32_t*>(q + i));
     const uint32_t m = 63 - l;  // full segments after this one
 #pragma unroll
     for (uint32_t j = 0; j < 6; ++j)
@@ -1626,81 +1632,94 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
     st = s0;
     len = ok ? uint32_t(e0 - s0) : 0u;
   };
+  // Always five 16-B loads per lane (bytes past the chunk come back 0 from the descriptor's
+  // bound) and five LDS stores: no predicated loads, so the compiler counts the waits
+  // exactly instead of draining everything (block metadata included) at the landing.
   u32x4 q[5];
   uint32_t qlead = 0;
   auto issue = [&](uint64_t cs, uint32_t sz) {  // loads of block bytes [cs, cs + sz)
     const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(a.blocks + cs) & 15));
     const rsrc_t R = make_rsrc(a.blocks + cs - lead, lead + sz);
-    const uint32_t n16 = (lead + sz + 15) >> 4;
 #pragma unroll
-    for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < n16) q[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
+    for (uint32_t i = 0; i < 5; ++i) q[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
     qlead = lead;
   };
-  uint64_t st;
-  uint32_t len;
+  // block metadata runs two blocks ahead of the folding, chunk loads one chunk ahead
+  uint64_t st, stn = 0;
+  uint32_t len, lenn = 0;
   meta(b, st, len);
+  if (b + stride < a.nblk) meta(b + stride, stn, lenn);
   uint32_t nch = (len + kCrcChunk - 1) / kCrcChunk;
-  if (nch) issue(st, len - kCrcChunk * (nch - 1));
+  issue(st, nch ? len - kCrcChunk * (nch - 1) : 0u);
   for (;;) {
-    const uint64_t bn = b + stride;
+    const uint64_t bn = b + stride, b2 = bn + stride;
     const bool has_next = bn < a.nblk;
-    uint64_t stn = 0;
-    uint32_t lenn = 0;
-    if (has_next) meta(bn, stn, lenn);  // in flight while this block is folded
+    uint64_t st2 = 0;
+    uint32_t len2 = 0;
+    if (b2 < a.nblk) meta(b2, st2, len2);
     const uint32_t nchn = (lenn + kCrcChunk - 1) / kCrcChunk;
     const uint32_t h = len - kCrcChunk * (nch ? nch - 1 : 0u);  // first chunk's size
     uint32_t acc = 0;
-    for (uint32_t c = 0; c < nch; ++c) {
+    for (uint32_t c = 0; c == 0 || c < nch; ++c) {  // an empty block still lands its (zero) loads
       const uint32_t sz = c == 0 ? h : kCrcChunk, lead = qlead;
-      const uint32_t n16 = (lead + sz + 15) >> 4;
 #pragma unroll
-      for (uint32_t i = 0; i < 5; ++i)
-        if (l + 64 * i < n16) *reinterpret_cast<u32x4*>(S + 16 * (l + 64 * i)) = q[i];
+      for (uint32_t i = 0; i < 5; ++i) *reinterpret_cast<u32x4*>(S + 16 * (l + 64 * i)) = q[i];
       wave_sync();
       if (c + 1 < nch) issue(st + h + uint64_t(kCrcChunk) * c, kCrcChunk);
-      else if (has_next && nchn) issue(stn, lenn - kCrcChunk * (nchn - 1));
-      const uint32_t part = crc_chunk(T, S + lead, sz, c == 0);
-      acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
+      else if (has_next) issue(stn, nchn ? lenn - kCrcChunk * (nchn - 1) : 0u);
+      if (nch) {
+        const uint32_t part = crc_chunk(T, S + lead, sz, c == 0);
+        acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
+      }
       wave_sync();  // the next landing overwrites S
     }
-    if (nch == 0 && has_next && nchn) issue(stn, lenn - kCrcChunk * (nchn - 1));  // empty block
     if (l == 0) a.crc[b] = nch ? ~acc : 0u;
     if (!has_next) break;
     b = bn;
     st = stn;
     len = lenn;
     nch = nchn;
+    stn = st2;
+    lenn = len2;
   }
   raise_err(a.stats, err);
 }
 
 }  // namespace
 
-// CRC tables (host): slicing-by-4 and the zero-extension maps Z(., 64 << j) as byte tables.
+// CRC tables (host).  Each linear map of the 32-bit register is tabulated by its columns
+// (the images of the 32 unit vectors), then as eight nibble tables.
+static uint32_t crc_bit_step(uint32_t c) { return (c >> 1) ^ ((c & 1) ? 0xEDB88320u : 0u); }
+static void crc_nibble_tables(const uint32_t (&col)[32], uint32_t (&m)[8][16]) {
+  for (uint32_t k = 0; k < 8; ++k)
+    for (uint32_t v = 0; v < 16; ++v) {
+      uint32_t y = 0;
+      for (uint32_t bit = 0; bit < 4; ++bit)
+        if ((v >> bit) & 1) y ^= col[4 * k + bit];
+      m[k][v] = y;
+    }
+}
 static void crc_host_tables(CrcTabs& T) {
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? 0xEDB88320u : 0u);
-    T.slice[0][i] = c;
+  for (uint32_t v = 0; v < 16; ++v) {
+    uint32_t c = v;
+    for (int s = 0; s < 4; ++s) c = crc_bit_step(c);
+    T.nib[v] = c;
   }
-  for (int k = 1; k < 4; ++k)
-    for (uint32_t i = 0; i < 256; ++i) T.slice[k][i] = (T.slice[k - 1][i] >> 8) ^ T.slice[0][T.slice[k - 1][i] & 0xFF];
-  for (uint32_t j = 0; j < kCrcMats; ++j) {
-    const uint32_t n = 64u << j;
-    uint32_t col[32];
+  uint32_t col[32];
+  for (uint32_t bit = 0; bit < 32; ++bit) {  // fold: 32 bit steps (4 zero bytes after the xor)
+    uint32_t x = 1u << bit;
+    for (int s = 0; s < 32; ++s) x = crc_bit_step(x);
+    col[bit] = x;
+  }
+  crc_nibble_tables(col, T.fold);
+  for (uint32_t j = 0; j < kCrcMats; ++j) {  // Z(., 64 << j): 8 (64 << j) bit steps
+    const uint32_t steps = 8u * (64u << j);
     for (uint32_t bit = 0; bit < 32; ++bit) {
       uint32_t x = 1u << bit;
-      for (uint32_t z = 0; z < n; ++z) x = T.slice[0][x & 0xFF] ^ (x >> 8);
+      for (uint32_t s = 0; s < steps; ++s) x = crc_bit_step(x);
       col[bit] = x;
     }
-    for (uint32_t k = 0; k < 4; ++k)
-      for (uint32_t v = 0; v < 256; ++v) {
-        uint32_t y = 0;
-        for (uint32_t bit = 0; bit < 8; ++bit)
-          if ((v >> bit) & 1) y ^= col[8 * k + bit];
-        T.shift[j][k][v] = y;
-      }
+    crc_nibble_tables(col, T.shift[j]);
   }
 }
 
@@ -2050,10 +2069,12 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
   a.crc = crc;
   a.tabs = c->crc_tabs;
   a.stats = stats;
-  // 32 KiB of tables + 4 x 4 KiB staging per workgroup: three workgroups per CU
-  int cus = 256;
+  // persistent: as many workgroups as are resident at once (4 KiB tables + 4 x 4 KiB staging)
+  int cus = 256, per_cu = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const uint64_t want = (nblk + 3) / 4, cap = uint64_t(cus > 0 ? cus : 256) * 3;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, crc_kernel, 256, 0) != hipSuccess || per_cu < 1)
+    per_cu = 3;
+  const uint64_t want = (nblk + 3) / 4, cap = uint64_t(cus > 0 ? cus : 256) * uint64_t(per_cu);
   hipLaunchKernelGGL(crc_kernel, dim3(uint32_t(want < cap ? want : cap)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
