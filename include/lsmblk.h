@@ -21,6 +21,8 @@
  *       lsmblk_encode_batch  replaces the per-entry loop  SsTableBuilder::add ->
  *                            BlockBuilder::add / finish_block  (src/table/builder.rs:48-65,
  *                                                           112-123), one segment per SST
+ *       lsmblk_crc32_batch   the per-block framing checksum  (src/table/builder.rs:120-122,
+ *                                                           src/table.rs:226-230)
  *     All pointers are DEVICE pointers; calls are asynchronous on `stream` (a hipStream_t
  *     passed as void*; NULL = the default stream).  Thread-safe per distinct context.
  *
@@ -176,14 +178,17 @@ int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint3
                         uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, void* stream);
 
 /* SST block framing (SURVEY.md §8 f, row 1): crc[b] = crc32fast::hash(block b) for block
- * b = blocks[blk_off[b] .. blk_off[b+1]) -- the checksum SsTableBuilder::finish_block appends
- * after every encoded block as a big-endian u32 (src/table/builder.rs:120-122) and
- * SsTable::read_block verifies before Block::decode (src/table.rs:219-230).  CRC-32/ISO-HDLC
- * (reflected 0xEDB88320, init and xorout 0xFFFFFFFF); an empty block's CRC is 0.
- * stats: [0] blocks [1] bytes [3] error flags (LSMBLK_ERR_MALFORMED: a block's offsets are
- * decreasing or it exceeds 2 GiB; its crc is then 0).  Asynchronous like the calls above. */
+ * b = blocks[blk_off[b] .. blk_off[b+1] - tail) -- the checksum SsTableBuilder::finish_block
+ * appends after every encoded block as a big-endian u32 (src/table/builder.rs:120-122) and
+ * SsTable::read_block verifies before Block::decode (src/table.rs:219-230).  tail = 0 for
+ * tightly packed blocks (lsmblk_encode_batch output); tail = 4 over a framed SST data section
+ * with blk_off = the BlockMeta offsets plus the meta-section offset (read_block's
+ * block_len = offset_end - offset - 4).  CRC-32/ISO-HDLC (reflected 0xEDB88320, init and
+ * xorout 0xFFFFFFFF); an empty block's CRC is 0.  stats: [0] blocks [1] bytes spanned
+ * [3] error flags (LSMBLK_ERR_MALFORMED: a range is shorter than tail, decreasing, or over
+ * 2 GiB; its crc is then 0).  Asynchronous like the calls above. */
 int lsmblk_crc32_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off,
-                       uint64_t nblk, uint32_t* crc, uint64_t* stats, void* stream);
+                       uint64_t nblk, uint32_t tail, uint32_t* crc, uint64_t* stats, void* stream);
 
 #ifdef __cplusplus
 }

@@ -175,22 +175,24 @@ def encode_kv(kv: KVStream, seg_start, block_size: int, stream=None):
     return out[:nbytes], blk_off[:nblk + 1]
 
 
-def crc32_into(blocks: torch.Tensor, blk_off: torch.Tensor, nblk: int, crc: torch.Tensor, stats, stream=None):
+def crc32_into(blocks: torch.Tensor, blk_off: torch.Tensor, nblk: int, crc: torch.Tensor, stats, stream=None,
+               tail: int = 0):
     """Asynchronous per-block CRC-32 into a preallocated int32 tensor (no host sync)."""
     dev = _dev_index(blk_off)
-    check(lib().lsmblk_crc32_batch(_ctx(dev), _ptr(blocks), blk_off.data_ptr(), nblk, _ptr(crc),
+    check(lib().lsmblk_crc32_batch(_ctx(dev), _ptr(blocks), blk_off.data_ptr(), nblk, tail, _ptr(crc),
                                    stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_crc32_batch")
 
 
-def crc32_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None) -> torch.Tensor:
+def crc32_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None, tail: int = 0) -> torch.Tensor:
     """crc32fast::hash of every block -- the SST framing checksum SsTableBuilder::finish_block
     appends (reference src/table/builder.rs:120-122) and SsTable::read_block verifies
-    (src/table.rs:226-230).  Returns an int32 tensor[nblk] holding the u32 CRCs."""
+    (src/table.rs:226-230).  Block b = blocks[blk_off[b] : blk_off[b+1] - tail] (tail=4 over a
+    framed SST data section).  Returns an int32 tensor[nblk] holding the u32 CRCs."""
     dev = torch.device("cuda", _dev_index(blk_off))
     nblk = blk_off.numel() - 1
     crc = torch.zeros(max(nblk, 1), dtype=torch.int32, device=dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
-    crc32_into(blocks, blk_off, nblk, crc, stats, stream)
+    crc32_into(blocks, blk_off, nblk, crc, stats, stream, tail)
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:

@@ -1568,6 +1568,7 @@ struct CrcArgs {
   const uint8_t* blocks;
   const uint64_t* blk_off;
   uint64_t nblk;
+  uint32_t tail;  // bytes of each range that are not block (4: the framing CRC itself)
   uint32_t* crc;
   const CrcTabs* tabs;
   uint64_t* stats;
@@ -1627,10 +1628,10 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   uint32_t err = 0;
   auto meta = [&](uint64_t bi, uint64_t& st, uint32_t& len) {
     const uint64_t s0 = uni64(a.blk_off[bi]), e0 = uni64(a.blk_off[bi + 1]);
-    const bool ok = e0 >= s0 && e0 - s0 <= 0x7FFFFFF0ull;
+    const bool ok = e0 >= s0 + a.tail && e0 - s0 <= 0x7FFFFFF0ull;
     if (!ok) err |= LSMBLK_ERR_MALFORMED;
     st = s0;
-    len = ok ? uint32_t(e0 - s0) : 0u;
+    len = ok ? uint32_t(e0 - s0) - a.tail : 0u;
   };
   // Always five 16-B loads per lane (bytes past the chunk come back 0 from the descriptor's
   // bound) and five LDS stores: no predicated loads, so the compiler counts the waits
@@ -2045,8 +2046,8 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
-int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t* crc,
-                       uint64_t* stats, void* stream) {
+int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+                       uint32_t* crc, uint64_t* stats, void* stream) {
   if (!c || !blk_off || !stats || (nblk && !crc)) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
@@ -2066,6 +2067,7 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
   a.blocks = blocks;
   a.blk_off = blk_off;
   a.nblk = nblk;
+  a.tail = tail;
   a.crc = crc;
   a.tabs = c->crc_tabs;
   a.stats = stats;

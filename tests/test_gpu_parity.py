@@ -325,3 +325,15 @@ def test_crc32_of_encoded_blocks():
     np.testing.assert_array_equal(got, np.array(want, np.uint32))
     one = batch.crc32_blocks(blocks, blk_off[:2]).cpu().numpy().view(np.uint32)
     assert int(one[0]) == want[0]
+    # a framed SST data section (block || u32 BE crc per block, finish_block) read back with the
+    # BlockMeta offsets and tail=4 (read_block: block_len = offset_end - offset - 4)
+    parts, meta = [], [0]
+    for i in range(len(ref_off) - 1):
+        blk = ref_blocks[int(ref_off[i]):int(ref_off[i + 1])].tobytes()
+        parts.append(blk + int(want[i]).to_bytes(4, "big"))
+        meta.append(meta[-1] + len(parts[-1]))
+    framed = np.frombuffer(b"".join(parts), np.uint8).copy()
+    db, do = dev_blocks(framed, np.array(meta, np.uint64), 3)
+    got = batch.crc32_blocks(db, do, tail=4).cpu().numpy().view(np.uint32)
+    stored = np.array([int.from_bytes(framed[m - 4:m].tobytes(), "big") for m in meta[1:]], np.uint32)
+    np.testing.assert_array_equal(got, stored)
