@@ -575,6 +575,94 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
   }
 }
 
+// ---------------------------------------------------------------- large blocks
+// Blocks over the LDS image (config M: 64 KiB blocks, values up to 4 KiB) with <= kDecMaxE
+// entries keep their entry tables in LDS and move bytes HBM -> HBM: every entry lane copies
+// its key and value as 16-B unaligned buffer loads/stores (last piece overlapping), with
+// kBigB pieces' loads issued before their stores (one memory round trip per kBigB pieces).
+constexpr uint32_t kBigB = 8;
+
+__device__ __forceinline__ u32x4 gload16(const rsrc_t& R, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(R, off, 0, 0);
+}
+
+// bytes [so, so + len) of RS -> bytes [dof, dof + len) of RD, any alignment on either side.
+// RS bytes past lim are not the block's: a short run near the end is read byte by byte, so
+// no 16-B load straddles the block end (the descriptor bound may zero a whole load).
+__device__ __forceinline__ void copy_run(const rsrc_t& RS, uint32_t so, uint32_t lim, const rsrc_t& RD, uint32_t dof,
+                                         uint32_t len) {
+  if (len == 0) return;
+  if (len < 16) {
+    uint32_t v[4] = {0, 0, 0, 0};
+    if (so + 16 <= lim) {
+      const u32x4 q = gload16(RS, so);
+      v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+    } else {
+      for (uint32_t i = 0; i < len; ++i) v[i >> 2] |= __builtin_amdgcn_raw_buffer_load_b8(RS, so + i, 0, 0) << (8 * (i & 3));
+    }
+    st_short(RD, dof, len, v);
+    return;
+  }
+  const uint32_t np = (len + 15) >> 4, last = len - 16;
+  for (uint32_t j0 = 0; j0 < np; j0 += kBigB) {
+    u32x4 q[kBigB];
+#pragma unroll
+    for (uint32_t j = 0; j < kBigB; ++j)
+      if (j0 + j < np) q[j] = gload16(RS, so + min(16 * (j0 + j), last));
+#pragma unroll
+    for (uint32_t j = 0; j < kBigB; ++j)
+      if (j0 + j < np) {
+        const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+        st16(RD, dof + min(16 * (j0 + j), last), v);
+      }
+  }
+}
+
+__device__ void dec_big_outputs(const DecodeArgs& a, const DecLds& L, const rsrc_t& R, uint32_t lead,
+                                const BlockHdr& h, uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V) {
+  const uint32_t l = lane_id();
+  const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
+  const rsrc_t RK = make_rsrc_exact(a.keys + (K0 - kb), kb + K), RV = make_rsrc_exact(a.vals + (V0 - vb), vb + V);
+  const GlbImg im{R, lead};
+  const uint32_t fk = lead + 4, lim = lead + h.len;  // descriptor bytes: first key, block end
+  for (uint32_t k = l; k < h.n; k += 64) {
+    const uint32_t epos = L.epos[k], p = L.pfx[k], s = L.sfx[k];
+    const uint32_t kout = L.kout[k], vout = L.vout[k], vl = L.vout[k + 1] - vout;
+    const uint32_t sb = lead + epos + 4, kl = p + s;  // descriptor byte of the suffix
+    const uint64_t e = E0 + k;
+    a.ts[e] = im.u64(epos + 4 + s);
+    a.key_off[e] = uint32_t(K0 + kout);
+    a.val_off[e] = uint32_t(V0 + vout);
+    for (uint32_t t = 0; t < kl; t += 16) {  // key byte x: first key x < p, else suffix x - p
+      const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
+      uint32_t v[4];
+      if (sb + o >= p && sb + o - p + 16 <= lim && fk + o + 16 <= lim) {
+        const u32x4 sq = gload16(R, sb + o - p), fq = gload16(R, fk + o);
+        const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w}, fv[4] = {fq.x, fq.y, fq.z, fq.w};
+#pragma unroll
+        for (uint32_t d = 0; d < 4; ++d) {
+          const int32_t nf = int32_t(p) - int32_t(o + 4 * d);
+          const uint32_t m = nf <= 0 ? 0u : nf >= 4 ? ~0u : (1u << (8 * nf)) - 1;
+          v[d] = (fv[d] & m) | (sv[d] & ~m);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t d = 0; d < 4; ++d) {
+          uint32_t wd = 0;
+          for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t x = o + 4 * d + i;
+            wd |= (x < p ? im.u8(4 + x) : im.u8(epos + 4 + x - p)) << (8 * i);
+          }
+          v[d] = wd;
+        }
+      }
+      if (kl >= 16) st16(RK, kb + kout + o, v);
+      else st_short(RK, kb + kout, kl, v);
+    }
+    copy_run(R, sb + s + 10, lim, RV, vb + vout, vl);
+  }
+}
+
 __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   const uint32_t l = lane_id();
   uint32_t err = 0;
@@ -616,12 +704,12 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   }
   if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
   const bool fast = fits && h.n <= kDecMaxE;
+  const bool big = !fits && h.n <= kDecMaxE;  // large block: tables in LDS, bytes from HBM
 
   // phase 1: parse entries, block aggregates (entries, key bytes, value bytes)
   uint64_t K = 0, V = 0;
   bool bad = false;
-  if (fast) {
-    const LdsImg im{L.img, lead};
+  auto parse_tables = [&](const auto& im) {
     for (uint32_t c = 0; c < h.n; c += 64) {
       const uint32_t k = c + l;
       uint32_t off = 0, p = 0, s = 0, vl = 0;
@@ -645,6 +733,11 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
       L.kout[h.n] = uint32_t(K);
       L.vout[h.n] = uint32_t(V);
     }
+  };
+  if (fast) {
+    parse_tables(LdsImg{L.img, lead});
+  } else if (big) {
+    parse_tables(GlbImg{R, lead});
   } else {
     for (uint32_t c = 0; c < h.n; c += 64) {
       const uint32_t k = c + l;
@@ -677,6 +770,8 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
     if (fast) {
       dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
+    } else if (big) {
+      dec_big_outputs(a, L, R, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V));
     } else if (fits) {
       dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
     } else {

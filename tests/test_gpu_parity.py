@@ -337,3 +337,20 @@ def test_crc32_of_encoded_blocks():
     got = batch.crc32_blocks(db, do, tail=4).cpu().numpy().view(np.uint32)
     stored = np.array([int.from_bytes(framed[m - 4:m].tobytes(), "big") for m in meta[1:]], np.uint32)
     np.testing.assert_array_equal(got, stored)
+
+
+@pytest.mark.parametrize("shift", [0, 9])
+def test_large_blocks_decode_paths(shift):
+    """Blocks over the LDS image: <= 128 entries take the HBM->HBM copy path, more take the
+    byte path.  Long shared prefixes, 1-5-byte key tails, values of 0-17 B next to 1-5 KB ones
+    (short runs at block ends), unaligned block stream."""
+    rng = np.random.default_rng(23)
+    base = bytes(rng.integers(0, 256, 60, dtype=np.uint8))
+    keys = sorted({base[:int(rng.integers(0, 60))] + bytes(rng.integers(0, 256, int(rng.integers(1, 6)), dtype=np.uint8))
+                   for _ in range(3000)})
+    sizes = [0, 1, 3, 7, 15, 16, 17, 100, 1000, 5000]
+    ents = [(k, i, bytes(rng.integers(0, 256, int(rng.choice(sizes)), dtype=np.uint8))) for i, k in enumerate(keys)]
+    kv = O.KV.from_entries(ents)
+    for bs in (65536, 16384):
+        _, off = roundtrip_check(kv, [0, kv.n], bs, shift=shift)
+        assert (np.diff(off) > 4400).mean() > 0.9  # mostly beyond the LDS image
