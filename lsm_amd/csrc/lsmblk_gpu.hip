@@ -1217,6 +1217,8 @@ struct EmitArgs {
   uint64_t out_cap, blk_cap;
   uint64_t n;  // entries; arena sizes are key_off[n], val_off[n]
   uint64_t* stats;
+  uint32_t* big_list;  // blocks beyond the LDS image, appended by emit_kernel for emit_big_kernel
+  uint32_t* big_cnt;
   uint32_t skip;  // ablation mask (timing experiments only): 16 entry-lane byte writes,
                   // 32 bulk value copy, 64 flush, 128 LCP
 };
@@ -1251,34 +1253,51 @@ __device__ __forceinline__ void lds_st_short(uint8_t* p, uint32_t len, const uin
   }
 }
 
-// Global byte readers for the simple path.
-struct GlbBytes {
-  rsrc_t r;
-  uint32_t lead;
-  __device__ __forceinline__ uint32_t u8(uint32_t pos) const {
-    return __builtin_amdgcn_raw_buffer_load_b8(r, lead + pos, 0, 0);
-  }
-};
-
-__device__ void emit_simple(const EmitArgs& a, const GlbBytes& KB, const GlbBytes& VB, uint32_t s,
-                            uint32_t n, uint64_t O, uint64_t size, uint32_t& err) {
+// Blocks beyond the LDS image (config M's 64 KiB blocks, oversize entries, > kEmitMaxE
+// entries): one pass, entry lanes write their records straight to HBM.  LCP against the
+// first key in 16-B compares; suffix and value as 16-B unaligned buffer loads/stores with
+// batched loads (copy_run); header, ts and value_len as single unaligned stores; the offset
+// slot at data_len + 2k, data_len = size - 2n - 2 known from the plan (checked at the end).
+__device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, uint64_t size, uint32_t& err) {
   const uint32_t l = lane_id();
-  const uint32_t fp = uni(a.key_off[s]), fl = uni(a.key_off[s + 1]) - fp;
+  const uint32_t kg = uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15), vg = uint32_t(reinterpret_cast<uintptr_t>(a.vals) & 15);
+  const uint32_t klim = kg + uni(a.key_off[a.n]), vlim = vg + uni(a.val_off[a.n]);  // valid descriptor bytes
+  const rsrc_t RK = make_rsrc(a.keys - kg, klim), RV = make_rsrc(a.vals - vg, vlim);
+  const uint32_t ob = uint32_t(O & 15);
+  const uint64_t room = O < a.out_cap ? a.out_cap - O : 0;  // never store past out_cap
+  const rsrc_t RO = make_rsrc_exact(a.out + (O - ob), ob + uint32_t(size < room ? size : room));
+  const uint32_t fp = kg + uni(a.key_off[s]), fl = uni(a.key_off[s + 1]) - (fp - kg);
+  const uint64_t data_len = size - 2ull * n - 2;
   uint64_t dc = 0;
-  auto put = [&](uint64_t pos, uint32_t byte) {
-    if (O + pos < a.out_cap) a.out[O + pos] = uint8_t(byte);
-  };
   for (uint32_t c = 0; c < n; c += 64) {
     const uint32_t k = c + l;
     uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
     if (k < n) {
-      kp = a.key_off[s + k];
-      kl = a.key_off[s + k + 1] - kp;
-      vp = a.val_off[s + k];
-      vl = a.val_off[s + k + 1] - vp;
-      if (k != 0) {
+      kp = kg + a.key_off[s + k];
+      kl = a.key_off[s + k + 1] - (kp - kg);
+      vp = vg + a.val_off[s + k];
+      vl = a.val_off[s + k + 1] - (vp - vg);
+      if (k != 0) {  // builder.rs:62 common_prefix(first_key, key)
         const uint32_t m = fl < kl ? fl : kl;
-        while (p < m && KB.u8(fp + p) == KB.u8(kp + p)) ++p;
+        p = m;
+        for (uint32_t q = 0; q < m; q += 16) {
+          uint32_t z = 16;  // first differing byte in [q, q + 16)
+          if (fp + q + 16 <= klim && kp + q + 16 <= klim) {
+            const u32x4 x = gload16(RK, fp + q), y = gload16(RK, kp + q);
+            const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
+            for (uint32_t i = 0; i < 4 && z == 16; ++i)
+              if (d[i]) z = 4 * i + (__builtin_ctz(d[i]) >> 3);
+          } else {
+            for (uint32_t i = 0; i < 16 && z == 16 && q + i < m; ++i)
+              if (__builtin_amdgcn_raw_buffer_load_b8(RK, fp + q + i, 0, 0) !=
+                  __builtin_amdgcn_raw_buffer_load_b8(RK, kp + q + i, 0, 0))
+                z = i;
+          }
+          if (z < 16) {
+            p = min(q + z, m);
+            break;
+          }
+        }
       }
     }
     const uint64_t dg = k < n ? uint64_t(kl) + vl + 14 - p : 0;
@@ -1286,48 +1305,22 @@ __device__ void emit_simple(const EmitArgs& a, const GlbBytes& KB, const GlbByte
     const uint64_t pos = dc + incl - dg;
     dc += __shfl(incl, 63, 64);
     if (k < n) {
-      const uint32_t sfx = kl - p;
-      put(pos + 0, (p >> 8) & 0xFF);
-      put(pos + 1, p & 0xFF);
-      put(pos + 2, (sfx >> 8) & 0xFF);
-      put(pos + 3, sfx & 0xFF);
-      for (uint32_t t = 0; t < sfx; ++t) put(pos + 4 + t, KB.u8(kp + p + t));
+      const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
+      // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value
+      __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
+      copy_run(RK, kp + p, klim, RO, at + 4, sfx);
       const uint64_t tsv = a.ts[s + k];
-      for (int t = 0; t < 8; ++t) put(pos + 4 + sfx + t, uint32_t(tsv >> (56 - 8 * t)) & 0xFF);
-      put(pos + 12 + sfx, (vl >> 8) & 0xFF);
-      put(pos + 13 + sfx, vl & 0xFF);
-      for (uint32_t t = 0; t < vl; ++t) put(pos + 14 + sfx + t, VB.u8(vp + t));
-      // offset slot (data.len() as u16) is written below once data_len is known
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bswap32(uint32_t(tsv >> 32)), __builtin_bswap32(uint32_t(tsv))},
+                                            RO, at + 4 + sfx, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(vl & 0xFFFF)), RO, at + 12 + sfx, 0, 0);
+      copy_run(RV, vp, vlim, RO, at + 14 + sfx, vl);
+      // builder.rs:71: offsets.push(data.len() as u16), BE
+      __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO,
+                                            ob + uint32_t(data_len) + 2 * k, 0, 0);
     }
   }
-  const uint64_t data_len = dc;
-  if (data_len + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
-  uint64_t dc2 = 0;
-  for (uint32_t c = 0; c < n; c += 64) {
-    const uint32_t k = c + l;
-    uint32_t kl = 0, vl = 0, p = 0;
-    if (k < n) {
-      const uint32_t kp = a.key_off[s + k];
-      kl = a.key_off[s + k + 1] - kp;
-      vl = a.val_off[s + k + 1] - a.val_off[s + k];
-      if (k != 0) {
-        const uint32_t m = fl < kl ? fl : kl;
-        while (p < m && KB.u8(fp + p) == KB.u8(kp + p)) ++p;
-      }
-    }
-    const uint64_t dg = k < n ? uint64_t(kl) + vl + 14 - p : 0;
-    const uint64_t incl = wave_incl_scan<uint64_t>(dg);
-    const uint64_t pos = dc2 + incl - dg;
-    dc2 += __shfl(incl, 63, 64);
-    if (k < n) {
-      put(data_len + 2 * k, uint32_t(pos >> 8) & 0xFF);
-      put(data_len + 2 * k + 1, uint32_t(pos) & 0xFF);
-    }
-  }
-  if (l == 0) {
-    put(size - 2, (n >> 8) & 0xFF);
-    put(size - 1, n & 0xFF);
-  }
+  if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
+  if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
 }
 
 // Block metadata of one emit unit: two levels of dependent loads (block tables, then the
@@ -1418,12 +1411,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint32_t klead = uint32_t((kaddr + kb0) & 15), vlead = uint32_t((vaddr + vb0) & 15);
     const uint32_t olead = uint32_t(O & 15);
     bool nxt_fast = false;
-    if (!cur_fast) {
-      const uint32_t kg = uint32_t(kaddr & 15), vg = uint32_t(vaddr & 15);
-      const uint32_t kt = uni(a.key_off[a.n]), vt = uni(a.val_off[a.n]);
-      const GlbBytes KB{make_rsrc(a.keys - kg, kg + kt), kg};
-      const GlbBytes VB{make_rsrc(a.vals - vg, vg + vt), vg};
-      emit_simple(a, KB, VB, s, n, O, size, err);
+    if (!cur_fast) {  // handed to emit_big_kernel (its registers stay out of this loop)
+      if (l == 0) a.big_list[atomicAdd(a.big_cnt, 1u)] = uint32_t(cur.bi);
       if (!has_next) break;
       meta2(nxt);
       nxt_fast = is_fast(nxt);
@@ -1619,6 +1608,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     if (!has_next) break;
     cur = nxt;
     cur_fast = nxt_fast;
+  }
+  raise_err(a.stats, err);
+}
+
+// The blocks emit_kernel listed as beyond its LDS image, one wave per block.
+__global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a) {
+  const uint32_t cnt = uni(*a.big_cnt);
+  const uint32_t nw = gridDim.x * 4;
+  uint32_t err = 0;
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < cnt; i += nw) {
+    const uint64_t bi = uni(a.big_list[i]);
+    const uint32_t s = uni(a.blk_first[bi]), e = uni(a.blk_first[bi + 1]);
+    const uint64_t O = uni64(a.blk_off[bi]), size = uni64(a.blk_off[bi + 1]) - O;
+    emit_big(a, s, e - s, O, size, err);
   }
   raise_err(a.stats, err);
 }
@@ -1823,7 +1826,7 @@ static void crc_host_tables(CrcTabs& T) {
 struct lsmblk_ctx {
   int device = 0;
   std::mutex mu;
-  uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket
+  uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket, [2] emit big-block count
   uint32_t* dec_agg = nullptr;   // (entries, key bytes, value bytes) per block
   uint64_t dec_cap = 0;
   CrcTabs* crc_tabs = nullptr;   // CRC-32 slicing + zero-extension tables (first CRC call)
@@ -1836,6 +1839,7 @@ struct lsmblk_ctx {
   uint32_t* rec_first = nullptr; // n+1
   uint32_t* blk_first = nullptr;
   uint32_t* ent = nullptr;       // 3 per entry: rec, alcp, block sizes (plan passes)
+  uint32_t* big_list = nullptr;  // n+1: blocks for emit_big_kernel
   uint64_t rec_cap = 0;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
@@ -1902,6 +1906,8 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
     if ((rc = grow(&c->blk_first, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
     if ((rc = grow(&c->ent, &cap, entries + 1, 3))) return rc;
+    cap = c->rec_cap;
+    if ((rc = grow(&c->big_list, &cap, entries + 1, 1))) return rc;
     c->rec_cap = cap;
   }
   return LSMBLK_OK;
@@ -1954,6 +1960,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->seg_inc);
   (void)hipFree(c->rec_first);
   (void)hipFree(c->ent);
+  (void)hipFree(c->big_list);
   (void)hipFree(c->blk_first);
   (void)hipFree(c->crc_tabs);
   for (auto& e : c->ev)
@@ -2129,7 +2136,10 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   e.blk_cap = blk_cap;
   e.n = in->n;
   e.stats = stats;
+  e.big_list = c->big_list;
+  e.big_cnt = c->counters + 2;
   e.skip = c->skip;
+  if (hipMemsetAsync(e.big_cnt, 0, sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   int per_cu = 0;
@@ -2137,6 +2147,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
   hipLaunchKernelGGL(emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  hipLaunchKernelGGL(emit_big_kernel, dim3(uint32_t(cus) * 4), dim3(256), 0, st, e);
   if (c->timing) (void)hipEventRecord(c->ev[6], st);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
