@@ -618,48 +618,103 @@ __device__ __forceinline__ void copy_run(const rsrc_t& RS, uint32_t so, uint32_t
   }
 }
 
+// The same copy by the whole wave (len >= 16, wave-uniform arguments): lane j moves pieces
+// j, j + 64, ... so a wave instruction moves 1 KiB of contiguous bytes.  Values of
+// kCoop bytes or more go this way: one long value no longer keeps 63 lanes idle.
+constexpr uint32_t kCoop = 256;
+__device__ __forceinline__ void copy_run_wave(const rsrc_t& RS, uint32_t so, const rsrc_t& RD, uint32_t dof,
+                                              uint32_t len) {
+  const uint32_t l = lane_id();
+  const uint32_t np = (len + 15) >> 4, last = len - 16;
+  for (uint32_t j0 = 0; j0 < np; j0 += 64 * kBigB) {
+    u32x4 q[kBigB];
+#pragma unroll
+    for (uint32_t j = 0; j < kBigB; ++j) {
+      const uint32_t idx = j0 + 64 * j + l;
+      if (idx < np) q[j] = gload16(RS, so + min(16 * idx, last));
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kBigB; ++j) {
+      const uint32_t idx = j0 + 64 * j + l;
+      if (idx < np) {
+        const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+        st16(RD, dof + min(16 * idx, last), v);
+      }
+    }
+  }
+}
+
+// Copies of every lane's run of kCoop bytes or more, one after another by the whole wave.
+__device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, uint32_t so, const rsrc_t& RD,
+                                               uint32_t dof, uint32_t len) {
+  for (uint64_t m = __ballot(longrun); m; m &= m - 1) {
+    const uint32_t j = uint32_t(__builtin_ctzll(m));
+    copy_run_wave(RS, __builtin_amdgcn_readlane(so, j), RD, __builtin_amdgcn_readlane(dof, j),
+                  __builtin_amdgcn_readlane(len, j));
+  }
+}
+
+// One entry of a large block: ts / key_off / val_off, and the key (first-key bytes below p,
+// suffix bytes from there on, one 16-B load of each source per piece, merged under byte
+// masks; byte loads where a piece would read past the block end).
+__device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecLds& L, const GlbImg& im, uint32_t k,
+                                              uint32_t lim, const rsrc_t& RK, uint32_t kb, uint64_t E0, uint64_t K0,
+                                              uint64_t V0) {
+  const rsrc_t& R = im.r;
+  const uint32_t lead = im.lead, fk = lead + 4;  // descriptor byte of the first key
+  const uint32_t epos = L.epos[k], p = L.pfx[k], s = L.sfx[k], kout = L.kout[k];
+  const uint32_t sb = lead + epos + 4, kl = p + s;  // descriptor byte of the suffix
+  const uint64_t e = E0 + k;
+  a.ts[e] = im.u64(epos + 4 + s);
+  a.key_off[e] = uint32_t(K0 + kout);
+  a.val_off[e] = uint32_t(V0 + L.vout[k]);
+  for (uint32_t t = 0; t < kl; t += 16) {
+    const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
+    uint32_t v[4];
+    if (sb + o >= p && sb + o - p + 16 <= lim && fk + o + 16 <= lim) {
+      const u32x4 sq = gload16(R, sb + o - p), fq = gload16(R, fk + o);
+      const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w}, fv[4] = {fq.x, fq.y, fq.z, fq.w};
+#pragma unroll
+      for (uint32_t d = 0; d < 4; ++d) {
+        const int32_t nf = int32_t(p) - int32_t(o + 4 * d);  // leading bytes from the first key
+        const uint32_t m = nf <= 0 ? 0u : nf >= 4 ? ~0u : (1u << (8 * nf)) - 1;
+        v[d] = (fv[d] & m) | (sv[d] & ~m);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t d = 0; d < 4; ++d) {
+        uint32_t wd = 0;
+        for (uint32_t i = 0; i < 4; ++i) {
+          const uint32_t x = o + 4 * d + i;
+          wd |= (x < p ? im.u8(4 + x) : im.u8(epos + 4 + x - p)) << (8 * i);
+        }
+        v[d] = wd;
+      }
+    }
+    if (kl >= 16) st16(RK, kb + kout + o, v);
+    else st_short(RK, kb + kout, kl, v);
+  }
+}
+
 __device__ void dec_big_outputs(const DecodeArgs& a, const DecLds& L, const rsrc_t& R, uint32_t lead,
                                 const BlockHdr& h, uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V) {
   const uint32_t l = lane_id();
   const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
   const rsrc_t RK = make_rsrc_exact(a.keys + (K0 - kb), kb + K), RV = make_rsrc_exact(a.vals + (V0 - vb), vb + V);
   const GlbImg im{R, lead};
-  const uint32_t fk = lead + 4, lim = lead + h.len;  // descriptor bytes: first key, block end
-  for (uint32_t k = l; k < h.n; k += 64) {
-    const uint32_t epos = L.epos[k], p = L.pfx[k], s = L.sfx[k];
-    const uint32_t kout = L.kout[k], vout = L.vout[k], vl = L.vout[k + 1] - vout;
-    const uint32_t sb = lead + epos + 4, kl = p + s;  // descriptor byte of the suffix
-    const uint64_t e = E0 + k;
-    a.ts[e] = im.u64(epos + 4 + s);
-    a.key_off[e] = uint32_t(K0 + kout);
-    a.val_off[e] = uint32_t(V0 + vout);
-    for (uint32_t t = 0; t < kl; t += 16) {  // key byte x: first key x < p, else suffix x - p
-      const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
-      uint32_t v[4];
-      if (sb + o >= p && sb + o - p + 16 <= lim && fk + o + 16 <= lim) {
-        const u32x4 sq = gload16(R, sb + o - p), fq = gload16(R, fk + o);
-        const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w}, fv[4] = {fq.x, fq.y, fq.z, fq.w};
-#pragma unroll
-        for (uint32_t d = 0; d < 4; ++d) {
-          const int32_t nf = int32_t(p) - int32_t(o + 4 * d);
-          const uint32_t m = nf <= 0 ? 0u : nf >= 4 ? ~0u : (1u << (8 * nf)) - 1;
-          v[d] = (fv[d] & m) | (sv[d] & ~m);
-        }
-      } else {
-#pragma unroll
-        for (uint32_t d = 0; d < 4; ++d) {
-          uint32_t wd = 0;
-          for (uint32_t i = 0; i < 4; ++i) {
-            const uint32_t x = o + 4 * d + i;
-            wd |= (x < p ? im.u8(4 + x) : im.u8(epos + 4 + x - p)) << (8 * i);
-          }
-          v[d] = wd;
-        }
-      }
-      if (kl >= 16) st16(RK, kb + kout + o, v);
-      else st_short(RK, kb + kout, kl, v);
+  const uint32_t lim = lead + h.len;  // descriptor byte of the block end
+  for (uint32_t c = 0; c < h.n; c += 64) {  // uniform trip count: the wave copies long values
+    const uint32_t k = c + l;
+    const bool live = k < h.n;
+    uint32_t vsrc = 0, vdst = 0, vl = 0;
+    if (live) {
+      dec_big_entry(a, L, im, k, lim, RK, kb, E0, K0, V0);
+      vsrc = lead + L.epos[k] + 14 + L.sfx[k];
+      vdst = vb + L.vout[k];
+      vl = L.vout[k + 1] - L.vout[k];
+      if (vl < kCoop) copy_run(R, vsrc, lim, RV, vdst, vl);
     }
-    copy_run(R, sb + s + 10, lim, RV, vb + vout, vl);
+    copy_long_runs(live && vl >= kCoop, R, vsrc, RV, vdst, vl);
   }
 }
 
@@ -1304,8 +1359,10 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
     const uint64_t incl = wave_incl_scan<uint64_t>(dg);
     const uint64_t pos = dc + incl - dg;
     dc += __shfl(incl, 63, 64);
+    uint32_t vdst = 0;
     if (k < n) {
       const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
+      vdst = at + 14 + sfx;
       // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value
       __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
       copy_run(RK, kp + p, klim, RO, at + 4, sfx);
@@ -1313,11 +1370,12 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bswap32(uint32_t(tsv >> 32)), __builtin_bswap32(uint32_t(tsv))},
                                             RO, at + 4 + sfx, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(vl & 0xFFFF)), RO, at + 12 + sfx, 0, 0);
-      copy_run(RV, vp, vlim, RO, at + 14 + sfx, vl);
+      if (vl < kCoop) copy_run(RV, vp, vlim, RO, vdst, vl);
       // builder.rs:71: offsets.push(data.len() as u16), BE
       __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO,
                                             ob + uint32_t(data_len) + 2 * k, 0, 0);
     }
+    copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl);
   }
   if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
   if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
