@@ -23,6 +23,8 @@
  *                                                           112-123), one segment per SST
  *       lsmblk_crc32_batch   the per-block framing checksum  (src/table/builder.rs:120-122,
  *                                                           src/table.rs:226-230)
+ *       lsmblk_block_meta_batch  the SST BlockMeta section per segment  (src/table.rs:29-63,
+ *                                                           src/table/builder.rs:68-77)
  *     All pointers are DEVICE pointers; calls are asynchronous on `stream` (a hipStream_t
  *     passed as void*; NULL = the default stream).  Thread-safe per distinct context.
  *
@@ -189,6 +191,32 @@ int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint3
  * 2 GiB; its crc is then 0).  Asynchronous like the calls above. */
 int lsmblk_crc32_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off,
                        uint64_t nblk, uint32_t tail, uint32_t* crc, uint64_t* stats, void* stream);
+
+/* Segment -> block table after an encode: seg_blk[s] (u32[nseg+1]) = index of segment s's
+ * first block in the lsmblk_encode_batch output (seg_blk[nseg] = nblk).  Must be called on the
+ * same context and stream as that encode, before the next encode on the context; seg_start and
+ * enc_stats are the encode's own arguments (device pointers).  After a failed encode every
+ * entry is 0.  Asynchronous. */
+int lsmblk_encode_segment_blocks(lsmblk_ctx* ctx, const uint32_t* seg_start, uint32_t nseg,
+                                 const uint64_t* enc_stats, uint32_t* seg_blk, void* stream);
+
+/* SST BlockMeta sections (SURVEY.md §8 f, row 1): for every segment s (an SST, blocks
+ * seg_blk[s] .. seg_blk[s+1]) the bytes BlockMeta::encode_block_meta writes after the SST data
+ * section (src/table.rs:29-63, called at src/table/builder.rs:77), as SsTableBuilder produces
+ * them: offset = the block's position in the framed data section (every block followed by its
+ * u32 CRC, builder.rs:118-122), first/last key = the block's first/last key with ts 0
+ * (key.rs:166-169), max_ts = 0, CRC-32 of the section after its u32 count.  The keys are parsed
+ * from the blocks themselves.  Block b = blocks[blk_off[b] .. blk_off[b+1] - tail): tail = 0 for
+ * packed blocks (encode output), 4 over a framed data section.  Section s is written to
+ * meta[meta_off[s] .. meta_off[s+1]) (meta_off u64[nseg+1]; meta_cap >= 16).  stats: [0] nseg
+ * [1] bytes required [3] error flags (MALFORMED: a block without entries or whose first/last
+ * entry does not parse; CAPACITY: meta_cap too small, stats[1] = required; SEGMENTS: bad
+ * seg_blk).  A segment without blocks gets the 16-byte section of an empty meta list (the
+ * reference would panic building an empty SST).  Asynchronous. */
+int lsmblk_block_meta_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off,
+                            uint64_t nblk, uint32_t tail, const uint32_t* seg_blk, uint32_t nseg,
+                            uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off, uint64_t* stats,
+                            void* stream);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,8 @@ SIGNATURES = [
     ("lsmblk_decode_batch", I, [P, P, P, U64, ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, P, U64, P, U64, P, P]),
     ("lsmblk_crc32_batch", I, [P, P, P, U64, U32, P, P, P]),
+    ("lsmblk_encode_segment_blocks", I, [P, P, U32, P, P, P]),
+    ("lsmblk_block_meta_batch", I, [P, P, P, U64, U32, P, U32, P, U64, P, P, P]),
 ]
 
 

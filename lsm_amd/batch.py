@@ -6,6 +6,9 @@
                  of segments (reference src/table/builder.rs:48-65,112-123)
   crc32_blocks   the per-block SST framing checksum (crc32fast::hash, reference
                  src/table/builder.rs:120-122, verified at src/table.rs:226-230)
+  block_meta     the SST BlockMeta section of every segment (BlockMeta::encode_block_meta,
+                 reference src/table.rs:29-63, written by SsTableBuilder::build :68-77)
+  encode_sst     encode_kv + the segment -> block table + block_meta in one stream
 
 Tensors live on a ROCm device (torch is only the allocator / stream provider).  The work
 is done by liblsmblk.so; there is no CPU path here.
@@ -198,3 +201,76 @@ def crc32_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None, tail:
     if st:
         raise LsmBlkError(st, "crc32_blocks")
     return crc[:nblk]
+
+
+def segment_blocks_into(seg_start: torch.Tensor, nseg: int, enc_stats: torch.Tensor, seg_blk: torch.Tensor,
+                        stream=None):
+    """After encode_into on the same device/stream: seg_blk[s] = first block of segment s."""
+    dev = _dev_index(seg_start)
+    check(lib().lsmblk_encode_segment_blocks(_ctx(dev), seg_start.data_ptr(), nseg, enc_stats.data_ptr(),
+                                             seg_blk.data_ptr(), _stream_ptr(stream, dev)),
+          "lsmblk_encode_segment_blocks")
+
+
+def block_meta_into(blocks, blk_off, nblk, seg_blk, nseg, meta, meta_cap, meta_off, stats, stream=None, tail=0):
+    """Asynchronous BlockMeta sections into preallocated buffers (no host sync)."""
+    dev = _dev_index(blk_off)
+    check(lib().lsmblk_block_meta_batch(_ctx(dev), _ptr(blocks), blk_off.data_ptr(), nblk, tail, seg_blk.data_ptr(),
+                                        nseg, meta.data_ptr(), meta_cap, meta_off.data_ptr(), stats.data_ptr(),
+                                        _stream_ptr(stream, dev)), "lsmblk_block_meta_batch")
+
+
+def block_meta(blocks: torch.Tensor, blk_off: torch.Tensor, seg_blk, stream=None, tail: int = 0):
+    """BlockMeta::encode_block_meta (reference src/table.rs:29-63) of every segment, as
+    SsTableBuilder::build writes it after the SST data section (src/table/builder.rs:68-77).
+    seg_blk[s] .. seg_blk[s+1] are segment s's blocks.  Returns (meta u8 tensor, meta_off
+    int64 tensor[nseg+1]); section s = meta[meta_off[s]:meta_off[s+1]]."""
+    dev = torch.device("cuda", _dev_index(blk_off))
+    if not isinstance(seg_blk, torch.Tensor):
+        seg_blk = torch.from_numpy(np.ascontiguousarray(seg_blk, np.uint32).view(np.int32))
+    seg_blk = seg_blk.to(dev)
+    nseg, nblk = seg_blk.numel() - 1, blk_off.numel() - 1
+    meta_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    cap = 16 * nseg + 56 * max(nblk, 1)
+    for _ in range(2):
+        meta = _aligned_empty(cap, dev)
+        block_meta_into(blocks, blk_off, nblk, seg_blk, nseg, meta, cap, meta_off, stats, stream, tail)
+        torch.cuda.synchronize(dev)
+        st = _status(stats)
+        if st == LSMBLK_E_CAPACITY:
+            cap = int(stats[1].item())
+            continue
+        if st:
+            raise LsmBlkError(st, "block_meta")
+        return meta[:int(stats[1].item())], meta_off
+    raise LsmBlkError(LSMBLK_E_CAPACITY, "block_meta")
+
+
+def encode_sst(kv: KVStream, seg_start, block_size: int, stream=None):
+    """One SsTableBuilder per segment, on the device: the packed blocks, their per-block
+    CRC-32s (finish_block, src/table/builder.rs:112-123) and the BlockMeta sections (build,
+    :68-77).  Returns dict(blocks, blk_off, seg_blk, crc, meta, meta_off)."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    if not isinstance(seg_start, torch.Tensor):
+        seg_start = torch.from_numpy(np.ascontiguousarray(seg_start, np.uint32).view(np.int32))
+    seg_start = seg_start.to(dev)
+    nseg = seg_start.numel() - 1
+    kb = int(kv.key_off[kv.n].item()) if kv.n else 0
+    vb = int(kv.val_off[kv.n].item()) if kv.n else 0
+    out_cap, blk_cap = encode_bound(kv, kb & 0xFFFFFFFF, vb & 0xFFFFFFFF)
+    out = _aligned_empty(out_cap, dev)
+    blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    seg_blk = torch.zeros(nseg + 1, dtype=torch.int32, device=dev)
+    encode_into(kv, seg_start, nseg, block_size, out, out_cap, blk_off, blk_cap, stats, stream)
+    segment_blocks_into(seg_start, nseg, stats, seg_blk, stream)
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "encode_sst")
+    nblk, nbytes = stats[0].item(), stats[1].item()
+    blocks, blk_off = out[:nbytes], blk_off[:nblk + 1]
+    crc = crc32_blocks(blocks, blk_off, stream)
+    meta, meta_off = block_meta(blocks, blk_off, seg_blk, stream)
+    return dict(blocks=blocks, blk_off=blk_off, seg_blk=seg_blk, crc=crc, meta=meta, meta_off=meta_off)

@@ -1880,6 +1880,214 @@ static void crc_host_tables(CrcTabs& T) {
   }
 }
 
+// ---------------------------------------------------------------- SST BlockMeta section
+// SsTableBuilder::build -> BlockMeta::encode_block_meta (src/table.rs:29-63), one section per
+// segment (SST):
+//   u32 num | { u32 offset | u16 flen | first_key | u64 0 | u16 llen | last_key | u64 0 }*
+//   | u64 max_ts (0) | u32 crc32(section[4 .. len - 4])              (big-endian integers)
+// The keys come from the encoded blocks themselves: entry 0 holds the whole first key
+// (get_first_key, src/block/iterator.rs:23-34) and the last entry is first_key[..p] || suffix.
+// BlockMeta keys carry ts 0 (KeyVec::set_from_slice copies key bytes only, src/key.rs:166-169)
+// and SsTableBuilder never raises max_ts (src/table/builder.rs:41,77).  offset = the block's
+// position in the SST data section, where every block is followed by its u32 CRC (:118-122).
+// Four small launches: record sizes per block, one-workgroup tile scan, record writes (one
+// lane per block), section headers; then crc_kernel over the sections and the CRC stores.
+// The section is ~1.3 % of the block bytes at config U (56 B per 4 KiB block).
+constexpr uint32_t kMetaTile = 256;  // blocks per workgroup (one lane each)
+
+struct MetaArgs {
+  const uint8_t* blocks;
+  const uint64_t* blk_off;
+  uint64_t nblk;
+  uint32_t tail;            // bytes after each block inside its blk_off range (4 = framed)
+  uint32_t nseg;
+  const uint32_t* seg_blk;  // nseg + 1: segment s = blocks [seg_blk[s], seg_blk[s+1])
+  uint8_t* meta;
+  uint64_t meta_cap;
+  uint64_t* meta_off;       // nseg + 1 (output)
+  uint32_t* rec;            // nblk: record bytes
+  uint64_t* tile_sum;       // per kMetaTile-block tile
+  uint64_t* tile_pre;
+  uint64_t* pos;            // nblk + 1: exclusive prefix of rec
+  const uint32_t* crc;      // nseg: section CRCs (crc_kernel output)
+  const uint64_t* crc_stats;
+  uint64_t* stats;
+};
+
+struct MetaBlk {
+  uint64_t base;
+  uint32_t s0, loff, p, s;
+  bool ok;
+};
+
+__device__ __forceinline__ void or_err(uint64_t* stats, uint32_t err) {
+  if (err) atomicOr(reinterpret_cast<unsigned long long*>(stats + 3), (unsigned long long)err);
+}
+
+// Parse block b's first key length and last entry; ok = false where the reference would panic
+// (no entries, trailer/offsets past the block, first or last entry past the data).
+__device__ MetaBlk meta_parse(const MetaArgs& a, uint64_t b) {
+  MetaBlk m{};
+  const uint64_t base = a.blk_off[b], end = a.blk_off[b + 1];
+  m.base = base;
+  if (end < base || end - base < uint64_t(a.tail) + 2) return m;
+  const uint64_t len = end - base - a.tail;
+  const uint8_t* q = a.blocks + base;
+  auto be16 = [&](uint64_t i) { return (uint32_t(q[i]) << 8) | q[i + 1]; };
+  const uint32_t n = be16(len - 2);
+  if (n == 0 || 2 + 2ull * n > len) return m;
+  const uint64_t dend = len - 2 - 2ull * n;
+  if (dend < 4) return m;
+  m.s0 = be16(2);
+  if (4ull + m.s0 + 8 > dend) return m;
+  m.loff = be16(dend + 2ull * (n - 1));
+  if (m.loff + 4ull > dend) return m;
+  m.p = be16(m.loff);
+  m.s = be16(m.loff + 2);
+  if (m.loff + 4ull + m.s > dend || m.p > m.s0 || m.p + m.s == 0) return m;
+  m.ok = true;
+  return m;
+}
+
+__global__ __launch_bounds__(256) void meta_size_kernel(MetaArgs a) {
+  const uint64_t b = uint64_t(blockIdx.x) * kMetaTile + threadIdx.x;
+  uint32_t r = 0;
+  if (b < a.nblk) {
+    const MetaBlk m = meta_parse(a, b);
+    if (!m.ok) or_err(a.stats, LSMBLK_ERR_MALFORMED);
+    r = 24u + (m.ok ? m.s0 + m.p + m.s : 0u);
+    a.rec[b] = r;
+  }
+  __shared__ uint32_t ws[4];
+  const uint32_t t = wave_sum32(r);
+  if (lane_id() == 0) ws[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) a.tile_sum[blockIdx.x] = uint64_t(ws[0]) + ws[1] + ws[2] + ws[3];
+}
+
+// One workgroup: exclusive scan of the tile sums, the total, the capacity check and the
+// segment-table check (seg_blk[0] = 0, non-decreasing, seg_blk[nseg] = nblk).
+__global__ __launch_bounds__(1024) void meta_scan_kernel(MetaArgs a) {
+  const uint32_t t = threadIdx.x;
+  const uint64_t ntiles = (a.nblk + kMetaTile - 1) / kMetaTile;
+  const uint64_t per = (ntiles + 1023) / 1024;
+  const uint64_t lo = min(ntiles, t * per), hi = min(ntiles, lo + per);
+  uint64_t s = 0;
+  for (uint64_t i = lo; i < hi; ++i) s += a.tile_sum[i];
+  __shared__ uint64_t wsum[16];
+  const uint64_t inc = wave_incl_scan<uint64_t>(s);
+  if (lane_id() == 63) wsum[t >> 6] = inc;
+  __syncthreads();
+  uint64_t base = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
+  uint64_t run = base + inc - s;
+  for (uint64_t i = lo; i < hi; ++i) {
+    a.tile_pre[i] = run;
+    run += a.tile_sum[i];
+  }
+  uint32_t err = 0;
+  if (t == 1023) {
+    const uint64_t total = base + inc, need = total + 16ull * a.nseg;
+    a.pos[a.nblk] = total;
+    a.stats[0] = a.nseg;
+    a.stats[1] = need;
+    if (need > a.meta_cap) err |= LSMBLK_ERR_CAPACITY;
+  }
+  for (uint64_t g = t; g <= a.nseg; g += 1024) {
+    const uint32_t v = a.seg_blk[g];
+    if ((g == 0 && v != 0) || (g == a.nseg && v != a.nblk) || (g < a.nseg && v > a.seg_blk[g + 1]))
+      err |= LSMBLK_ERR_SEGMENTS;
+  }
+  or_err(a.stats, err);
+}
+
+__device__ __forceinline__ void put_be(uint8_t* d, uint64_t v, uint32_t nbytes) {
+  for (uint32_t i = 0; i < nbytes; ++i) d[i] = uint8_t(v >> (8 * (nbytes - 1 - i)));
+}
+
+// One lane per block: its position (tile prefix + in-workgroup scan), its segment (binary
+// search of seg_blk) and the record bytes.
+__global__ __launch_bounds__(256) void meta_write_kernel(MetaArgs a) {
+  if (a.stats[3]) return;
+  const uint64_t b = uint64_t(blockIdx.x) * kMetaTile + threadIdx.x;
+  const uint32_t r = b < a.nblk ? a.rec[b] : 0u;
+  const uint32_t inc = wave_incl_scan32(r);
+  __shared__ uint32_t ws[4];
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane_id() == 63) ws[w] = inc;
+  __syncthreads();
+  if (b >= a.nblk) return;
+  uint64_t pos = a.tile_pre[blockIdx.x] + inc - r;
+  for (uint32_t j = 0; j < w; ++j) pos += ws[j];
+  a.pos[b] = pos;
+  uint32_t lo = 0, hi = a.nseg;  // largest seg with seg_blk[seg] <= b
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.seg_blk[mid] <= b) lo = mid; else hi = mid;
+  }
+  const uint32_t seg = lo;
+  const uint64_t first = a.seg_blk[seg];
+  const MetaBlk m = meta_parse(a, b);
+  const uint64_t off = a.blk_off[b] - a.blk_off[first] + (4ull - a.tail) * (b - first);
+  uint8_t* d = a.meta + pos + 16ull * seg + 4;
+  const uint8_t* q = a.blocks + m.base;
+  put_be(d, uint32_t(off), 4);  // offset as u32 (table.rs:44)
+  put_be(d + 4, m.s0, 2);
+  for (uint32_t i = 0; i < m.s0; ++i) d[6 + i] = q[4 + i];
+  d += 6 + m.s0;
+  put_be(d, 0, 8);
+  put_be(d + 8, (m.p + m.s) & 0xFFFFu, 2);
+  for (uint32_t i = 0; i < m.p; ++i) d[10 + i] = q[4 + i];
+  for (uint32_t i = 0; i < m.s; ++i) d[10 + m.p + i] = q[m.loff + 4 + i];
+  put_be(d + 10 + m.p + m.s, 0, 8);
+}
+
+// One lane per segment: section offsets, u32 num and u64 max_ts.  After an error every offset
+// is 0, so the CRC pass over the sections reads nothing.
+__global__ __launch_bounds__(256) void meta_seg_kernel(MetaArgs a) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (g >= a.nseg) return;
+  if (a.stats[3]) {
+    a.meta_off[g] = 0;
+    if (g == a.nseg - 1) a.meta_off[a.nseg] = 0;
+    return;
+  }
+  const uint32_t b0 = a.seg_blk[g], b1 = a.seg_blk[g + 1];
+  const uint64_t st = a.pos[b0] + 16ull * g, en = a.pos[b1] + 16ull * (g + 1);
+  a.meta_off[g] = st;
+  if (g == a.nseg - 1) a.meta_off[a.nseg] = en;
+  put_be(a.meta + st, b1 - b0, 4);
+  put_be(a.meta + en - 12, 0, 8);
+}
+
+__global__ __launch_bounds__(256) void meta_crc_put_kernel(MetaArgs a) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (a.stats[3]) return;
+  if (g == 0) or_err(a.stats, uint32_t(a.crc_stats[3]));
+  if (g >= a.nseg) return;
+  put_be(a.meta + a.meta_off[g + 1] - 4, a.crc[g], 4);
+}
+
+// Segment -> first block after an encode: seg_blk[s] = lower_bound(blk_first[0 .. nblk),
+// seg_start[s]) -- every non-empty segment starts a block (table/builder.rs:48-65).
+__global__ __launch_bounds__(256) void seg_blocks_kernel(const uint32_t* blk_first, const uint64_t* enc_stats,
+                                                        const uint32_t* seg_start, uint32_t nseg,
+                                                        uint32_t* seg_blk) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (g > nseg) return;
+  if (enc_stats[3]) {
+    seg_blk[g] = 0;
+    return;
+  }
+  const uint32_t key = seg_start[g];
+  uint32_t lo = 0, hi = uint32_t(enc_stats[0]);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (blk_first[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  seg_blk[g] = lo;
+}
+
 // ================================================================ host side
 struct lsmblk_ctx {
   int device = 0;
@@ -1905,6 +2113,15 @@ struct lsmblk_ctx {
   bool timing = false;           // record HIP events around every kernel (diagnostics)
   hipEvent_t ev[8] = {};         // decode: 0 count 1 scan 2 decode 3 | encode: 4 plan 5 emit 6
   bool dec_timed = false, enc_timed = false;
+  // BlockMeta sections (lsmblk_block_meta_batch)
+  uint32_t* meta_rec = nullptr;     // nblk
+  uint64_t* meta_pos = nullptr;     // nblk + 1
+  uint64_t meta_blk_cap = 0;
+  uint64_t* meta_tile = nullptr;    // 2 per tile: sums, prefixes
+  uint64_t meta_tile_cap = 0;
+  uint32_t* meta_crc = nullptr;     // nseg
+  uint64_t meta_seg_cap = 0;
+  uint64_t* meta_cstats = nullptr;  // crc_kernel stats of the section CRC pass
 };
 
 namespace {
@@ -1985,6 +2202,9 @@ int next_epoch(lsmblk_ctx* c, hipStream_t st) {
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+int ensure_crc_tabs(lsmblk_ctx* c);
+int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+               uint32_t* crc, uint64_t* stats, hipStream_t st);
 
 }  // namespace
 
@@ -2021,6 +2241,11 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->big_list);
   (void)hipFree(c->blk_first);
   (void)hipFree(c->crc_tabs);
+  (void)hipFree(c->meta_rec);
+  (void)hipFree(c->meta_pos);
+  (void)hipFree(c->meta_tile);
+  (void)hipFree(c->meta_crc);
+  (void)hipFree(c->meta_cstats);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2215,18 +2440,97 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
   if (!c || !blk_off || !stats || (nblk && !crc)) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
-  if (!c->crc_tabs) {
-    CrcTabs h;
-    crc_host_tables(h);
-    if (hipMalloc(reinterpret_cast<void**>(&c->crc_tabs), sizeof(CrcTabs)) != hipSuccess) {
-      c->crc_tabs = nullptr;
-      return LSMBLK_E_NOMEM;
-    }
-    if (hipMemcpy(c->crc_tabs, &h, sizeof(CrcTabs), hipMemcpyHostToDevice) != hipSuccess) return LSMBLK_E_HIP;
-  }
+  int rc = ensure_crc_tabs(c);
+  if (rc) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nblk == 0) return LSMBLK_OK;
+  return launch_crc(c, blocks, blk_off, nblk, tail, crc, stats, st);
+}
+
+int lsmblk_encode_segment_blocks(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg, const uint64_t* enc_stats,
+                                 uint32_t* seg_blk, void* stream) {
+  if (!c || !seg_start || !enc_stats || !seg_blk) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  if (!c->blk_first) return LSMBLK_E_INVAL;  // no encode ran on this context
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg) + 256) / 256)), dim3(256), 0, st,
+                     c->blk_first, enc_stats, seg_start, nseg, seg_blk);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
+                            uint32_t tail, const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap,
+                            uint64_t* meta_off, uint64_t* stats, void* stream) {
+  if (!c || !blk_off || !seg_blk || !meta_off || !stats || !meta || meta_cap < 16) return LSMBLK_E_INVAL;
+  if (nseg == 0 || nblk >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  int rc = ensure_crc_tabs(c);
+  if (rc) return rc;
+  const uint64_t ntiles = (nblk + kMetaTile - 1) / kMetaTile;
+  if (nblk + 1 > c->meta_blk_cap) {
+    uint64_t cap = c->meta_blk_cap;
+    if ((rc = grow(&c->meta_rec, &cap, nblk + 1, 1))) return rc;
+    cap = c->meta_blk_cap;
+    if ((rc = grow(&c->meta_pos, &cap, nblk + 1, 1))) return rc;
+    c->meta_blk_cap = cap;
+  }
+  if ((rc = grow(&c->meta_tile, &c->meta_tile_cap, ntiles + 1, 2))) return rc;
+  if ((rc = grow(&c->meta_crc, &c->meta_seg_cap, nseg, 1))) return rc;
+  if (!c->meta_cstats && hipMalloc(reinterpret_cast<void**>(&c->meta_cstats), LSMBLK_STATS_WORDS * 8) != hipSuccess) {
+    c->meta_cstats = nullptr;
+    return LSMBLK_E_NOMEM;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  MetaArgs a;
+  a.blocks = blocks;
+  a.blk_off = blk_off;
+  a.nblk = nblk;
+  a.tail = tail;
+  a.nseg = nseg;
+  a.seg_blk = seg_blk;
+  a.meta = meta;
+  a.meta_cap = meta_cap;
+  a.meta_off = meta_off;
+  a.rec = c->meta_rec;
+  a.tile_sum = c->meta_tile;
+  a.tile_pre = c->meta_tile + c->meta_tile_cap;
+  a.pos = c->meta_pos;
+  a.crc = c->meta_crc;
+  a.crc_stats = c->meta_cstats;
+  a.stats = stats;
+  const uint32_t sg = uint32_t((uint64_t(nseg) + 255) / 256);
+  if (ntiles) hipLaunchKernelGGL(meta_size_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(meta_scan_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (ntiles) hipLaunchKernelGGL(meta_write_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(meta_seg_kernel, dim3(sg), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
+  // section CRC over [meta_off[s] + 4, meta_off[s+1] - 4): blocks = meta + 4, tail = 8
+  if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if ((rc = launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st))) return rc;
+  hipLaunchKernelGGL(meta_crc_put_kernel, dim3(sg), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+}  // extern "C"
+
+namespace {
+int ensure_crc_tabs(lsmblk_ctx* c) {
+  if (c->crc_tabs) return LSMBLK_OK;
+  CrcTabs h;
+  crc_host_tables(h);
+  if (hipMalloc(reinterpret_cast<void**>(&c->crc_tabs), sizeof(CrcTabs)) != hipSuccess) {
+    c->crc_tabs = nullptr;
+    return LSMBLK_E_NOMEM;
+  }
+  return hipMemcpy(c->crc_tabs, &h, sizeof(CrcTabs), hipMemcpyHostToDevice) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+               uint32_t* crc, uint64_t* stats, hipStream_t st) {
   CrcArgs a;
   a.blocks = blocks;
   a.blk_off = blk_off;
@@ -2244,5 +2548,4 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
   hipLaunchKernelGGL(crc_kernel, dim3(uint32_t(want < cap ? want : cap)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
-
-}  // extern "C"
+}  // namespace

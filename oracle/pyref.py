@@ -102,3 +102,65 @@ def encode_segments(entries, seg_start, block_size):
         if not b.is_empty():
             blocks.append(b.build_encoded())
     return blocks
+
+
+def sst_block_metas(entries, block_size):
+    """SsTableBuilder::add / finish_block (table/builder.rs:48-65, 112-123) for ONE SST ->
+    [(offset, first_key, last_key)] per block.  offset = data.len() before the block, where the
+    data section holds every block followed by its u32 CRC (:118-122).  first_key / last_key are
+    set with KeyVec::set_from_slice (key.rs:166-169), which copies the key bytes only: the
+    BlockMeta keys keep ts 0."""
+    metas, data_len = [], 0
+    b, first, last = BlockBuilder(block_size), b"", b""
+    for key, ts, value in entries:
+        if not first:  # :49-51
+            first = key
+        if b.add(key, ts, value):  # :55-58
+            last = key
+            continue
+        blk = b.build_encoded()  # finish_block, :112-123
+        metas.append((data_len, first, last))
+        data_len += len(blk) + 4
+        b = BlockBuilder(block_size)
+        assert b.add(key, ts, value)  # :62-64
+        first = last = key
+    if not b.is_empty():  # build() -> finish_block (:73)
+        metas.append((data_len, first, last))
+    return metas
+
+
+def encode_block_meta(metas, max_ts=0) -> bytes:
+    """BlockMeta::encode_block_meta (table.rs:29-63): u32 num | {u32 offset | u16 len | first
+    key | u64 ts | u16 len | last key | u64 ts}* | u64 max_ts | u32 crc32 of everything after
+    num (`buf[original_len + 4..]`).  Key ts are 0 (see sst_block_metas); SsTableBuilder never
+    raises max_ts from 0 (table/builder.rs:41, 77)."""
+    import zlib
+    body = bytearray()
+    for off, fk, lk in metas:
+        body += struct.pack(">I", off & 0xFFFFFFFF)
+        body += U16.pack(len(fk) & 0xFFFF) + fk + U64.pack(0)
+        body += U16.pack(len(lk) & 0xFFFF) + lk + U64.pack(0)
+    body += U64.pack(max_ts)
+    return struct.pack(">I", len(metas) & 0xFFFFFFFF) + bytes(body) + struct.pack(">I", zlib.crc32(body))
+
+
+def decode_block_meta(buf: bytes):
+    """BlockMeta::decode_block_meta (table.rs:65-93) -> ([(offset, first_key, last_key)], max_ts);
+    raises ValueError on the reference's "meta checksum mismatched"."""
+    import zlib
+    num = struct.unpack_from(">I", buf, 0)[0]
+    checksum = zlib.crc32(buf[4:len(buf) - 4])
+    pos, metas = 4, []
+    for _ in range(num):
+        off = struct.unpack_from(">I", buf, pos)[0]
+        fl = U16.unpack_from(buf, pos + 4)[0]
+        fk = bytes(buf[pos + 6:pos + 6 + fl])
+        pos += 6 + fl + 8
+        ll = U16.unpack_from(buf, pos)[0]
+        lk = bytes(buf[pos + 2:pos + 2 + ll])
+        pos += 2 + ll + 8
+        metas.append((off, fk, lk))
+    max_ts = U64.unpack_from(buf, pos)[0]
+    if struct.unpack_from(">I", buf, pos + 8)[0] != checksum:
+        raise ValueError("meta checksum mismatched")
+    return metas, max_ts

@@ -354,3 +354,86 @@ def test_large_blocks_decode_paths(shift):
     for bs in (65536, 16384):
         _, off = roundtrip_check(kv, [0, kv.n], bs, shift=shift)
         assert (np.diff(off) > 4400).mean() > 0.9  # mostly beyond the LDS image
+
+
+def _meta_want(kv: O.KV, seg, block_size):
+    from oracle import pyref
+    ents = kv.entries()
+    return [pyref.encode_block_meta(pyref.sst_block_metas(ents[seg[g]:seg[g + 1]], block_size))
+            for g in range(len(seg) - 1)]
+
+
+def _meta_check(kv: O.KV, seg, block_size):
+    r = batch.encode_sst(to_dev(kv), seg, block_size)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, block_size)
+    assert rc == 0
+    np.testing.assert_array_equal(r["blocks"].cpu().numpy(), ref_blocks)
+    want = _meta_want(kv, seg, block_size)
+    meta = r["meta"].cpu().numpy().tobytes()
+    mo = r["meta_off"].cpu().numpy()
+    assert len(mo) == len(want) + 1 and mo[-1] == len(meta)
+    for g, w in enumerate(want):
+        got = meta[mo[g]:mo[g + 1]]
+        assert got == w, f"segment {g}: {len(got)} B vs {len(w)} B"
+    return r, ref_blocks, ref_off
+
+
+@pytest.mark.parametrize("cfg", ["U", "Z", "M"])
+def test_block_meta_sections_match_sst_builder(cfg):
+    """lsmblk_block_meta_batch == BlockMeta::encode_block_meta of one SsTableBuilder per segment
+    (src/table.rs:29-63, src/table/builder.rs:48-77), byte for byte, incl. the section CRC."""
+    gen = {"U": synth.gen_uniform, "Z": synth.gen_zipf, "M": synth.gen_mixed}[cfg]
+    n = 4000 if cfg == "M" else 20000
+    kv = O.KV(*gen(n, seed=21))
+    bs = 65536 if cfg == "M" else 4096
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, (1 << 20) if cfg == "M" else (128 << 10))
+    r, _, _ = _meta_check(kv, seg, bs)
+    seg_blk = r["seg_blk"].cpu().numpy().view(np.uint32)
+    assert seg_blk[0] == 0 and seg_blk[-1] == r["blk_off"].numel() - 1
+
+
+def test_block_meta_empty_and_one_entry_segments_long_keys():
+    rng = np.random.default_rng(5)
+    base = bytes(rng.integers(0, 256, 90, dtype=np.uint8))
+    keys = sorted({base[:int(rng.integers(20, 90))] + bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+                   for _ in range(1500)})
+    ents = [(k, i, bytes(rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8)))
+            for i, k in enumerate(keys)]
+    kv = O.KV.from_entries(ents)
+    n = kv.n
+    _meta_check(kv, [0, 0, 1, 2, 700, 700, 1400, n, n], 1024)  # empty segments first, inside, last
+    kv1 = O.KV(*synth.gen_uniform(300, seed=8))
+    _meta_check(kv1, np.arange(kv1.n + 1, dtype=np.uint32), 4096)  # one-entry SSTs
+
+
+def test_block_meta_over_framed_data_section_and_errors():
+    """tail = 4: the section computed from a framed data section (block || BE u32 CRC) with the
+    BlockMeta offsets, as a reader holding the SST file would; a block without entries and a
+    bad segment table report errors."""
+    kv = O.KV(*synth.gen_uniform(6000, seed=4))
+    seg = [0, 2500, kv.n]
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, 4096)
+    want = _meta_want(kv, seg, 4096)
+    r = batch.encode_sst(to_dev(kv), seg, 4096)
+    seg_blk = r["seg_blk"]
+    parts, off = [], [0]
+    for i in range(len(ref_off) - 1):
+        blk = ref_blocks[int(ref_off[i]):int(ref_off[i + 1])].tobytes()
+        parts.append(blk + zlib.crc32(blk).to_bytes(4, "big"))
+        off.append(off[-1] + len(parts[-1]))
+    framed = np.frombuffer(b"".join(parts), np.uint8).copy()
+    db, do = dev_blocks(framed, np.array(off, np.uint64), 5)
+    meta, mo = batch.block_meta(db, do, seg_blk, tail=4)
+    meta, mo = meta.cpu().numpy().tobytes(), mo.cpu().numpy()
+    assert [meta[mo[g]:mo[g + 1]] for g in range(len(seg) - 1)] == want
+    # an entry-less block (u16 count 0) is malformed; a segment table not ending at nblk too
+    bad = np.concatenate([ref_blocks, np.zeros(2, np.uint8)])
+    boff = np.concatenate([ref_off, [ref_off[-1] + 2]]).astype(np.uint64)
+    db, do = dev_blocks(bad, boff)
+    nb = len(boff) - 1
+    with pytest.raises(LsmBlkError) as e:
+        batch.block_meta(db, do, np.array([0, nb], np.uint32))
+    assert e.value.status == LSMBLK_E_MALFORMED
+    db, do = dev_blocks(ref_blocks, ref_off)
+    with pytest.raises(LsmBlkError):
+        batch.block_meta(db, do, np.array([0, 1], np.uint32))

@@ -215,3 +215,33 @@ def test_golden_fixtures():
         np.testing.assert_array_equal(off, z["blk_off"])
         np.testing.assert_array_equal(blocks, z["blocks"])
         assert zlib.crc32(blocks.tobytes()) == m["crc32"]
+
+
+def test_block_meta_restatement_week1_day4_day7():
+    """BlockMeta (src/table.rs:29-93) over the reference's own SST tests: week1_day4 (key_%03d,
+    block_size 128: >= 2 blocks) and week1_day7 (key_%010d: <= 34 blocks).  Offsets count
+    every block plus its u32 CRC (table/builder.rs:118-122); keys keep ts 0; the section's
+    CRC covers everything after the u32 count and decode_block_meta verifies it."""
+    import zlib
+    from oracle import pyref
+    for fmt in ("key_%03d", "key_%010d"):
+        ents = [((fmt % i).encode(), 0, ("value_%010d" % i).encode()) for i in range(100)]
+        metas = pyref.sst_block_metas(ents, 128)
+        blocks = pyref.encode_segments(ents, [0, 100], 128)
+        assert len(metas) == len(blocks) == 34
+        off = 0
+        for (o, fk, lk), blk in zip(metas, blocks):
+            es = pyref.block_entries(blk)
+            assert o == off and fk == es[0][0] and lk == es[-1][0]
+            off += len(blk) + 4
+        sec = pyref.encode_block_meta(metas)
+        assert int.from_bytes(sec[:4], "big") == 34
+        assert int.from_bytes(sec[-4:], "big") == zlib.crc32(sec[4:-4])
+        assert pyref.decode_block_meta(sec) == (metas, 0)
+        bad = bytearray(sec)
+        bad[10] ^= 1
+        with pytest.raises(ValueError):
+            pyref.decode_block_meta(bytes(bad))
+    # a one-block SST: first and last keys of the block; an empty meta list is 16 bytes
+    assert pyref.sst_block_metas([(b"k", 5, b"v")], 4096) == [(0, b"k", b"k")]
+    assert len(pyref.encode_block_meta([])) == 16
