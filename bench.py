@@ -212,6 +212,7 @@ def main():
             "cpu_baseline": None,
         }
         result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
+        result["framing_meta"] = framing_meta(out_blocks, out_off, nblk, seg_t, st_enc, dev, stream)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
         if args.pcie:
@@ -254,6 +255,45 @@ def framing_crc32(blocks, blk_off, nblk, E, dev, stream, reps=5):
     return {"kernel": "crc_kernel", "ms": round(ms, 4), "gib_s": round(E / (ms * 1e-3) / GiB, 2),
             "achieved_gbs": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
             "bytes_per_launch": E, "checked_vs_zlib": int(len(idx)) if ok else 0, "ok": bool(ok)}
+
+
+def framing_meta(blocks, blk_off, nblk, seg_t, st_enc, dev, stream, reps=5):
+    """SST framing row: the BlockMeta section of every segment (SST) of the
+    last re-encode (lsmblk_encode_segment_blocks + lsmblk_block_meta_batch: 4 small kernels +
+    crc_kernel over the sections + the CRC stores), HIP events on the launch stream.  Not part
+    of `value`.  Spot check: every sampled section's u32 count equals its block count and its
+    trailing CRC equals zlib.crc32 of the bytes after the count (table.rs:29-63)."""
+    import zlib
+    nseg = seg_t.numel() - 1
+    seg_blk = torch.zeros(nseg + 1, dtype=torch.int32, device=dev)
+    batch.segment_blocks_into(seg_t, nseg, st_enc, seg_blk)
+    cap = 16 * nseg + 64 * nblk
+    meta = batch._aligned_empty(cap, dev)
+    meta_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+    ob = blk_off[:nblk + 1]
+    batch.block_meta_into(blocks, ob, nblk, seg_blk, nseg, meta, cap, meta_off, st)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        batch.block_meta_into(blocks, ob, nblk, seg_blk, nseg, meta, cap, meta_off, st)
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    mo = meta_off.cpu().numpy()
+    sb = seg_blk.cpu().numpy().view(np.uint32)
+    total = int(st[1].item())
+    host = meta[:total].cpu().numpy().tobytes()
+    ok = st[3].item() == 0 and int(mo[-1]) == total
+    for g in np.linspace(0, nseg - 1, 16).astype(np.int64):
+        sec = host[int(mo[g]):int(mo[g + 1])]
+        ok = ok and int.from_bytes(sec[:4], "big") == int(sb[g + 1] - sb[g])
+        ok = ok and int.from_bytes(sec[-4:], "big") == zlib.crc32(sec[4:-4])
+    E = int(blk_off[nblk].item())
+    return {"kernels": "meta_size/scan/write/seg + crc_kernel + crc_put", "ms": round(ms, 4),
+            "meta_bytes": total, "block_bytes_read": E, "sections": nseg,
+            "gib_s_of_blocks": round(E / (ms * 1e-3) / GiB, 2), "checked_sections": 16 if ok else 0,
+            "ok": bool(ok)}
 
 
 def kernel_times(ctx, step, dev, reps=3):
