@@ -2005,41 +2005,96 @@ __device__ __forceinline__ void put_be(uint8_t* d, uint64_t v, uint32_t nbytes) 
   for (uint32_t i = 0; i < nbytes; ++i) d[i] = uint8_t(v >> (8 * (nbytes - 1 - i)));
 }
 
-// One lane per block: its position (tile prefix + in-workgroup scan), its segment (binary
-// search of seg_blk) and the record bytes.
-__global__ __launch_bounds__(256) void meta_write_kernel(MetaArgs a) {
-  if (a.stats[3]) return;
-  const uint64_t b = uint64_t(blockIdx.x) * kMetaTile + threadIdx.x;
-  const uint32_t r = b < a.nblk ? a.rec[b] : 0u;
-  const uint32_t inc = wave_incl_scan32(r);
-  __shared__ uint32_t ws[4];
-  const uint32_t w = threadIdx.x >> 6;
-  if (lane_id() == 63) ws[w] = inc;
-  __syncthreads();
-  if (b >= a.nblk) return;
-  uint64_t pos = a.tile_pre[blockIdx.x] + inc - r;
-  for (uint32_t j = 0; j < w; ++j) pos += ws[j];
-  a.pos[b] = pos;
-  uint32_t lo = 0, hi = a.nseg;  // largest seg with seg_blk[seg] <= b
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a.seg_blk[mid] <= b) lo = mid; else hi = mid;
+// len bytes from global src to dst (LDS or global), any alignment: unaligned 16-B loads and
+// stores (gfx9 unaligned access mode), the last piece overlapping the one before; byte copies
+// under 16 bytes.  The source range must lie inside the block.
+__device__ __forceinline__ void copy_bytes16(uint8_t* dst, const uint8_t* src, uint32_t len) {
+  if (len < 16) {
+    for (uint32_t i = 0; i < len; ++i) dst[i] = src[i];
+    return;
   }
-  const uint32_t seg = lo;
-  const uint64_t first = a.seg_blk[seg];
-  const MetaBlk m = meta_parse(a, b);
-  const uint64_t off = a.blk_off[b] - a.blk_off[first] + (4ull - a.tail) * (b - first);
-  uint8_t* d = a.meta + pos + 16ull * seg + 4;
-  const uint8_t* q = a.blocks + m.base;
-  put_be(d, uint32_t(off), 4);  // offset as u32 (table.rs:44)
+  for (uint32_t i = 0;; i += 16) {
+    const uint32_t o = min(i, len - 16);
+    *reinterpret_cast<u32x4*>(dst + o) = *reinterpret_cast<const u32x4*>(src + o);
+    if (o == len - 16) break;
+  }
+}
+
+// One BlockMeta record at d: u32 offset | u16 flen | first key | u64 0 | u16 llen | last key |
+// u64 0 (table.rs:42-51).
+__device__ __forceinline__ void meta_record(uint8_t* d, const uint8_t* q, const MetaBlk& m, uint32_t off) {
+  put_be(d, off, 4);  // offset as u32 (table.rs:44)
   put_be(d + 4, m.s0, 2);
-  for (uint32_t i = 0; i < m.s0; ++i) d[6 + i] = q[4 + i];
+  copy_bytes16(d + 6, q + 4, m.s0);
   d += 6 + m.s0;
   put_be(d, 0, 8);
   put_be(d + 8, (m.p + m.s) & 0xFFFFu, 2);
-  for (uint32_t i = 0; i < m.p; ++i) d[10 + i] = q[4 + i];
-  for (uint32_t i = 0; i < m.s; ++i) d[10 + m.p + i] = q[m.loff + 4 + i];
+  copy_bytes16(d + 10, q + 4, m.p);
+  copy_bytes16(d + 10 + m.p, q + m.loff + 4, m.s);
   put_be(d + 10 + m.p + m.s, 0, 8);
+}
+
+// One lane per block: its position (tile prefix + in-workgroup scan), its segment (binary
+// search of seg_blk) and the record.  A tile's records (and the section headers/footers
+// between them, rewritten by the later kernels) span one contiguous range: it is composed in
+// LDS and flushed with aligned 16-B stores, byte-masked only at the two ends.  A tile whose
+// range exceeds the image (long keys) writes its records straight to HBM.
+constexpr uint32_t kMetaImg = 24576;
+__global__ __launch_bounds__(256) void meta_write_kernel(MetaArgs a) {
+  if (a.stats[3]) return;
+  __shared__ __attribute__((aligned(16))) uint8_t img[kMetaImg + 16];
+  __shared__ uint32_t ws[4];
+  __shared__ uint64_t ext[2];
+  const uint64_t b = uint64_t(blockIdx.x) * kMetaTile + threadIdx.x;
+  const uint64_t bend = min(a.nblk, uint64_t(blockIdx.x + 1) * kMetaTile);
+  const bool live = b < a.nblk;
+  const uint32_t r = live ? a.rec[b] : 0u;
+  const uint32_t inc = wave_incl_scan32(r);
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane_id() == 63) ws[w] = inc;
+  __syncthreads();
+  uint64_t pos = a.tile_pre[blockIdx.x] + inc - r;
+  for (uint32_t j = 0; j < w; ++j) pos += ws[j];
+  uint32_t seg = 0;
+  MetaBlk m{};
+  uint64_t dst = 0;
+  uint32_t off = 0;
+  if (live) {
+    a.pos[b] = pos;
+    uint32_t lo = 0, hi = a.nseg;  // largest seg with seg_blk[seg] <= b
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.seg_blk[mid] <= b) lo = mid; else hi = mid;
+    }
+    seg = lo;
+    const uint64_t first = a.seg_blk[seg];
+    m = meta_parse(a, b);
+    off = uint32_t(a.blk_off[b] - a.blk_off[first] + (4ull - a.tail) * (b - first));
+    dst = pos + 16ull * seg + 4;
+    if (b == uint64_t(blockIdx.x) * kMetaTile) ext[0] = dst;
+    if (b == bend - 1) ext[1] = dst + r;
+  }
+  __syncthreads();
+  const uint64_t t_lo = ext[0], t_hi = ext[1];
+  uint8_t* gb = a.meta + t_lo;
+  const uint32_t lead = uint32_t(reinterpret_cast<uintptr_t>(gb) & 15);
+  const uint64_t span = lead + (t_hi - t_lo);
+  const uint8_t* q = a.blocks + m.base;
+  if (span > kMetaImg) {
+    if (live) meta_record(a.meta + dst, q, m, off);
+    return;
+  }
+  if (live) meta_record(img + lead + (dst - t_lo), q, m, off);
+  __syncthreads();
+  uint8_t* ga = gb - lead;
+  const uint32_t nc = uint32_t((span + 15) >> 4);
+  for (uint32_t c = threadIdx.x; c < nc; c += 256) {
+    const u32x4 v4 = *reinterpret_cast<const u32x4*>(img + 16 * c);
+    const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
+    const uint32_t lo = c == 0 ? lead : 0u;
+    const uint32_t hi = uint32_t(min<uint64_t>(16, span - 16ull * c));
+    store_chunk(ga + 16 * c, v, lo, hi);
+  }
 }
 
 // One lane per segment: section offsets, u32 num and u64 max_ts.  After an error every offset
