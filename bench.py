@@ -370,9 +370,49 @@ def cpu_baseline(blocks, blk_off, seg, bs, seconds):
                 break
     except OSError:
         pass
-    return {"value": round(len(host_blocks) * reps / dt / GiB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{nb} blocks ({len(host_blocks) / 2**20:.1f} MiB encoded) decode+re-encode x{reps}, "
-                      f"oracle/lsmblk_oracle.c -O3 single thread, {cpu}, host nproc={os.cpu_count()}"}
+    res = {"value": round(len(host_blocks) * reps / dt / GiB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+           "sample": f"{nb} blocks ({len(host_blocks) / 2**20:.1f} MiB encoded) decode+re-encode x{reps}, "
+                     f"oracle/lsmblk_oracle.c -O3 single thread, {cpu}, host nproc={os.cpu_count()}"}
+    res["all_cores"] = cpu_baseline_threads(host_blocks, off, s, bs, max(seconds / 2, 2.0))
+    return res
+
+
+def cpu_baseline_threads(host_blocks, off, s, bs, seconds):
+    """the same sample on T host threads at once, one independent
+    decode + re-encode replica per thread (the reference runs one builder per SST, so SSTs are
+    the unit of host parallelism).  T = the job's CPU share (OMP_NUM_THREADS, else the
+    affinity mask), at most 64.  ctypes releases the GIL inside the C oracle."""
+    import threading
+    from oracle import oracle as O
+    T = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    T = max(1, min(T, 64))
+    counts = [0] * T
+    errs = []
+    start = threading.Barrier(T + 1)
+    stop = [False]
+
+    def work(i):
+        start.wait()
+        while not stop[0]:
+            rc1, kv2 = O.decode_blocks(host_blocks, off)
+            rc2, b2, _ = O.encode_segments(kv2, s, bs)
+            if rc1 or rc2 or len(b2) != len(host_blocks):
+                errs.append((rc1, rc2))
+                return
+            counts[i] += 1
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
+    for t in th:
+        t.start()
+    start.wait()
+    t0 = time.perf_counter()
+    time.sleep(seconds)
+    stop[0] = True
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"value": round(len(host_blocks) * sum(counts) / dt / GiB, 4), "unit": "GiB/s", "cores": T,
+            "ok": not errs, "sample": f"{T} threads x the same {len(off) - 1}-block sample, {sum(counts)} passes"}
 
 
 def pcie_inclusive(blocks, blk_off, E, out_kv, n, K, V, seg_t, seg, bs, out_blocks, out_cap, out_off, blk_cap,
