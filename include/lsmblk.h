@@ -25,6 +25,7 @@
  *                                                           src/table.rs:226-230)
  *       lsmblk_block_meta_batch  the SST BlockMeta section per segment  (src/table.rs:29-63,
  *                                                           src/table/builder.rs:68-77)
+ *       lsmblk_compact_filter_batch  compaction's per-entry keep/drop rules  (src/compact.rs:234-299)
  *     All pointers are DEVICE pointers; calls are asynchronous on `stream` (a hipStream_t
  *     passed as void*; NULL = the default stream).  Thread-safe per distinct context.
  *
@@ -217,6 +218,22 @@ int lsmblk_block_meta_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64
                             uint64_t nblk, uint32_t tail, const uint32_t* seg_blk, uint32_t nseg,
                             uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off, uint64_t* stats,
                             void* stream);
+
+/* Compaction filter (SURVEY.md §8 f, row 2 -- the per-entry rules of compact_generate_sst,
+ * src/compact.rs:234-299) over a MERGED stream `in` (user keys ascending, versions newest
+ * first, as MergeIterator yields them).  Keeps every version newer than `watermark` and, of
+ * each key's versions at or below it, only the newest -- unless bottom_level and that version
+ * is a tombstone (empty value) with no newer version (:244-254), or the key starts with one of
+ * the nprefix prefixes (prefixes[prefix_off[f] .. prefix_off[f+1]), device memory;
+ * CompactionFilter::Prefix, :264-275).  The kept entries are written in order to `out` (any
+ * alignment).  stats: [0] kept entries [1] key bytes [2] value bytes [3] error flags
+ * (CAPACITY: out's entry_cap / key_cap / val_cap too small, stats hold the required sizes,
+ * nothing written).  SST rotation (:278-289) stays with the encode's segment table.
+ * Asynchronous. */
+int lsmblk_compact_filter_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uint64_t watermark,
+                                int bottom_level, const uint8_t* prefixes, const uint32_t* prefix_off,
+                                uint32_t nprefix, const lsmblk_kv_stream* out, uint64_t* stats,
+                                void* stream);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,8 @@
   block_meta     the SST BlockMeta section of every segment (BlockMeta::encode_block_meta,
                  reference src/table.rs:29-63, written by SsTableBuilder::build :68-77)
   encode_sst     encode_kv + the segment -> block table + block_meta in one stream
+  compact_filter compaction's keep/drop rules over a merged stream (reference
+                 src/compact.rs:234-299: watermark, bottom-level tombstones, prefix filters)
 
 Tensors live on a ROCm device (torch is only the allocator / stream provider).  The work
 is done by liblsmblk.so; there is no CPU path here.
@@ -274,3 +276,32 @@ def encode_sst(kv: KVStream, seg_start, block_size: int, stream=None):
     crc = crc32_blocks(blocks, blk_off, stream)
     meta, meta_off = block_meta(blocks, blk_off, seg_blk, stream)
     return dict(blocks=blocks, blk_off=blk_off, seg_blk=seg_blk, crc=crc, meta=meta, meta_off=meta_off)
+
+
+def compact_filter(kv: KVStream, watermark: int, bottom_level: bool, prefixes=(), stream=None) -> KVStream:
+    """compact_generate_sst's per-entry rules (reference src/compact.rs:234-299) over a merged
+    stream (keys ascending, versions newest first) -> the kept entries as a new KVStream."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    pf = b"".join(prefixes)
+    po = np.zeros(len(prefixes) + 1, np.uint32)
+    po[1:] = np.cumsum([len(p) for p in prefixes]) if prefixes else []
+    pfx = torch.frombuffer(bytearray(pf or b"\0"), dtype=torch.uint8).to(dev)
+    pfo = torch.from_numpy(po.view(np.int32)).to(dev)
+    kb = int(kv.key_off[kv.n].item()) & 0xFFFFFFFF if kv.n else 0
+    vb = int(kv.val_off[kv.n].item()) & 0xFFFFFFFF if kv.n else 0
+    n = kv.n
+    out = KVStream(_aligned_empty(kb + 16, dev), torch.zeros(n + 1, dtype=torch.int32, device=dev),
+                   _aligned_empty(vb + 16, dev), torch.zeros(n + 1, dtype=torch.int32, device=dev),
+                   torch.zeros(max(n, 1), dtype=torch.int64, device=dev), 0)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    ci, co = kv._c(), out._c(n, kb + 16, vb + 16)
+    check(lib().lsmblk_compact_filter_batch(_ctx(dev.index), ctypes.byref(ci), watermark, int(bool(bottom_level)),
+                                            pfx.data_ptr(), pfo.data_ptr(), len(prefixes), ctypes.byref(co),
+                                            stats.data_ptr(), _stream_ptr(stream, dev.index)),
+          "lsmblk_compact_filter_batch")
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "compact_filter")
+    out.n = int(stats[0].item())
+    return out

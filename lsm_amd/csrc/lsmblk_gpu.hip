@@ -2143,6 +2143,168 @@ __global__ __launch_bounds__(256) void seg_blocks_kernel(const uint32_t* blk_fir
   seg_blk[g] = lo;
 }
 
+// ---------------------------------------------------------------- compaction filter
+// The per-entry rules of compact_generate_sst (src/compact.rs:234-299) over a merged KV stream
+// (user keys ascending, versions newest first, as MergeIterator yields them).  Walking the
+// loop's state (last_key, first_key_below_watermark) through one key's versions gives a rule
+// that needs only the entry and its predecessor, so every entry is decided independently:
+//   start  = first version of its key (key differs from the previous entry's)
+//   keep   = ts > watermark
+//         || (first version at or below the watermark: start || prev.ts > watermark)
+//            && !(bottom_level && start && value empty)       (:244-254, a tombstone with no
+//                                                               newer version is dropped)
+//            && !any prefix filter matches the key             (:264-275)
+// Every later version at or below the watermark is dropped (:256-260).  The closed form is
+// checked against a line-by-line restatement of the loop (tests/test_oracle.py).
+// Three launches: keep flags + per-tile sums, a one-workgroup tile scan (totals, capacity),
+// and the compaction into the output stream (16-B unaligned copies of keys and values).
+constexpr uint32_t kFiltTile = 256;
+
+struct FiltArgs {
+  const uint8_t* keys;
+  const uint32_t* key_off;
+  const uint8_t* vals;
+  const uint32_t* val_off;
+  const uint64_t* ts;
+  uint64_t n;
+  uint64_t wm;
+  uint32_t bottom;
+  uint32_t npfx;
+  const uint8_t* pfx;
+  const uint32_t* pfx_off;
+  uint8_t* okeys;
+  uint32_t* okey_off;
+  uint8_t* ovals;
+  uint32_t* oval_off;
+  uint64_t* ots;
+  uint64_t entry_cap, key_cap, val_cap;
+  uint32_t* keep;      // n
+  uint64_t* tile_sum;  // 3 per tile: entries, key bytes, value bytes
+  uint64_t* tile_pre;
+  uint64_t* stats;
+};
+
+__device__ __forceinline__ bool filt_keep(const FiltArgs& a, uint64_t i) {
+  const uint64_t t = a.ts[i];
+  if (t > a.wm) return true;
+  const uint32_t k0 = a.key_off[i], k1 = a.key_off[i + 1];
+  bool start = true;
+  if (i > 0) {
+    const uint32_t p0 = a.key_off[i - 1];
+    if (k0 - p0 == k1 - k0) {
+      start = false;
+      for (uint32_t j = 0; j < k1 - k0; ++j)
+        if (a.keys[p0 + j] != a.keys[k0 + j]) {
+          start = true;
+          break;
+        }
+    }
+    if (!start && a.ts[i - 1] <= a.wm) return false;  // a later version below the watermark
+  }
+  if (a.bottom && start && a.val_off[i + 1] == a.val_off[i]) return false;
+  for (uint32_t f = 0; f < a.npfx; ++f) {
+    const uint32_t f0 = a.pfx_off[f], fl = a.pfx_off[f + 1] - f0;
+    if (fl > k1 - k0) continue;
+    bool m = true;
+    for (uint32_t j = 0; j < fl && m; ++j) m = a.pfx[f0 + j] == a.keys[k0 + j];
+    if (m) return false;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void filt_flag_kernel(FiltArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + threadIdx.x;
+  uint32_t c = 0, kb = 0, vb = 0;
+  if (i < a.n) {
+    const bool k = filt_keep(a, i);
+    a.keep[i] = k;
+    if (k) {
+      c = 1;
+      kb = a.key_off[i + 1] - a.key_off[i];
+      vb = a.val_off[i + 1] - a.val_off[i];
+    }
+  }
+  __shared__ uint64_t ws[4][3];
+  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t sc = wave_sum32(c);
+  const uint64_t sk = wave_sum<uint64_t>(kb), sv = wave_sum<uint64_t>(vb);
+  if (lane_id() == 0) ws[w][0] = sc, ws[w][1] = sk, ws[w][2] = sv;
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const uint32_t q = threadIdx.x;
+    a.tile_sum[3 * uint64_t(blockIdx.x) + q] = ws[0][q] + ws[1][q] + ws[2][q] + ws[3][q];
+  }
+}
+
+__global__ __launch_bounds__(1024) void filt_scan_kernel(FiltArgs a) {
+  const uint32_t t = threadIdx.x;
+  const uint64_t ntiles = (a.n + kFiltTile - 1) / kFiltTile;
+  const uint64_t per = (ntiles + 1023) / 1024;
+  const uint64_t lo = min(ntiles, t * per), hi = min(ntiles, lo + per);
+  __shared__ uint64_t wsum[16][3];
+  uint64_t base[3];
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += a.tile_sum[3 * i + q];
+    const uint64_t inc = wave_incl_scan<uint64_t>(s);
+    if (lane_id() == 63) wsum[t >> 6][q] = inc;
+    base[q] = inc - s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    for (uint32_t w = 0; w < (t >> 6); ++w) base[q] += wsum[w][q];
+    uint64_t run = base[q];
+    for (uint64_t i = lo; i < hi; ++i) {
+      a.tile_pre[3 * i + q] = run;
+      run += a.tile_sum[3 * i + q];
+    }
+  }
+  if (t == 1023) {
+    uint64_t tot[3];
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+      tot[q] = 0;
+      for (uint32_t w = 0; w < 16; ++w) tot[q] += wsum[w][q];
+      a.stats[q] = tot[q];
+    }
+    uint32_t err = 0;
+    if (tot[1] > 0xFFFFFFFFull || tot[2] > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+    if (tot[0] > a.entry_cap || tot[1] > a.key_cap || tot[2] > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
+    if (!err) {
+      a.okey_off[tot[0]] = uint32_t(tot[1]);
+      a.oval_off[tot[0]] = uint32_t(tot[2]);
+    }
+    or_err(a.stats, err);
+  }
+}
+
+__global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
+  if (a.stats[3]) return;
+  const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + threadIdx.x;
+  const bool live = i < a.n;
+  const bool k = live && a.keep[i];
+  const uint32_t kl = k ? a.key_off[i + 1] - a.key_off[i] : 0u;
+  const uint32_t vl = k ? a.val_off[i + 1] - a.val_off[i] : 0u;
+  const uint32_t ic = wave_incl_scan32(k ? 1u : 0u);
+  const uint64_t ik = wave_incl_scan<uint64_t>(kl), iv = wave_incl_scan<uint64_t>(vl);
+  __shared__ uint64_t ws[4][3];
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane_id() == 63) ws[w][0] = ic, ws[w][1] = ik, ws[w][2] = iv;
+  __syncthreads();
+  if (!k) return;
+  uint64_t j = a.tile_pre[3 * uint64_t(blockIdx.x)] + ic - 1;
+  uint64_t ko = a.tile_pre[3 * uint64_t(blockIdx.x) + 1] + ik - kl;
+  uint64_t vo = a.tile_pre[3 * uint64_t(blockIdx.x) + 2] + iv - vl;
+  for (uint32_t q = 0; q < w; ++q) j += ws[q][0], ko += ws[q][1], vo += ws[q][2];
+  a.okey_off[j] = uint32_t(ko);
+  a.oval_off[j] = uint32_t(vo);
+  a.ots[j] = a.ts[i];
+  copy_bytes16(a.okeys + ko, a.keys + a.key_off[i], kl);
+  copy_bytes16(a.ovals + vo, a.vals + a.val_off[i], vl);
+}
+
 // ================================================================ host side
 struct lsmblk_ctx {
   int device = 0;
@@ -2177,6 +2339,11 @@ struct lsmblk_ctx {
   uint32_t* meta_crc = nullptr;     // nseg
   uint64_t meta_seg_cap = 0;
   uint64_t* meta_cstats = nullptr;  // crc_kernel stats of the section CRC pass
+  // compaction filter (lsmblk_compact_filter_batch)
+  uint32_t* filt_keep = nullptr;    // n
+  uint64_t filt_cap = 0;
+  uint64_t* filt_tile = nullptr;    // 6 per tile: sums, prefixes
+  uint64_t filt_tile_cap = 0;
 };
 
 namespace {
@@ -2301,6 +2468,8 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->meta_tile);
   (void)hipFree(c->meta_crc);
   (void)hipFree(c->meta_cstats);
+  (void)hipFree(c->filt_keep);
+  (void)hipFree(c->filt_tile);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2567,6 +2736,50 @@ int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t
   if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if ((rc = launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st))) return rc;
   hipLaunchKernelGGL(meta_crc_put_kernel, dim3(sg), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint64_t watermark, int bottom_level,
+                                const uint8_t* prefixes, const uint32_t* prefix_off, uint32_t nprefix,
+                                const lsmblk_kv_stream* out, uint64_t* stats, void* stream) {
+  if (!c || !in || !out || !stats || !in->key_off || !in->val_off || !out->key_off || !out->val_off) return LSMBLK_E_INVAL;
+  if (nprefix && (!prefixes || !prefix_off)) return LSMBLK_E_INVAL;
+  if (in->n >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  const uint64_t n = in->n, ntiles = (n + kFiltTile - 1) / kFiltTile;
+  int rc;
+  if ((rc = grow(&c->filt_keep, &c->filt_cap, n + 1, 1))) return rc;
+  if ((rc = grow(&c->filt_tile, &c->filt_tile_cap, ntiles + 1, 6))) return rc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  FiltArgs a;
+  a.keys = in->keys;
+  a.key_off = in->key_off;
+  a.vals = in->vals;
+  a.val_off = in->val_off;
+  a.ts = in->ts;
+  a.n = n;
+  a.wm = watermark;
+  a.bottom = bottom_level ? 1u : 0u;
+  a.npfx = nprefix;
+  a.pfx = prefixes;
+  a.pfx_off = prefix_off;
+  a.okeys = out->keys;
+  a.okey_off = out->key_off;
+  a.ovals = out->vals;
+  a.oval_off = out->val_off;
+  a.ots = out->ts;
+  a.entry_cap = out->entry_cap;
+  a.key_cap = out->key_cap;
+  a.val_cap = out->val_cap;
+  a.keep = c->filt_keep;
+  a.tile_sum = c->filt_tile;
+  a.tile_pre = c->filt_tile + 3 * c->filt_tile_cap;
+  a.stats = stats;
+  if (ntiles) hipLaunchKernelGGL(filt_flag_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(filt_scan_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (ntiles) hipLaunchKernelGGL(filt_write_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 

@@ -164,3 +164,49 @@ def decode_block_meta(buf: bytes):
     if struct.unpack_from(">I", buf, pos + 8)[0] != checksum:
         raise ValueError("meta checksum mismatched")
     return metas, max_ts
+
+
+def compact_filter_loop(entries, watermark, bottom_level, prefixes=()):
+    """compact_generate_sst (src/compact.rs:223-311), the per-entry loop restated line by line
+    over a merged stream [(key, ts, value)] (keys ascending, versions newest first); returns
+    the entries handed to SsTableBuilder::add (:292).  SST rotation (:278-289) is left out:
+    it does not change which entries are kept."""
+    out, last_key, first_key_below_watermark = [], b"", False
+    have_last = False
+    for key, ts, value in entries:
+        same_as_last_key = have_last and key == last_key  # :239
+        if not same_as_last_key:
+            first_key_below_watermark = True  # :240-242
+        if bottom_level and not same_as_last_key and ts <= watermark and len(value) == 0:  # :244-254
+            last_key, have_last = key, True
+            first_key_below_watermark = False
+            continue
+        if ts <= watermark:  # :256-276
+            if same_as_last_key and not first_key_below_watermark:
+                continue
+            first_key_below_watermark = False
+            if any(key.startswith(p) for p in prefixes):
+                continue
+        out.append((key, ts, value))  # :292
+        if not same_as_last_key:
+            last_key, have_last = key, True
+    return out
+
+
+def compact_filter_rule(entries, watermark, bottom_level, prefixes=()):
+    """The closed form the GPU evaluates per entry (lsmblk_gpu.hip, filt_keep): an entry needs
+    only itself and its predecessor."""
+    out = []
+    for i, (key, ts, value) in enumerate(entries):
+        if ts > watermark:
+            out.append((key, ts, value))
+            continue
+        start = i == 0 or entries[i - 1][0] != key
+        if not start and entries[i - 1][1] <= watermark:
+            continue
+        if bottom_level and start and len(value) == 0:
+            continue
+        if any(key.startswith(p) for p in prefixes):
+            continue
+        out.append((key, ts, value))
+    return out

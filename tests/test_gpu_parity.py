@@ -437,3 +437,25 @@ def test_block_meta_over_framed_data_section_and_errors():
     db, do = dev_blocks(ref_blocks, ref_off)
     with pytest.raises(LsmBlkError):
         batch.block_meta(db, do, np.array([0, 1], np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_compact_filter_matches_reference_loop(seed):
+    """lsmblk_compact_filter_batch == compact_generate_sst's keep/drop loop (src/compact.rs:234-299,
+    restated in oracle/pyref.py) on merged streams: watermarks, bottom-level tombstones, prefix
+    filters, long and empty values, unaligned arenas."""
+    from oracle import pyref
+    rng = np.random.default_rng(100 + seed)
+    ents = []
+    for k in range(3000):
+        key = (b"ab" if rng.random() < 0.2 else b"key-") + b"%08d" % k + (b"x" * int(rng.integers(0, 40)))
+        for t in sorted(rng.choice(1000, size=int(rng.integers(1, 7)), replace=False), reverse=True):
+            v = b"" if rng.random() < 0.25 else bytes(rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8))
+            ents.append((key, int(t), v))
+    kv = to_dev(O.KV.from_entries(ents))
+    for wm, bottom, pf in ((0, False, ()), (500, True, ()), (500, False, (b"ab",)), (10**6, True, (b"ab", b"key-0000"))):
+        got = batch.compact_filter(kv, wm, bottom, pf)
+        want = O.KV.from_entries(pyref.compact_filter_loop(ents, wm, bottom, pf))
+        assert_kv_equal(got, want)
+    empty = batch.compact_filter(to_dev(O.KV.from_entries([])), 5, True)
+    assert empty.n == 0

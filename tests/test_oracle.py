@@ -245,3 +245,30 @@ def test_block_meta_restatement_week1_day4_day7():
     # a one-block SST: first and last keys of the block; an empty meta list is 16 bytes
     assert pyref.sst_block_metas([(b"k", 5, b"v")], 4096) == [(0, b"k", b"k")]
     assert len(pyref.encode_block_meta([])) == 16
+
+
+def _merged_stream(rng, nkeys, maxver, tomb=0.25, pfx_rate=0.2):
+    """Keys ascending, versions newest first (MergeIterator order), tombstones = empty values."""
+    ents = []
+    for k in range(nkeys):
+        key = (b"ab" if rng.random() < pfx_rate else b"k") + b"%06d" % k
+        for t in sorted(rng.choice(1000, size=int(rng.integers(1, maxver + 1)), replace=False), reverse=True):
+            v = b"" if rng.random() < tomb else bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8))
+            ents.append((key, int(t), v))
+    return ents
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_compaction_filter_closed_form_equals_reference_loop(seed):
+    """The per-entry rule the GPU evaluates == compact_generate_sst's loop restated line by line
+    (src/compact.rs:234-299), over watermarks below, inside and above the ts range, bottom or
+    not, with and without prefix filters."""
+    rng = np.random.default_rng(seed)
+    ents = _merged_stream(rng, 400, 6)
+    for wm in (0, 250, 500, 999, 5000):
+        for bottom in (False, True):
+            for pf in ((), (b"ab",), (b"ab", b"k0001")):
+                assert pyref.compact_filter_rule(ents, wm, bottom, pf) == pyref.compact_filter_loop(ents, wm, bottom, pf)
+    # watermark above every ts: one version per key survives, bottom tombstones vanish
+    kept = pyref.compact_filter_loop(ents, 10**6, True)
+    assert len({k for k, _, _ in kept}) == len(kept) and all(v for _, _, v in kept)
