@@ -213,6 +213,7 @@ def main():
         }
         result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
         result["framing_meta"] = framing_meta(out_blocks, out_off, nblk, seg_t, st_enc, dev, stream)
+        result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
         if args.pcie:
@@ -294,6 +295,43 @@ def framing_meta(blocks, blk_off, nblk, seg_t, st_enc, dev, stream, reps=5):
             "meta_bytes": total, "block_bytes_read": E, "sections": nseg,
             "gib_s_of_blocks": round(E / (ms * 1e-3) / GiB, 2), "checked_sections": 16 if ok else 0,
             "ok": bool(ok)}
+
+
+def compaction_filter(kv, n, K, V, dev, stream, reps=5):
+    """Compaction row (merge rules): lsmblk_compact_filter_batch over the
+    decoded stream (unique keys; watermark 2^39 puts about half the 40-bit ts below it; bottom
+    level; one prefix filter matching nothing).  Every entry is kept, so a launch reads and
+    writes the whole stream: algorithmic bytes 2 D (+ 4 B keep flag per entry).  Not part of
+    `value`."""
+    import ctypes
+    from lsm_amd._lib import check as _check, lib as _lib
+    out = batch.KVStream(batch._aligned_empty(K + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
+                         batch._aligned_empty(V + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
+                         torch.empty(n, dtype=torch.int64, device=dev), 0)
+    pfx = torch.tensor([0xFF, 0xFF, 0xFF], dtype=torch.uint8, device=dev)
+    pfo = torch.tensor([0, 3], dtype=torch.int32, device=dev)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+    ci, co = kv._c(), out._c(n, K + 16, V + 16)
+    ctx = batch._ctx(dev.index)
+
+    def run():
+        _check(_lib().lsmblk_compact_filter_batch(ctx, ctypes.byref(ci), 1 << 39, 1, pfx.data_ptr(), pfo.data_ptr(), 1,
+                                                  ctypes.byref(co), st.data_ptr(), stream.cuda_stream))
+    run()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        run()
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    D = K + V + 16 * n
+    s = st.cpu().tolist()
+    ok = s[3] == 0 and s[0] == n and torch.equal(out.ts[:n], kv.ts[:n]) and torch.equal(out.vals[:V], kv.vals[:V])
+    gbs = (2 * D + 4 * n) / (ms * 1e-3) / 1e9
+    return {"kernels": "filt_flag + filt_scan + filt_write", "ms": round(ms, 4), "entries": n, "kept": int(s[0]),
+            "achieved_gbs": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "bytes_per_launch": 2 * D + 4 * n, "ok": bool(ok)}
 
 
 def kernel_times(ctx, step, dev, reps=3):

@@ -2191,13 +2191,16 @@ __device__ __forceinline__ bool filt_keep(const FiltArgs& a, uint64_t i) {
   bool start = true;
   if (i > 0) {
     const uint32_t p0 = a.key_off[i - 1];
-    if (k0 - p0 == k1 - k0) {
+    const uint32_t kl = k1 - k0;
+    if (k0 - p0 == kl) {
       start = false;
-      for (uint32_t j = 0; j < k1 - k0; ++j)
-        if (a.keys[p0 + j] != a.keys[k0 + j]) {
-          start = true;
-          break;
-        }
+      uint32_t j = 0;
+      for (; j + 16 <= kl && !start; j += 16) {  // unaligned 16-B compares, then bytes
+        const u32x4 x = *reinterpret_cast<const u32x4*>(a.keys + p0 + j);
+        const u32x4 y = *reinterpret_cast<const u32x4*>(a.keys + k0 + j);
+        start = x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+      }
+      for (; j < kl && !start; ++j) start = a.keys[p0 + j] != a.keys[k0 + j];
     }
     if (!start && a.ts[i - 1] <= a.wm) return false;  // a later version below the watermark
   }
@@ -2280,6 +2283,22 @@ __global__ __launch_bounds__(1024) void filt_scan_kernel(FiltArgs a) {
   }
 }
 
+// Copy len bytes src -> dst by the whole wave (wave-uniform arguments): lane l moves 16-B
+// pieces l, l + 64, ... (unaligned loads/stores, 1 KiB of contiguous bytes per instruction);
+// the lane holding a final piece under 16 bytes copies it bytewise.
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint64_t len) {
+  for (uint64_t o = 16ull * lane_id(); o < len; o += 1024) {
+    if (o + 16 <= len) {
+      *reinterpret_cast<u32x4*>(dst + o) = *reinterpret_cast<const u32x4*>(src + o);
+    } else {
+      for (uint64_t x = o; x < len; ++x) dst[x] = src[x];
+    }
+  }
+}
+
+// Output offsets and ts per kept entry; key and value bytes by runs: consecutive kept entries
+// are one contiguous range in the input arenas and in the output, so each wave copies its
+// runs whole (one run per wave when nothing in it is dropped).
 __global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
   if (a.stats[3]) return;
   const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + threadIdx.x;
@@ -2293,16 +2312,28 @@ __global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
   const uint32_t w = threadIdx.x >> 6;
   if (lane_id() == 63) ws[w][0] = ic, ws[w][1] = ik, ws[w][2] = iv;
   __syncthreads();
-  if (!k) return;
   uint64_t j = a.tile_pre[3 * uint64_t(blockIdx.x)] + ic - 1;
   uint64_t ko = a.tile_pre[3 * uint64_t(blockIdx.x) + 1] + ik - kl;
   uint64_t vo = a.tile_pre[3 * uint64_t(blockIdx.x) + 2] + iv - vl;
   for (uint32_t q = 0; q < w; ++q) j += ws[q][0], ko += ws[q][1], vo += ws[q][2];
-  a.okey_off[j] = uint32_t(ko);
-  a.oval_off[j] = uint32_t(vo);
-  a.ots[j] = a.ts[i];
-  copy_bytes16(a.okeys + ko, a.keys + a.key_off[i], kl);
-  copy_bytes16(a.ovals + vo, a.vals + a.val_off[i], vl);
+  uint32_t ki = 0, vi = 0;
+  if (k) {
+    ki = a.key_off[i];
+    vi = a.val_off[i];
+    a.okey_off[j] = uint32_t(ko);
+    a.oval_off[j] = uint32_t(vo);
+    a.ots[j] = a.ts[i];
+  }
+  for (uint64_t mask = __ballot(k); mask;) {
+    const uint32_t s = uint32_t(__builtin_ctzll(mask));
+    const uint64_t rest = ~(mask >> s);
+    const uint32_t e = rest ? s + uint32_t(__builtin_ctzll(rest)) : 64u;  // run = lanes [s, e)
+    const uint32_t ks = __builtin_amdgcn_readlane(ki, s), ke = __builtin_amdgcn_readlane(ki + kl, e - 1);
+    const uint32_t vs = __builtin_amdgcn_readlane(vi, s), ve = __builtin_amdgcn_readlane(vi + vl, e - 1);
+    wave_copy(a.okeys + lane64(ko, s), a.keys + ks, ke - ks);
+    wave_copy(a.ovals + lane64(vo, s), a.vals + vs, ve - vs);
+    mask = e >= 64 ? 0ull : mask & (~0ull << e);
+  }
 }
 
 // ================================================================ host side
