@@ -2239,39 +2239,38 @@ __global__ __launch_bounds__(256) void filt_flag_kernel(FiltArgs a) {
   }
 }
 
+// Rounds of 1024 consecutive tiles (coalesced loads), each a workgroup scan plus the carry.
 __global__ __launch_bounds__(1024) void filt_scan_kernel(FiltArgs a) {
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, w = t >> 6;
   const uint64_t ntiles = (a.n + kFiltTile - 1) / kFiltTile;
-  const uint64_t per = (ntiles + 1023) / 1024;
-  const uint64_t lo = min(ntiles, t * per), hi = min(ntiles, lo + per);
   __shared__ uint64_t wsum[16][3];
-  uint64_t base[3];
-#pragma unroll
-  for (uint32_t q = 0; q < 3; ++q) {
-    uint64_t s = 0;
-    for (uint64_t i = lo; i < hi; ++i) s += a.tile_sum[3 * i + q];
-    const uint64_t inc = wave_incl_scan<uint64_t>(s);
-    if (lane_id() == 63) wsum[t >> 6][q] = inc;
-    base[q] = inc - s;
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t q = 0; q < 3; ++q) {
-    for (uint32_t w = 0; w < (t >> 6); ++w) base[q] += wsum[w][q];
-    uint64_t run = base[q];
-    for (uint64_t i = lo; i < hi; ++i) {
-      a.tile_pre[3 * i + q] = run;
-      run += a.tile_sum[3 * i + q];
-    }
-  }
-  if (t == 1023) {
-    uint64_t tot[3];
+  uint64_t carry[3] = {0, 0, 0};
+  for (uint64_t r = 0; r < ntiles; r += 1024) {
+    const uint64_t i = r + t;
+    uint64_t v[3], inc[3];
 #pragma unroll
     for (uint32_t q = 0; q < 3; ++q) {
-      tot[q] = 0;
-      for (uint32_t w = 0; w < 16; ++w) tot[q] += wsum[w][q];
-      a.stats[q] = tot[q];
+      v[q] = i < ntiles ? a.tile_sum[3 * i + q] : 0ull;
+      inc[q] = wave_incl_scan<uint64_t>(v[q]);
+      if (lane_id() == 63) wsum[w][q] = inc[q];
     }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+      uint64_t base = carry[q], tot = carry[q];
+      for (uint32_t x = 0; x < 16; ++x) {
+        if (x < w) base += wsum[x][q];
+        tot += wsum[x][q];
+      }
+      if (i < ntiles) a.tile_pre[3 * i + q] = base + inc[q] - v[q];
+      carry[q] = tot;
+    }
+    __syncthreads();
+  }
+  if (t == 1023) {
+    const uint64_t tot[3] = {carry[0], carry[1], carry[2]};
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) a.stats[q] = tot[q];
     uint32_t err = 0;
     if (tot[1] > 0xFFFFFFFFull || tot[2] > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
     if (tot[0] > a.entry_cap || tot[1] > a.key_cap || tot[2] > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
