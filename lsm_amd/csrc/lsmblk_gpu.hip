@@ -2158,7 +2158,7 @@ __global__ __launch_bounds__(256) void seg_blocks_kernel(const uint32_t* blk_fir
 // checked against a line-by-line restatement of the loop (tests/test_oracle.py).
 // Three launches: keep flags + per-tile sums, a one-workgroup tile scan (totals, capacity),
 // and the compaction into the output stream (16-B unaligned copies of keys and values).
-constexpr uint32_t kFiltTile = 256;
+constexpr uint32_t kFiltTile = 1024;  // entries per workgroup (4 rounds of 256 lanes)
 
 struct FiltArgs {
   const uint8_t* keys;
@@ -2216,15 +2216,19 @@ __device__ __forceinline__ bool filt_keep(const FiltArgs& a, uint64_t i) {
 }
 
 __global__ __launch_bounds__(256) void filt_flag_kernel(FiltArgs a) {
-  const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + threadIdx.x;
-  uint32_t c = 0, kb = 0, vb = 0;
-  if (i < a.n) {
-    const bool k = filt_keep(a, i);
-    a.keep[i] = k;
-    if (k) {
-      c = 1;
-      kb = a.key_off[i + 1] - a.key_off[i];
-      vb = a.val_off[i + 1] - a.val_off[i];
+  uint32_t c = 0;
+  uint64_t kb = 0, vb = 0;
+#pragma unroll
+  for (uint32_t sub = 0; sub < kFiltTile / 256; ++sub) {
+    const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + sub * 256 + threadIdx.x;
+    if (i < a.n) {
+      const bool k = filt_keep(a, i);
+      a.keep[i] = k;
+      if (k) {
+        c += 1;
+        kb += a.key_off[i + 1] - a.key_off[i];
+        vb += a.val_off[i + 1] - a.val_off[i];
+      }
     }
   }
   __shared__ uint64_t ws[4][3];
@@ -2300,38 +2304,42 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
 // runs whole (one run per wave when nothing in it is dropped).
 __global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
   if (a.stats[3]) return;
-  const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + threadIdx.x;
-  const bool live = i < a.n;
-  const bool k = live && a.keep[i];
-  const uint32_t kl = k ? a.key_off[i + 1] - a.key_off[i] : 0u;
-  const uint32_t vl = k ? a.val_off[i + 1] - a.val_off[i] : 0u;
-  const uint32_t ic = wave_incl_scan32(k ? 1u : 0u);
-  const uint64_t ik = wave_incl_scan<uint64_t>(kl), iv = wave_incl_scan<uint64_t>(vl);
   __shared__ uint64_t ws[4][3];
   const uint32_t w = threadIdx.x >> 6;
-  if (lane_id() == 63) ws[w][0] = ic, ws[w][1] = ik, ws[w][2] = iv;
-  __syncthreads();
-  uint64_t j = a.tile_pre[3 * uint64_t(blockIdx.x)] + ic - 1;
-  uint64_t ko = a.tile_pre[3 * uint64_t(blockIdx.x) + 1] + ik - kl;
-  uint64_t vo = a.tile_pre[3 * uint64_t(blockIdx.x) + 2] + iv - vl;
-  for (uint32_t q = 0; q < w; ++q) j += ws[q][0], ko += ws[q][1], vo += ws[q][2];
-  uint32_t ki = 0, vi = 0;
-  if (k) {
-    ki = a.key_off[i];
-    vi = a.val_off[i];
-    a.okey_off[j] = uint32_t(ko);
-    a.oval_off[j] = uint32_t(vo);
-    a.ots[j] = a.ts[i];
-  }
-  for (uint64_t mask = __ballot(k); mask;) {
-    const uint32_t s = uint32_t(__builtin_ctzll(mask));
-    const uint64_t rest = ~(mask >> s);
-    const uint32_t e = rest ? s + uint32_t(__builtin_ctzll(rest)) : 64u;  // run = lanes [s, e)
-    const uint32_t ks = __builtin_amdgcn_readlane(ki, s), ke = __builtin_amdgcn_readlane(ki + kl, e - 1);
-    const uint32_t vs = __builtin_amdgcn_readlane(vi, s), ve = __builtin_amdgcn_readlane(vi + vl, e - 1);
-    wave_copy(a.okeys + lane64(ko, s), a.keys + ks, ke - ks);
-    wave_copy(a.ovals + lane64(vo, s), a.vals + vs, ve - vs);
-    mask = e >= 64 ? 0ull : mask & (~0ull << e);
+  uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)], a.tile_pre[3 * uint64_t(blockIdx.x) + 1],
+                       a.tile_pre[3 * uint64_t(blockIdx.x) + 2]};
+  for (uint32_t sub = 0; sub < kFiltTile / 256; ++sub) {  // 256 entries per round, running carry
+    const uint64_t i = uint64_t(blockIdx.x) * kFiltTile + sub * 256 + threadIdx.x;
+    const bool k = i < a.n && a.keep[i];
+    const uint32_t kl = k ? a.key_off[i + 1] - a.key_off[i] : 0u;
+    const uint32_t vl = k ? a.val_off[i + 1] - a.val_off[i] : 0u;
+    const uint32_t ic = wave_incl_scan32(k ? 1u : 0u);
+    const uint64_t ik = wave_incl_scan<uint64_t>(kl), iv = wave_incl_scan<uint64_t>(vl);
+    if (lane_id() == 63) ws[w][0] = ic, ws[w][1] = ik, ws[w][2] = iv;
+    __syncthreads();
+    uint64_t j = carry[0] + ic - 1, ko = carry[1] + ik - kl, vo = carry[2] + iv - vl;
+    for (uint32_t q = 0; q < w; ++q) j += ws[q][0], ko += ws[q][1], vo += ws[q][2];
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) carry[q] += ws[0][q] + ws[1][q] + ws[2][q] + ws[3][q];
+    __syncthreads();  // ws is rewritten by the next round
+    uint32_t ki = 0, vi = 0;
+    if (k) {
+      ki = a.key_off[i];
+      vi = a.val_off[i];
+      a.okey_off[j] = uint32_t(ko);
+      a.oval_off[j] = uint32_t(vo);
+      a.ots[j] = a.ts[i];
+    }
+    for (uint64_t mask = __ballot(k); mask;) {
+      const uint32_t s = uint32_t(__builtin_ctzll(mask));
+      const uint64_t rest = ~(mask >> s);
+      const uint32_t e = rest ? s + uint32_t(__builtin_ctzll(rest)) : 64u;  // run = lanes [s, e)
+      const uint32_t ks = __builtin_amdgcn_readlane(ki, s), ke = __builtin_amdgcn_readlane(ki + kl, e - 1);
+      const uint32_t vs = __builtin_amdgcn_readlane(vi, s), ve = __builtin_amdgcn_readlane(vi + vl, e - 1);
+      wave_copy(a.okeys + lane64(ko, s), a.keys + ks, ke - ks);
+      wave_copy(a.ovals + lane64(vo, s), a.vals + vs, ve - vs);
+      mask = e >= 64 ? 0ull : mask & (~0ull << e);
+    }
   }
 }
 
