@@ -459,3 +459,20 @@ def test_compact_filter_matches_reference_loop(seed):
         assert_kv_equal(got, want)
     empty = batch.compact_filter(to_dev(O.KV.from_entries([])), 5, True)
     assert empty.n == 0
+
+
+def test_compact_filter_many_tiles_against_loop():
+    """~450 K entries (hundreds of 1024-entry tiles, many runs per wave): the GPU filter vs the
+    restated loop, watermark mid-range, bottom level, one prefix filter."""
+    from oracle import pyref
+    rng = np.random.default_rng(77)
+    base = O.KV(*synth.gen_uniform(200000, seed=31))
+    reps = rng.integers(1, 4, base.n)
+    ents = []
+    for i in range(base.n):
+        k = bytes(base.keys[16 * i:16 * i + 16])
+        for t in sorted(rng.choice(1 << 20, size=int(reps[i]), replace=False), reverse=True):
+            ents.append((k, int(t), b"" if rng.random() < 0.2 else bytes(8 + (t % 90))))
+    pf = (ents[5][0][:1],)
+    got = batch.compact_filter(to_dev(O.KV.from_entries(ents)), 1 << 19, True, pf)
+    assert_kv_equal(got, O.KV.from_entries(pyref.compact_filter_loop(ents, 1 << 19, True, pf)))
