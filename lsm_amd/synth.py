@@ -78,6 +78,39 @@ def gen_mixed(n, seed=44, vmin=8, vmax=4096):
     return keys, _offsets(np.full(n, 16, np.uint64)), vals, _offsets(vl), _ts(rng, n)
 
 
+def gen_runs(n_keys, nrun=8, overwrite=0.10, tombstone=0.02, seed=45, value_len=100, versions=1):
+    """Compaction-shaped input (SURVEY.md section 8(d) config 5 at one-GPU scale): `nrun` sorted
+    runs (L0 SSTs, run 0 the newest) over one key space with overlapping ranges.  Every key has
+    a home run; a fraction `overwrite` also appears in a second run.  A run holds `versions`
+    versions per key it contains (newest first, as SsTableBuilder receives them); ts are larger
+    in newer runs; `tombstone` of the values are empty (deletes).  Returns (keys, key_off, vals,
+    val_off, ts, run_start) with the runs concatenated in priority order."""
+    rng = np.random.default_rng(seed)
+    base = _sorted_keys16(rng, n_keys).reshape(n_keys, 16)
+    home = rng.integers(0, nrun, n_keys)
+    extra = rng.random(n_keys) < overwrite
+    second = (home + rng.integers(1, max(nrun, 2), n_keys)) % max(nrun, 1)
+    idx, run = [np.arange(n_keys)], [home]
+    if nrun > 1 and extra.any():
+        idx.append(np.flatnonzero(extra))
+        run.append(second[extra])
+    idx, run = np.concatenate(idx), np.concatenate(run)
+    order = np.lexsort((idx, run))            # by run, then key
+    idx, run = idx[order], run[order]
+    # ts: run r's versions lie in band (nrun - r); inside a key, versions newest first
+    ts = ((np.uint64(nrun) - run.astype(np.uint64)) << np.uint64(32)) + \
+        (rng.integers(0, 1 << 24, len(idx), dtype=np.uint64) << np.uint64(4))
+    if versions > 1:
+        idx, run, ts = np.repeat(idx, versions), np.repeat(run, versions), np.repeat(ts, versions)
+        ts += np.tile(np.arange(versions, dtype=np.uint64)[::-1], len(ts) // versions)
+    n = len(idx)
+    keys = base[idx].reshape(-1)
+    vlen = np.where(rng.random(n) < tombstone, 0, value_len).astype(np.uint64)
+    vals = _random_bytes(rng, int(vlen.sum()))
+    run_start = np.searchsorted(run, np.arange(nrun + 1)).astype(np.uint32)
+    return keys, _offsets(np.full(n, 16, np.uint64)), vals, _offsets(vlen), ts, run_start
+
+
 GENERATORS = {"U": gen_uniform, "Z": gen_zipf, "M": gen_mixed}
 BLOCK_SIZE = {"U": 4096, "Z": 4096, "M": 65536}
 

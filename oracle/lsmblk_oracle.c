@@ -346,6 +346,163 @@ int orc_segment_like_compaction(const orc_kv* kv, size_t block_size, uint64_t ta
   return g + 1 <= seg_cap ? ORC_OK : ORC_E_CAPACITY;
 }
 
+/* ------------------------------------------------------------------ merge */
+/* MergeIterator (src/iterators/merge_iterator.rs:59-184) over nrun sorted runs of one KV stream,
+ * run r = entries [run_start[r], run_start[r+1]), run 0 the highest priority.  The BinaryHeap of
+ * HeapWrapper(idx, iter) orders by (user key, idx) reversed (:21-33, key.rs:63-81 ignores ts), so
+ * it is kept here as a binary min-heap on (head key, run index). */
+typedef struct { const orc_kv* kv; uint64_t* pos; const uint32_t* end; } merge_ctx;
+
+static int head_cmp(const merge_ctx* m, uint32_t a, uint32_t b) {
+  const orc_kv* kv = m->kv;
+  uint64_t ia = m->pos[a], ib = m->pos[b];
+  int c = key_cmp(kv->keys + kv->key_off[ia], kv->key_off[ia + 1] - kv->key_off[ia],
+                  kv->keys + kv->key_off[ib], kv->key_off[ib + 1] - kv->key_off[ib]);
+  if (c) return c;
+  return a < b ? -1 : (a > b ? 1 : 0);
+}
+static void sift_down(const merge_ctx* m, uint32_t* h, uint32_t n, uint32_t i) {
+  for (;;) {
+    uint32_t l = 2 * i + 1, r = l + 1, s = i;
+    if (l < n && head_cmp(m, h[l], h[s]) < 0) s = l;
+    if (r < n && head_cmp(m, h[r], h[s]) < 0) s = r;
+    if (s == i) return;
+    uint32_t t = h[i]; h[i] = h[s]; h[s] = t; i = s;
+  }
+}
+static void sift_up(const merge_ctx* m, uint32_t* h, uint32_t i) {
+  while (i) {
+    uint32_t p = (i - 1) / 2;
+    if (head_cmp(m, h[i], h[p]) >= 0) return;
+    uint32_t t = h[i]; h[i] = h[p]; h[p] = t; i = p;
+  }
+}
+static int same_key(const orc_kv* kv, uint64_t a, uint64_t b) {
+  uint32_t al = kv->key_off[a + 1] - kv->key_off[a], bl = kv->key_off[b + 1] - kv->key_off[b];
+  return al == bl && memcmp(kv->keys + kv->key_off[a], kv->keys + kv->key_off[b], al) == 0;
+}
+
+int orc_merge_runs(const orc_kv* in, const uint32_t* run_start, uint32_t nrun, uint32_t* src,
+                   uint64_t src_cap, uint64_t* n_out) {
+  uint64_t* pos = (uint64_t*)malloc((nrun + 1) * sizeof(uint64_t));
+  uint32_t* heap = (uint32_t*)malloc((nrun + 1) * sizeof(uint32_t));
+  merge_ctx m = {in, pos, run_start + 1};
+  uint32_t hn = 0, cur = 0;
+  int have = 0;
+  uint64_t n = 0;
+  for (uint32_t r = 0; r < nrun; ++r) {          /* create, :93-100: push the valid iterators */
+    pos[r] = run_start[r];
+    if (run_start[r] < run_start[r + 1]) { heap[hn] = r; sift_up(&m, heap, hn); ++hn; }
+  }
+  if (hn) { cur = heap[0]; heap[0] = heap[--hn]; sift_down(&m, heap, hn, 0); have = 1; }
+  while (have) {                                  /* is_valid, :123-128 */
+    if (n < src_cap) src[n] = (uint32_t)pos[cur];
+    ++n;
+    /* next(), :130-169: advance every heap iterator whose head equals the current key */
+    while (hn && same_key(in, pos[heap[0]], pos[cur])) {
+      uint32_t t = heap[0];
+      if (++pos[t] < run_start[t + 1]) sift_down(&m, heap, hn, 0);
+      else { heap[0] = heap[--hn]; sift_down(&m, heap, hn, 0); }
+    }
+    if (++pos[cur] >= run_start[cur + 1]) {       /* :156-161 */
+      if (hn) { cur = heap[0]; heap[0] = heap[--hn]; sift_down(&m, heap, hn, 0); }
+      else have = 0;
+      continue;
+    }
+    if (hn && head_cmp(&m, cur, heap[0]) > 0) {   /* :163-167: swap with the top */
+      uint32_t t = heap[0]; heap[0] = cur; cur = t; sift_down(&m, heap, hn, 0);
+    }
+  }
+  free(pos); free(heap);
+  *n_out = n;
+  return n <= src_cap ? ORC_OK : ORC_E_CAPACITY;
+}
+
+/* compact_generate_sst (src/compact.rs:223-311) over a merged stream given as src[0..n) indices
+ * into `in`: the keep/drop rules (:239-276), the SST rotation (:278-289) and SsTableBuilder::add
+ * (table/builder.rs:48-65) with estimate_size() = data.len() (finished blocks + 4-B CRC each,
+ * :105-123).  Outputs the blocks packed (no CRC), blk_off[nblk+1], for every SST its first
+ * block sst_blk[s] and its first kept entry sst_ent[s] (nsst+1 values each), and kept[] = the
+ * src positions handed to SsTableBuilder::add.  If nothing is kept the reference panics
+ * building an empty SST; here nsst = 0. */
+int orc_compact(const orc_kv* in, const uint32_t* src, uint64_t n, uint64_t watermark, int bottom,
+                const uint8_t* const* prefixes, const size_t* prefix_len, uint32_t nprefix,
+                size_t block_size, uint64_t target, uint8_t* out, uint64_t out_cap, uint64_t* blk_off,
+                uint64_t blk_cap, uint32_t* sst_blk, uint32_t* sst_ent, uint64_t sst_cap, uint32_t* kept,
+                uint64_t kept_cap, uint64_t* nblk_out, uint64_t* nbytes_out, uint64_t* nsst_out,
+                uint64_t* nkept_out) {
+  orc_builder* b = NULL;
+  uint64_t data_len = 0, nb = 0, pos = 0, nsst = 0, nk = 0;
+  const uint8_t* last_key = NULL;
+  size_t last_len = 0;
+  int first_below = 0, rc = ORC_OK;
+  size_t scratch_cap = 1 << 16;
+  uint8_t* scratch = (uint8_t*)malloc(scratch_cap);
+#define EMIT_BLOCK()                                                                   \
+  do {                                                                                  \
+    size_t need = orc_builder_estimated_size(b), l;                                     \
+    if (need > scratch_cap) { scratch_cap = need; scratch = (uint8_t*)realloc(scratch, need); } \
+    orc_builder_finish(b, scratch, scratch_cap, &l);                                    \
+    if (nb < blk_cap) blk_off[nb] = pos;                                                \
+    if (pos + l <= out_cap) memcpy(out + pos, scratch, l); else rc = ORC_E_CAPACITY;    \
+    pos += l; ++nb; data_len += l + 4;                                                  \
+  } while (0)
+  for (uint64_t j = 0; j < n; ++j) {
+    uint64_t i = src[j];
+    const uint8_t* k = in->keys + in->key_off[i];
+    size_t kl = in->key_off[i + 1] - in->key_off[i];
+    const uint8_t* v = in->vals + in->val_off[i];
+    size_t vl = in->val_off[i + 1] - in->val_off[i];
+    uint64_t ts = in->ts[i];
+    if (!b) {                                                   /* :235-237 */
+      b = orc_builder_new(block_size);
+      data_len = 0;
+      if (nsst < sst_cap) { sst_blk[nsst] = (uint32_t)nb; sst_ent[nsst] = (uint32_t)nk; }
+      ++nsst;
+    }
+    int same = last_key && last_len == kl && memcmp(last_key, k, kl) == 0;   /* :239 */
+    if (!same) first_below = 1;
+    if (bottom && !same && ts <= watermark && vl == 0) {       /* :244-254 */
+      last_key = k; last_len = kl; first_below = 0;
+      continue;
+    }
+    if (ts <= watermark) {                                      /* :256-276 */
+      if (same && !first_below) continue;
+      first_below = 0;
+      int drop = 0;
+      for (uint32_t f = 0; f < nprefix && !drop; ++f)
+        drop = prefix_len[f] <= kl && memcmp(prefixes[f], k, prefix_len[f]) == 0;
+      if (drop) continue;
+    }
+    if (data_len >= target && !same) {                          /* :278-289 */
+      if (!orc_builder_is_empty(b)) EMIT_BLOCK();               /* build() -> finish_block */
+      data_len = 0;
+      if (nsst < sst_cap) { sst_blk[nsst] = (uint32_t)nb; sst_ent[nsst] = (uint32_t)nk; }
+      ++nsst;
+    }
+    int a = orc_builder_add(b, k, kl, ts, v, vl);               /* SsTableBuilder::add */
+    if (a < 0) { rc = a; goto done; }
+    if (a == 0) {
+      EMIT_BLOCK();                                             /* finish_block */
+      if (orc_builder_add(b, k, kl, ts, v, vl) != 1) { rc = ORC_E_INVAL; goto done; }
+    }
+    if (nk < kept_cap) kept[nk] = (uint32_t)j;
+    ++nk;
+    if (!same) { last_key = k; last_len = kl; }                 /* :294-297 */
+  }
+  if (b && !orc_builder_is_empty(b)) EMIT_BLOCK();
+  if (b && nk == 0) nsst = 0;   /* the reference would panic: build() of an empty SST */
+#undef EMIT_BLOCK
+  if (nb < blk_cap) blk_off[nb] = pos;
+  if (nsst < sst_cap) { sst_blk[nsst] = (uint32_t)nb; sst_ent[nsst] = (uint32_t)nk; }
+  if (nb + 1 > blk_cap || nsst + 1 > sst_cap || nk > kept_cap) rc = rc ? rc : ORC_E_CAPACITY;
+done:
+  *nblk_out = nb; *nbytes_out = pos; *nsst_out = nsst; *nkept_out = nk;
+  free(scratch);
+  orc_builder_free(b);
+  return rc;
+}
+
 /* ------------------------------------------------------------------ crc32 */
 uint32_t orc_crc32(const uint8_t* p, size_t n) {
   static uint32_t table[256];

@@ -88,6 +88,23 @@ int orc_decode_blocks(const uint8_t* blocks, const uint64_t* blk_off, uint64_t n
 int orc_segment_like_compaction(const orc_kv* kv, size_t block_size, uint64_t target_sst_size,
                                 uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg);
 
+/* MergeIterator (src/iterators/merge_iterator.rs:59-184) over the sorted runs
+ * [run_start[r], run_start[r+1]) of `in` (run 0 = highest priority): src[j] = the input index
+ * of the j-th merged entry. */
+int orc_merge_runs(const orc_kv* in, const uint32_t* run_start, uint32_t nrun, uint32_t* src,
+                   uint64_t src_cap, uint64_t* n_out);
+
+/* compact_generate_sst (src/compact.rs:223-311) over the merged stream src[0..n): compaction
+ * rules, SST rotation at target_sst_size, one SsTableBuilder per SST.  Blocks packed (no CRC)
+ * with blk_off[nblk+1]; per SST its first block sst_blk[] and first kept entry sst_ent[]
+ * (nsst+1 values); kept[] = merged positions handed to SsTableBuilder::add. */
+int orc_compact(const orc_kv* in, const uint32_t* src, uint64_t n, uint64_t watermark, int bottom,
+                const uint8_t* const* prefixes, const size_t* prefix_len, uint32_t nprefix,
+                size_t block_size, uint64_t target, uint8_t* out, uint64_t out_cap, uint64_t* blk_off,
+                uint64_t blk_cap, uint32_t* sst_blk, uint32_t* sst_ent, uint64_t sst_cap, uint32_t* kept,
+                uint64_t kept_cap, uint64_t* nblk_out, uint64_t* nbytes_out, uint64_t* nsst_out,
+                uint64_t* nkept_out);
+
 /* CRC-32/ISO-HDLC (crc32fast 1.4.0 == zlib crc32), used by SST framing. */
 uint32_t orc_crc32(const uint8_t* p, size_t n);
 

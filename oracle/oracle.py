@@ -48,6 +48,10 @@ def lib():
                                                ctypes.POINTER(S), ctypes.POINTER(S)]
         L.orc_crc32.argtypes = [P, S]
         L.orc_crc32.restype = U32
+        L.orc_merge_runs.argtypes = [P, P, U32, P, U64, ctypes.POINTER(U64)]
+        L.orc_compact.argtypes = [P, P, U64, U64, I, P, P, U32, S, U64, P, U64, P, U64, P, P, U64, P, U64,
+                                  ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                  ctypes.POINTER(U64)]
         _lib = L
     return _lib
 
@@ -150,6 +154,65 @@ def segment_like_compaction(kv: KV, block_size: int, target_sst_size: int):
                                            seg.ctypes.data, len(seg), ctypes.byref(ns))
     assert rc == ORC_OK, rc
     return seg[:ns.value + 1]
+
+
+def merge_runs(kv: KV, run_start):
+    """MergeIterator over the sorted runs of kv -> src u32[n_merged] (input indices)."""
+    rs = np.ascontiguousarray(run_start, np.uint32)
+    src = np.zeros(max(kv.n, 1), np.uint32)
+    n = ctypes.c_uint64()
+    c = kv._c()
+    rc = lib().orc_merge_runs(ctypes.byref(c), rs.ctypes.data, len(rs) - 1, src.ctypes.data, len(src),
+                              ctypes.byref(n))
+    assert rc == ORC_OK, rc
+    return src[:n.value]
+
+
+def gather(kv: KV, idx) -> KV:
+    """The sub-stream kv[idx] (entries in the order of idx)."""
+    idx = np.asarray(idx, np.int64)
+    kl = (kv.key_off[idx + 1] - kv.key_off[idx]).astype(np.int64)
+    vl = (kv.val_off[idx + 1] - kv.val_off[idx]).astype(np.int64)
+    ko = np.zeros(len(idx) + 1, np.uint32)
+    vo = np.zeros(len(idx) + 1, np.uint32)
+    ko[1:] = np.cumsum(kl)
+    vo[1:] = np.cumsum(vl)
+
+    def cat(arena, off, ln):
+        if len(idx) == 0 or ln.sum() == 0:
+            return np.zeros(0, np.uint8)
+        starts = off[idx].astype(np.int64)
+        rep = np.repeat(starts - np.concatenate([[0], np.cumsum(ln)[:-1]]), ln)
+        return arena[np.arange(int(ln.sum()), dtype=np.int64) + rep]
+    return KV(cat(kv.keys, kv.key_off, kl), ko, cat(kv.vals, kv.val_off, vl), vo, kv.ts[idx].copy())
+
+
+def compact(kv: KV, src, watermark, bottom, prefixes, block_size, target):
+    """compact_generate_sst over the merged stream kv[src] -> dict(blocks, blk_off, sst_blk,
+    sst_ent, kept) (kept = merged positions added to an SST)."""
+    src = np.ascontiguousarray(src, np.uint32)
+    n = len(src)
+    kl = int((kv.key_off[src.astype(np.int64) + 1] - kv.key_off[src]).sum()) if n else 0
+    vl = int((kv.val_off[src.astype(np.int64) + 1] - kv.val_off[src]).sum()) if n else 0
+    out_cap = kl + vl + 18 * n + 16
+    out = np.zeros(max(out_cap, 1), np.uint8)
+    blk_off = np.zeros(n + 2, np.uint64)
+    sst_blk = np.zeros(n + 2, np.uint32)
+    sst_ent = np.zeros(n + 2, np.uint32)
+    kept = np.zeros(max(n, 1), np.uint32)
+    pf = [bytes(p) for p in prefixes]
+    pbufs = [ctypes.create_string_buffer(p, len(p)) for p in pf]
+    parr = (ctypes.c_void_p * max(len(pf), 1))(*[ctypes.addressof(b) for b in pbufs])
+    plen = (ctypes.c_size_t * max(len(pf), 1))(*[len(p) for p in pf])
+    nb, nbytes, nsst, nk = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    c = kv._c()
+    rc = lib().orc_compact(ctypes.byref(c), src.ctypes.data if n else None, n, watermark, int(bool(bottom)),
+                           parr, plen, len(pf), block_size, target, out.ctypes.data, out_cap, blk_off.ctypes.data,
+                           len(blk_off), sst_blk.ctypes.data, sst_ent.ctypes.data, len(sst_blk), kept.ctypes.data,
+                           len(kept), ctypes.byref(nb), ctypes.byref(nbytes), ctypes.byref(nsst), ctypes.byref(nk))
+    assert rc == ORC_OK, rc
+    return dict(blocks=out[:nbytes.value], blk_off=blk_off[:nb.value + 1], sst_blk=sst_blk[:nsst.value + 1],
+                sst_ent=sst_ent[:nsst.value + 1], kept=kept[:nk.value])
 
 
 class Builder:

@@ -193,6 +193,211 @@ def compact_filter_loop(entries, watermark, bottom_level, prefixes=()):
     return out
 
 
+class ListIter:
+    """StorageIterator over a list of (key, ts, value) -- the role SsTableIterator / MockIterator
+    play for MergeIterator (src/iterators.rs:5-23, src/tests/harness.rs:18-84).  key() returns the
+    user key only: Key's Eq / Ord ignore the ts (src/key.rs:63-81)."""
+
+    def __init__(self, entries):
+        self.e, self.i = list(entries), 0
+
+    def is_valid(self):
+        return self.i < len(self.e)
+
+    def key(self):
+        return self.e[self.i][0]
+
+    def entry(self):
+        return self.e[self.i]
+
+    def next(self):
+        self.i += 1
+
+
+class MergeIterator:
+    """src/iterators/merge_iterator.rs:59-184, line by line.  The BinaryHeap of HeapWrapper(idx,
+    iter) is a max-heap under the REVERSED (key, idx) order (:21-33), i.e. a min-heap on
+    (user key, idx): heapq with (key, idx) tuples pops the same element (idx are distinct)."""
+
+    def __init__(self, iters):
+        import heapq
+        self._hq = heapq
+        self.iters = {}
+        self.heap = []
+        self.current = None
+        if not iters:  # :73-78
+            return
+        if all(not it.is_valid() for it in iters):  # :84-90
+            self.current = (0, iters[-1])
+            return
+        for idx, it in enumerate(iters):  # :93-97
+            if it.is_valid():
+                self.iters[idx] = it
+                heapq.heappush(self.heap, (it.key(), idx))
+        _, idx = heapq.heappop(self.heap)  # :100
+        self.current = (idx, self.iters.pop(idx))
+
+    def is_valid(self):  # :123-128
+        return self.current is not None and self.current[1].is_valid()
+
+    def entry(self):
+        return self.current[1].entry()
+
+    def next(self):  # :130-169
+        hq = self._hq
+        cidx, cur = self.current
+        while self.heap:  # peek_mut
+            key, idx = self.heap[0]
+            if key == cur.key():  # :139, ts-agnostic Eq
+                it = self.iters[idx]
+                it.next()
+                hq.heappop(self.heap)
+                if it.is_valid():  # PeekMut drop re-sifts the advanced iterator
+                    hq.heappush(self.heap, (it.key(), idx))
+                else:  # :146-148
+                    del self.iters[idx]
+            else:
+                break
+        cur.next()  # :154
+        if not cur.is_valid():  # :156-161
+            if self.heap:
+                _, idx = hq.heappop(self.heap)
+                self.current = (idx, self.iters.pop(idx))
+            return
+        if self.heap:  # :163-167: swap when current's (key, idx) is greater than the top's
+            key, idx = self.heap[0]
+            if (cur.key(), cidx) > (key, idx):
+                hq.heappop(self.heap)
+                top = self.iters.pop(idx)
+                self.iters[cidx] = cur
+                hq.heappush(self.heap, (cur.key(), cidx))
+                self.current = (idx, top)
+
+
+class TwoMergeIterator:
+    """src/iterators/two_merge_iterator.rs:5-98, line by line, quirks included: skip_b advances b
+    ONCE per equal key (:45-50), choose_a is false as soon as b is invalid (:32-42), so the
+    merged stream ends with b."""
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+        self._skip_b()
+        self.choose_a = self._choose_a()
+
+    def _choose_a(self):
+        if not self.a.is_valid() or not self.b.is_valid():
+            return False
+        return self.a.entry()[0] < self.b.entry()[0]
+
+    def _skip_b(self):
+        if self.a.is_valid() and self.b.is_valid() and self.b.entry()[0] == self.a.entry()[0]:
+            self.b.next()
+
+    def is_valid(self):
+        return self.a.is_valid() if self.choose_a else self.b.is_valid()
+
+    def entry(self):
+        return self.a.entry() if self.choose_a else self.b.entry()
+
+    def next(self):
+        (self.a if self.choose_a else self.b).next()
+        self._skip_b()
+        self.choose_a = self._choose_a()
+
+
+def drain(it):
+    out = []
+    while it.is_valid():
+        out.append(it.entry())
+        it.next()
+    return out
+
+
+def merge_runs(runs):
+    """MergeIterator over sorted runs (run 0 = highest priority, e.g. the newest L0 SST)."""
+    return drain(MergeIterator([ListIter(r) for r in runs]))
+
+
+def merge_runs_rule(runs):
+    """The closed form the GPU merge evaluates: for every user key, all the versions held by the
+    lowest-index run containing that key, in that run's order; keys ascending."""
+    owner = {}
+    for r, run in enumerate(runs):
+        for k, _, _ in run:
+            owner.setdefault(k, r)
+    out = []
+    for k in sorted(owner):
+        out += [e for e in runs[owner[k]] if e[0] == k]
+    return out
+
+
+class SsTableBuilderRef:
+    """SsTableBuilder (src/table/builder.rs:16-123) for one SST: blocks, the data section
+    length estimate_size() (blocks + 4-B CRC each, :105-107, 112-123) and the entries added."""
+
+    def __init__(self, block_size):
+        self.block_size = block_size
+        self.builder = BlockBuilder(block_size)
+        self.blocks, self.data_len, self.entries = [], 0, []
+
+    def add(self, key, ts, value):  # :48-65
+        self.entries.append((key, ts, value))
+        if self.builder.add(key, ts, value):
+            return
+        self.finish_block()
+        assert self.builder.add(key, ts, value)
+
+    def finish_block(self):  # :112-123
+        blk = self.builder.build_encoded()
+        self.builder = BlockBuilder(self.block_size)
+        self.blocks.append(blk)
+        self.data_len += len(blk) + 4
+
+    def estimate_size(self):
+        return self.data_len
+
+    def build(self):  # :68-74 (the file layout after the data section is not modelled here)
+        self.finish_block()
+        return self.blocks, self.entries
+
+
+def compact_generate_sst(it, watermark, bottom_level, prefixes, block_size, target_sst_size):
+    """compact_generate_sst (src/compact.rs:223-311) line by line over a StorageIterator:
+    the compaction rules AND the SST rotation (:278-289).  Returns [(blocks, entries)] per SST."""
+    builder, new_sst = None, []
+    last_key, first_key_below_watermark = b"", False
+    while it.is_valid():  # :234
+        if builder is None:  # :235-237
+            builder = SsTableBuilderRef(block_size)
+        key, ts, value = it.entry()
+        same_as_last_key = key == last_key  # :239
+        if not same_as_last_key:
+            first_key_below_watermark = True
+        if bottom_level and not same_as_last_key and ts <= watermark and len(value) == 0:  # :244-254
+            last_key = key
+            it.next()
+            first_key_below_watermark = False
+            continue
+        if ts <= watermark:  # :256-276
+            if same_as_last_key and not first_key_below_watermark:
+                it.next()
+                continue
+            first_key_below_watermark = False
+            if any(key.startswith(p) for p in prefixes):
+                it.next()
+                continue
+        if builder.estimate_size() >= target_sst_size and not same_as_last_key:  # :278-289
+            new_sst.append(builder.build())
+            builder = SsTableBuilderRef(block_size)
+        builder.add(key, ts, value)  # :291-292
+        if not same_as_last_key:  # :294-297
+            last_key = key
+        it.next()
+    if builder is not None:  # :301-309
+        new_sst.append(builder.build())
+    return new_sst
+
+
 def compact_filter_rule(entries, watermark, bottom_level, prefixes=()):
     """The closed form the GPU evaluates per entry (lsmblk_gpu.hip, filt_keep): an entry needs
     only itself and its predecessor."""
