@@ -115,7 +115,7 @@ def main():
     seg_t = torch.from_numpy(seg.view(np.int32)).to(dev)
     st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
     st_enc = torch.zeros(4, dtype=torch.int64, device=dev)
-    ctx = batch._ctx(local)
+    ctx = batch._ctx(local, torch.cuda.current_stream(dev))
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
     stream = torch.cuda.current_stream(dev)
 
@@ -312,7 +312,7 @@ def compaction_filter(kv, n, K, V, dev, stream, reps=5):
     pfo = torch.tensor([0, 3], dtype=torch.int32, device=dev)
     st = torch.zeros(4, dtype=torch.int64, device=dev)
     ci, co = kv._c(), out._c(n, K + 16, V + 16)
-    ctx = batch._ctx(dev.index)
+    ctx = batch._ctx(dev.index, stream)
 
     def run():
         _check(_lib().lsmblk_compact_filter_batch(ctx, ctypes.byref(ci), 1 << 39, 1, pfx.data_ptr(), pfo.data_ptr(), 1,

@@ -235,6 +235,20 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uin
                                 uint32_t nprefix, const lsmblk_kv_stream* out, uint64_t* stats,
                                 void* stream);
 
+/* k-way merge of sorted runs (SURVEY.md §8 f, row 2) with MergeIterator's semantics
+ * (src/iterators/merge_iterator.rs:59-184): run r = entries [run_start[r], run_start[r+1]) of `in`
+ * (run_start: device u32[nrun+1], [0] = 0, [nrun] = in->n; 1 <= nrun <= 64), run 0 the highest
+ * priority (MergeIterator::create's index 0, e.g. the newest L0 SST).  Heads compare by user key
+ * only (src/key.rs:63-81) with the run index breaking ties, and every step advances the other
+ * runs' heads equal to the current key (:134-152): for every user key the output holds all the
+ * versions of the lowest-index run containing it, in that run's order.  Each run must be sorted
+ * by key (the reference's debug_assert :135-138); a merged order that is not reports
+ * LSMBLK_ERR_MALFORMED.  The merged stream is written to `out` (any alignment; capacities as
+ * for decode).  stats: [0] entries [1] key bytes [2] value bytes [3] error flags (CAPACITY with
+ * the required sizes in [0..2]; SEGMENTS: bad run_start).  Asynchronous. */
+int lsmblk_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                       const lsmblk_kv_stream* out, uint64_t* stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,6 +75,7 @@ SIGNATURES = [
     ("lsmblk_block_meta_batch", I, [P, P, P, U64, U32, P, U32, P, U64, P, P, P]),
     ("lsmblk_compact_filter_batch", I, [P, ctypes.POINTER(KVStreamC), U64, I, P, P, U32,
                                         ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_merge_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(KVStreamC), P, P]),
 ]
 
 

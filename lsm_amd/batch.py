@@ -29,14 +29,30 @@ _ctx_lock = threading.Lock()
 _ctxs = {}
 
 
-def _ctx(device: int):
+class _Ctx:
+    """One lsmblk_ctx per (device, stream): a context's device workspace is reused by every call
+    on it, so two streams never share one.  `lock` serialises call sequences that depend on the
+    workspace between calls (encode_into -> segment_blocks_into) across host threads."""
+
+    def __init__(self, handle):
+        self.h = handle
+        self.lock = threading.RLock()
+
+
+def _ctx_for(device: int, stream_ptr: int) -> _Ctx:
+    key = (device, stream_ptr)
     with _ctx_lock:
-        c = _ctxs.get(device)
+        c = _ctxs.get(key)
         if c is None:
             h = ctypes.c_void_p()
             check(lib().lsmblk_ctx_create(device, ctypes.byref(h)), "lsmblk_ctx_create")
-            c = _ctxs[device] = h.value
+            c = _ctxs[key] = _Ctx(h.value)
         return c
+
+
+def _ctx(device: int, stream=None):
+    """Context handle for `device` and `stream` (default: the device's current stream)."""
+    return _ctx_for(device, _stream_ptr(stream, device)).h
 
 
 def _stream_ptr(stream, device):
@@ -52,6 +68,21 @@ def _dev_index(t: torch.Tensor) -> int:
 
 def _ptr(t):
     return t.data_ptr() if t is not None and t.numel() else None
+
+
+def _need(t, dtype, name, dev, min_numel=0):
+    """The C ABI reads raw pointers: check dtype, contiguity, device and size before a call."""
+    if t is None:
+        raise ValueError(f"{name}: missing tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.device.type != "cuda" or _dev_index(t) != dev:
+        raise ValueError(f"{name}: must be on cuda:{dev}, got {t.device}")
+    if t.numel() < min_numel:
+        raise ValueError(f"{name}: needs >= {min_numel} elements, has {t.numel()}")
+    return t
 
 
 def _aligned_empty(nbytes: int, device) -> torch.Tensor:
@@ -81,6 +112,16 @@ class KVStream:
                          self.keys.numel() if key_cap is None else key_cap,
                          self.vals.numel() if val_cap is None else val_cap)
 
+    def check(self, dev, name="kv", entries=None):
+        """Dtypes / contiguity / device / sizes of the five arrays for `entries` (default n)."""
+        e = self.n if entries is None else entries
+        _need(self.keys, torch.uint8, name + ".keys", dev)
+        _need(self.vals, torch.uint8, name + ".vals", dev)
+        _need(self.key_off, torch.int32, name + ".key_off", dev, e + 1)
+        _need(self.val_off, torch.int32, name + ".val_off", dev, e + 1)
+        _need(self.ts, torch.int64, name + ".ts", dev, e)
+        return self
+
     @staticmethod
     def from_numpy(keys, key_off, vals, val_off, ts, device="cuda"):
         dev = torch.device(device)
@@ -94,7 +135,26 @@ class KVStream:
         ko = torch.from_numpy(np.ascontiguousarray(key_off, np.uint32).view(np.int32)).to(dev)
         vo = torch.from_numpy(np.ascontiguousarray(val_off, np.uint32).view(np.int32)).to(dev)
         t = torch.from_numpy(np.ascontiguousarray(ts, np.uint64).view(np.int64)).to(dev)
+        if n == 0:
+            t = torch.zeros(1, dtype=torch.int64, device=dev)
         return KVStream(k, ko, v, vo, t, n)
+
+    @staticmethod
+    def empty(n, key_bytes, val_bytes, device):
+        """Output buffers for up to n entries / key_bytes / val_bytes (16-B aligned arenas)."""
+        return KVStream(_aligned_empty(key_bytes + 16, device), torch.zeros(n + 1, dtype=torch.int32, device=device),
+                        _aligned_empty(val_bytes + 16, device), torch.zeros(n + 1, dtype=torch.int32, device=device),
+                        torch.zeros(max(n, 1), dtype=torch.int64, device=device), 0)
+
+    def caps(self):
+        """(entry_cap, key_cap, val_cap) of a stream made by empty()."""
+        return self.key_off.numel() - 1, self.keys.numel(), self.vals.numel()
+
+    def byte_sizes(self):
+        """(key bytes, value bytes) of the stream (reads the sentinels: synchronizes)."""
+        if self.n == 0:
+            return 0, 0
+        return (int(self.key_off[self.n].item()) & 0xFFFFFFFF, int(self.val_off[self.n].item()) & 0xFFFFFFFF)
 
     def to_numpy(self):
         """-> (keys u8, key_off u32, vals u8, val_off u32, ts u64) trimmed to the stream."""
@@ -109,11 +169,25 @@ def _status(stats: torch.Tensor) -> int:
     return lib().lsmblk_stats_status(int(stats[3].item()) & 0xFFFFFFFFFFFFFFFF)
 
 
+def _u32_table(x, dev):
+    if not isinstance(x, torch.Tensor):
+        x = torch.from_numpy(np.ascontiguousarray(x, np.uint32).view(np.int32))
+    return x.to(dev).contiguous()
+
+
 def decode_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_cap, val_cap, stream=None):
     """Asynchronous decode into preallocated buffers (no host sync). stats: int64[4] device."""
     dev = _dev_index(blk_off)
+    _need(blk_off, torch.int64, "blk_off", dev, nblk + 1)
+    if nblk:
+        _need(blocks, torch.uint8, "blocks", dev)
+    _need(stats, torch.int64, "stats", dev, STATS_WORDS)
+    out.check(dev, "out", 0)
+    if out.key_off.numel() < entry_cap + 1 or out.ts.numel() < entry_cap or out.keys.numel() < key_cap \
+            or out.vals.numel() < val_cap:
+        raise ValueError("decode_into: capacities exceed the output tensors")
     c = out._c(entry_cap, key_cap, val_cap)
-    check(lib().lsmblk_decode_batch(_ctx(dev), _ptr(blocks), _ptr(blk_off), nblk, ctypes.byref(c),
+    check(lib().lsmblk_decode_batch(_ctx(dev, stream), _ptr(blocks), _ptr(blk_off), nblk, ctypes.byref(c),
                                     stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_decode_batch")
 
 
@@ -152,8 +226,13 @@ def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: in
                 blk_off, blk_cap, stats, stream=None):
     """Asynchronous encode into preallocated buffers (no host sync)."""
     dev = _dev_index(seg_start)
+    kv.check(dev, "kv")
+    _need(seg_start, torch.int32, "seg_start", dev, nseg + 1)
+    _need(out, torch.uint8, "out", dev, out_cap)
+    _need(blk_off, torch.int64, "blk_off", dev, blk_cap)
+    _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     c = kv._c()
-    check(lib().lsmblk_encode_batch(_ctx(dev), ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
+    check(lib().lsmblk_encode_batch(_ctx(dev, stream), ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
                                     _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
                                     _stream_ptr(stream, dev)), "lsmblk_encode_batch")
 
@@ -161,13 +240,10 @@ def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: in
 def encode_kv(kv: KVStream, seg_start, block_size: int, stream=None):
     """Greedy block packing per segment -> (blocks u8 tensor, blk_off int64 tensor[nblk+1])."""
     dev = torch.device("cuda", _dev_index(kv.key_off))
-    if not isinstance(seg_start, torch.Tensor):
-        seg_start = torch.from_numpy(np.ascontiguousarray(seg_start, np.uint32).view(np.int32))
-    seg_start = seg_start.to(dev)
+    seg_start = _u32_table(seg_start, dev)
     nseg = seg_start.numel() - 1
-    kb = int(kv.key_off[kv.n].item()) if kv.n else 0
-    vb = int(kv.val_off[kv.n].item()) if kv.n else 0
-    out_cap, blk_cap = encode_bound(kv, kb & 0xFFFFFFFF, vb & 0xFFFFFFFF)
+    kb, vb = kv.byte_sizes()
+    out_cap, blk_cap = encode_bound(kv, kb, vb)
     out = _aligned_empty(out_cap, dev)
     blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
@@ -184,7 +260,12 @@ def crc32_into(blocks: torch.Tensor, blk_off: torch.Tensor, nblk: int, crc: torc
                tail: int = 0):
     """Asynchronous per-block CRC-32 into a preallocated int32 tensor (no host sync)."""
     dev = _dev_index(blk_off)
-    check(lib().lsmblk_crc32_batch(_ctx(dev), _ptr(blocks), blk_off.data_ptr(), nblk, tail, _ptr(crc),
+    _need(blk_off, torch.int64, "blk_off", dev, nblk + 1)
+    _need(crc, torch.int32, "crc", dev, nblk)
+    _need(stats, torch.int64, "stats", dev, STATS_WORDS)
+    if nblk:
+        _need(blocks, torch.uint8, "blocks", dev)
+    check(lib().lsmblk_crc32_batch(_ctx(dev, stream), _ptr(blocks), blk_off.data_ptr(), nblk, tail, _ptr(crc),
                                    stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_crc32_batch")
 
 
@@ -209,7 +290,10 @@ def segment_blocks_into(seg_start: torch.Tensor, nseg: int, enc_stats: torch.Ten
                         stream=None):
     """After encode_into on the same device/stream: seg_blk[s] = first block of segment s."""
     dev = _dev_index(seg_start)
-    check(lib().lsmblk_encode_segment_blocks(_ctx(dev), seg_start.data_ptr(), nseg, enc_stats.data_ptr(),
+    _need(seg_start, torch.int32, "seg_start", dev, nseg + 1)
+    _need(seg_blk, torch.int32, "seg_blk", dev, nseg + 1)
+    _need(enc_stats, torch.int64, "enc_stats", dev, STATS_WORDS)
+    check(lib().lsmblk_encode_segment_blocks(_ctx(dev, stream), seg_start.data_ptr(), nseg, enc_stats.data_ptr(),
                                              seg_blk.data_ptr(), _stream_ptr(stream, dev)),
           "lsmblk_encode_segment_blocks")
 
@@ -217,9 +301,14 @@ def segment_blocks_into(seg_start: torch.Tensor, nseg: int, enc_stats: torch.Ten
 def block_meta_into(blocks, blk_off, nblk, seg_blk, nseg, meta, meta_cap, meta_off, stats, stream=None, tail=0):
     """Asynchronous BlockMeta sections into preallocated buffers (no host sync)."""
     dev = _dev_index(blk_off)
-    check(lib().lsmblk_block_meta_batch(_ctx(dev), _ptr(blocks), blk_off.data_ptr(), nblk, tail, seg_blk.data_ptr(),
-                                        nseg, meta.data_ptr(), meta_cap, meta_off.data_ptr(), stats.data_ptr(),
-                                        _stream_ptr(stream, dev)), "lsmblk_block_meta_batch")
+    _need(blk_off, torch.int64, "blk_off", dev, nblk + 1)
+    _need(seg_blk, torch.int32, "seg_blk", dev, nseg + 1)
+    _need(meta, torch.uint8, "meta", dev, meta_cap)
+    _need(meta_off, torch.int64, "meta_off", dev, nseg + 1)
+    _need(stats, torch.int64, "stats", dev, STATS_WORDS)
+    check(lib().lsmblk_block_meta_batch(_ctx(dev, stream), _ptr(blocks), blk_off.data_ptr(), nblk, tail,
+                                        seg_blk.data_ptr(), nseg, meta.data_ptr(), meta_cap, meta_off.data_ptr(),
+                                        stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_block_meta_batch")
 
 
 def block_meta(blocks: torch.Tensor, blk_off: torch.Tensor, seg_blk, stream=None, tail: int = 0):
@@ -228,9 +317,7 @@ def block_meta(blocks: torch.Tensor, blk_off: torch.Tensor, seg_blk, stream=None
     seg_blk[s] .. seg_blk[s+1] are segment s's blocks.  Returns (meta u8 tensor, meta_off
     int64 tensor[nseg+1]); section s = meta[meta_off[s]:meta_off[s+1]]."""
     dev = torch.device("cuda", _dev_index(blk_off))
-    if not isinstance(seg_blk, torch.Tensor):
-        seg_blk = torch.from_numpy(np.ascontiguousarray(seg_blk, np.uint32).view(np.int32))
-    seg_blk = seg_blk.to(dev)
+    seg_blk = _u32_table(seg_blk, dev)
     nseg, nblk = seg_blk.numel() - 1, blk_off.numel() - 1
     meta_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
@@ -254,19 +341,19 @@ def encode_sst(kv: KVStream, seg_start, block_size: int, stream=None):
     CRC-32s (finish_block, src/table/builder.rs:112-123) and the BlockMeta sections (build,
     :68-77).  Returns dict(blocks, blk_off, seg_blk, crc, meta, meta_off)."""
     dev = torch.device("cuda", _dev_index(kv.key_off))
-    if not isinstance(seg_start, torch.Tensor):
-        seg_start = torch.from_numpy(np.ascontiguousarray(seg_start, np.uint32).view(np.int32))
-    seg_start = seg_start.to(dev)
+    seg_start = _u32_table(seg_start, dev)
     nseg = seg_start.numel() - 1
-    kb = int(kv.key_off[kv.n].item()) if kv.n else 0
-    vb = int(kv.val_off[kv.n].item()) if kv.n else 0
-    out_cap, blk_cap = encode_bound(kv, kb & 0xFFFFFFFF, vb & 0xFFFFFFFF)
+    kb, vb = kv.byte_sizes()
+    out_cap, blk_cap = encode_bound(kv, kb, vb)
     out = _aligned_empty(out_cap, dev)
     blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
     seg_blk = torch.zeros(nseg + 1, dtype=torch.int32, device=dev)
-    encode_into(kv, seg_start, nseg, block_size, out, out_cap, blk_off, blk_cap, stats, stream)
-    segment_blocks_into(seg_start, nseg, stats, seg_blk, stream)
+    # the segment -> block table reads the encode's workspace: no other encode on this context
+    # (same device and stream) may run in between
+    with _ctx_for(dev.index, _stream_ptr(stream, dev.index)).lock:
+        encode_into(kv, seg_start, nseg, block_size, out, out_cap, blk_off, blk_cap, stats, stream)
+        segment_blocks_into(seg_start, nseg, stats, seg_blk, stream)
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:
@@ -278,30 +365,63 @@ def encode_sst(kv: KVStream, seg_start, block_size: int, stream=None):
     return dict(blocks=blocks, blk_off=blk_off, seg_blk=seg_blk, crc=crc, meta=meta, meta_off=meta_off)
 
 
-def compact_filter(kv: KVStream, watermark: int, bottom_level: bool, prefixes=(), stream=None) -> KVStream:
-    """compact_generate_sst's per-entry rules (reference src/compact.rs:234-299) over a merged
-    stream (keys ascending, versions newest first) -> the kept entries as a new KVStream."""
-    dev = torch.device("cuda", _dev_index(kv.key_off))
-    pf = b"".join(prefixes)
+def _prefix_tables(prefixes, dev):
+    pf = b"".join(bytes(p) for p in prefixes)
     po = np.zeros(len(prefixes) + 1, np.uint32)
     po[1:] = np.cumsum([len(p) for p in prefixes]) if prefixes else []
     pfx = torch.frombuffer(bytearray(pf or b"\0"), dtype=torch.uint8).to(dev)
     pfo = torch.from_numpy(po.view(np.int32)).to(dev)
-    kb = int(kv.key_off[kv.n].item()) & 0xFFFFFFFF if kv.n else 0
-    vb = int(kv.val_off[kv.n].item()) & 0xFFFFFFFF if kv.n else 0
+    return pfx, pfo
+
+
+def compact_filter(kv: KVStream, watermark: int, bottom_level: bool, prefixes=(), stream=None) -> KVStream:
+    """compact_generate_sst's per-entry rules (reference src/compact.rs:234-299) over a merged
+    stream (keys ascending, versions newest first) -> the kept entries as a new KVStream."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    kv.check(dev.index, "kv")
+    pfx, pfo = _prefix_tables(prefixes, dev)
+    kb, vb = kv.byte_sizes()
     n = kv.n
-    out = KVStream(_aligned_empty(kb + 16, dev), torch.zeros(n + 1, dtype=torch.int32, device=dev),
-                   _aligned_empty(vb + 16, dev), torch.zeros(n + 1, dtype=torch.int32, device=dev),
-                   torch.zeros(max(n, 1), dtype=torch.int64, device=dev), 0)
+    out = KVStream.empty(n, kb, vb, dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
     ci, co = kv._c(), out._c(n, kb + 16, vb + 16)
-    check(lib().lsmblk_compact_filter_batch(_ctx(dev.index), ctypes.byref(ci), watermark, int(bool(bottom_level)),
-                                            pfx.data_ptr(), pfo.data_ptr(), len(prefixes), ctypes.byref(co),
-                                            stats.data_ptr(), _stream_ptr(stream, dev.index)),
+    check(lib().lsmblk_compact_filter_batch(_ctx(dev.index, stream), ctypes.byref(ci), watermark,
+                                            int(bool(bottom_level)), pfx.data_ptr(), pfo.data_ptr(), len(prefixes),
+                                            ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev.index)),
           "lsmblk_compact_filter_batch")
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:
         raise LsmBlkError(st, "compact_filter")
+    out.n = int(stats[0].item())
+    return out
+
+
+def merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, out: KVStream, stats, stream=None):
+    """Asynchronous MergeIterator over the runs of kv into preallocated `out` (no host sync)."""
+    dev = _dev_index(run_start)
+    kv.check(dev, "kv")
+    _need(run_start, torch.int32, "run_start", dev, nrun + 1)
+    out.check(dev, "out", 0)
+    _need(stats, torch.int64, "stats", dev, STATS_WORDS)
+    ci, co = kv._c(), out._c(*out.caps())
+    check(lib().lsmblk_merge_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun,
+                                   ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev)),
+          "lsmblk_merge_batch")
+
+
+def merge_runs(kv: KVStream, run_start, stream=None) -> KVStream:
+    """MergeIterator (reference src/iterators/merge_iterator.rs:59-184) over the sorted runs
+    kv[run_start[r]:run_start[r+1]] (run 0 = highest priority) -> the merged KVStream."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    rs = _u32_table(run_start, dev)
+    kb, vb = kv.byte_sizes()
+    out = KVStream.empty(kv.n, kb, vb, dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    merge_into(kv, rs, rs.numel() - 1, out, stats, stream)
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "merge_runs")
     out.n = int(stats[0].item())
     return out

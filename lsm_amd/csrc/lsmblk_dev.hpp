@@ -1,0 +1,383 @@
+// lsmblk_dev.hpp -- shared by the HIP translation units of liblsmblk.so: wave primitives,
+// buffer-descriptor helpers, look-back granules (device) and the context struct (host).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "lsmblk.h"
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr uint32_t kSpinLimit = 1u << 22;  // look-back bound (~seconds); never reached when correct
+
+// ---------------------------------------------------------------- wave primitives
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return (uint64_t(uni(uint32_t(x >> 32))) << 32) | uni(uint32_t(x));
+}
+// lane j's x (readlane returns int: both halves go through uint32_t, no sign extension)
+__device__ __forceinline__ uint64_t lane64(uint64_t x, uint32_t j) {
+  return (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), j))) << 32) |
+         uint32_t(__builtin_amdgcn_readlane(uint32_t(x), j));
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// Wave64 inclusive scan / sum of u32 with DPP (row_shr 1,2,4,8 then row_bcast 15 / 31):
+// pure VALU, no ds_bpermute traffic through the LDS crossbar.
+#define LSM_DPP(v, ctrl, rmask) __builtin_amdgcn_update_dpp(0u, (v), (ctrl), (rmask), 0xF, false)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  v += LSM_DPP(v, 0x111, 0xF);  // row_shr:1
+  v += LSM_DPP(v, 0x112, 0xF);  // row_shr:2
+  v += LSM_DPP(v, 0x114, 0xF);  // row_shr:4
+  v += LSM_DPP(v, 0x118, 0xF);  // row_shr:8
+  v += LSM_DPP(v, 0x142, 0xA);  // row_bcast:15 -> rows 1, 3
+  v += LSM_DPP(v, 0x143, 0xC);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
+  v = max(v, LSM_DPP(v, 0x111, 0xF));
+  v = max(v, LSM_DPP(v, 0x112, 0xF));
+  v = max(v, LSM_DPP(v, 0x114, 0xF));
+  v = max(v, LSM_DPP(v, 0x118, 0xF));
+  v = max(v, LSM_DPP(v, 0x142, 0xA));
+  v = max(v, LSM_DPP(v, 0x143, 0xC));
+  return v;
+}
+// Inclusive min-scan of values <= 0x7FFFFFFF as the max-scan of 0x7FFFFFFF - v: DPP lanes
+// shifted in from outside a row read 0, the max identity.  (Measured on gfx950: an
+// update_dpp "old" of 0xFFFFFFFF does not reach those lanes, and ~max(~v) was folded away.)
+__device__ __forceinline__ uint32_t wave_incl_min31(uint32_t v) { return 0x7FFFFFFFu - wave_incl_max32(0x7FFFFFFFu - v); }
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+  return __builtin_amdgcn_readlane(wave_incl_scan32(v), 63);
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return T(wave_incl_scan32(uint32_t(v)));
+  } else {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      T t = __shfl_up(v, d, 64);
+      if (l >= d) v += t;
+    }
+    return v;
+  }
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return T(__builtin_amdgcn_readlane(wave_incl_scan32(uint32_t(v)), 63));
+  } else {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+  }
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p16, uint32_t nbytes) {
+  const uint32_t n = nbytes >= 0xFFFFFFF0u ? 0xFFFFFFFFu : (nbytes + 15) & ~15u;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p16), (short)0, (int)n, 0x00020000);
+}
+// Store descriptor with an exact byte bound: an access reaching past nbytes is dropped.
+__device__ __forceinline__ rsrc_t make_rsrc_exact(void* p16, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p16, (short)0, (int)nbytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF); }
+
+// ---------------------------------------------------------------- look-back granules
+// 8-byte granule = value << 16 | epoch << 2 | flag  (flag 1 = aggregate, 2 = inclusive).
+// Written by one relaxed agent-scope store (global_store sc1), read by relaxed agent-scope
+// loads: the value and its tag travel in one naturally aligned 8-byte word, so no fence is
+// needed (MI355X_MICROARCH.md, "granule" hand-off).
+// Poll protocol (kernel argument `poll`): 0 = sc1 loads; 1 = sc1 loads + agent acquire
+// fence between polls; 2 = agent-scope atomic RMW (fetch_or 0) polls and atomic-swap
+// publishes, performed at the coherence point.
+__device__ __forceinline__ uint64_t gload(const uint64_t* p, uint32_t poll) {
+  if (poll == 2)
+    return __hip_atomic_fetch_or(const_cast<uint64_t*>(p), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore(uint64_t* p, uint64_t v, uint32_t poll) {
+  if (poll == 2)
+    (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NQ>
+__device__ __forceinline__ void publish(uint64_t* arr, uint64_t idx, const uint64_t (&v)[NQ],
+                                        uint32_t tag, uint32_t flag, uint32_t poll) {
+  const uint32_t l = lane_id();
+  if (l < NQ) {
+    uint64_t x = v[0];
+    if (NQ > 1 && l == 1) x = v[1 % NQ];
+    if (NQ > 2 && l == 2) x = v[2 % NQ];
+    gstore(arr + idx * NQ + l, (x << 16) | (uint64_t(tag) << 2) | flag, poll);
+  }
+}
+
+// Wave-parallel decoupled look-back: lane j inspects predecessor (pred - j).  Returns false
+// on timeout (then excl is garbage and the caller raises LSMBLK_ERR_TIMEOUT).
+template <int NQ>
+__device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self, uint32_t tag,
+                         uint32_t poll, uint64_t (&excl)[NQ]) {
+  const uint32_t l = lane_id();
+  const uint64_t want_agg = (uint64_t(tag) << 2) | 1, want_inc = (uint64_t(tag) << 2) | 2;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) excl[q] = 0;
+  int64_t pred = int64_t(self) - 1;
+  uint32_t spins = 0;
+  while (pred >= 0) {
+    const int64_t idx = pred - int64_t(l);
+    uint64_t vi[NQ], va[NQ];
+    bool li = idx < 0, la = false;  // lanes before block 0 read as "inclusive 0"
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) vi[q] = va[q] = 0;
+    uint32_t round = 0;
+    for (;;) {
+      // Only lanes still unresolved poll.  A granule carrying the current epoch tag is the
+      // value its producer wrote (each is written once per epoch), so a ready observation
+      // is final; only not-ready observations are re-polled (first round plain sc1 loads,
+      // later rounds the protocol `poll`).
+      const uint32_t pm = round == 0 ? 0u : poll;
+      if (!li && !la) {
+        bool ri = true;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          vi[q] = gload(inc + idx * NQ + q, pm);
+          ri = ri && ((vi[q] & 0xFFFF) == want_inc);
+        }
+        li = ri;
+        if (!ri) {
+          bool ra = true;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            va[q] = gload(agg + idx * NQ + q, pm);
+            ra = ra && ((va[q] & 0xFFFF) == want_agg);
+          }
+          la = ra;
+        }
+      }
+      const uint64_t im = __ballot(li);
+      const uint64_t rm = __ballot(li || la);
+      const uint32_t first = im ? uint32_t(__builtin_ctzll(im)) : 64u;
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+      if ((rm & need) == need) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const uint64_t c = l < first ? (va[q] >> 16) : (l == first ? (vi[q] >> 16) : 0);
+          excl[q] += wave_sum(c);
+        }
+        if (first < 64) return true;
+        pred -= 64;
+        break;
+      }
+      ++round;
+      if (++spins > kSpinLimit) return false;
+      if (poll == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr) {
+  uint32_t t = 0;
+  if (lane_id() == 0) t = atomicAdd(ctr, 1u);
+  return uni(__shfl(t, 0, 64));
+}
+
+__device__ __forceinline__ void raise_err(uint64_t* stats, uint32_t err) {
+  if (err && lane_id() == 0) atomicOr(reinterpret_cast<unsigned long long*>(stats + 3), (unsigned long long)err);
+}
+
+// ---------------------------------------------------------------- byte sources
+// An "image" is a block's bytes addressed block-relative; LdsImg reads the LDS staging copy,
+// GlbImg reads global memory through a bounds-checked buffer descriptor (OOB reads = 0).
+// Decode reads the (unswizzled) LDS image with unaligned ds_read_u16/b32/b64/b128 (the gfx9
+// unaligned access mode): one instruction per field instead of one per byte.
+struct LdsImg {
+  const uint8_t* base;  // LDS image; block byte 0 is image byte lead
+  uint32_t lead;
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return base[lead + i]; }
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const {
+    return bswap16(*reinterpret_cast<const uint16_t*>(base + lead + i));
+  }
+  __device__ __forceinline__ uint32_t le32(uint32_t i) const {
+    return *reinterpret_cast<const uint32_t*>(base + lead + i);
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
+    const u32x2 q = *reinterpret_cast<const u32x2*>(base + lead + i);
+    return __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
+  }
+};
+struct GlbImg {
+  rsrc_t r;
+  uint32_t lead;  // rsrc base = block start - lead
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, lead + i, 0, 0);
+  }
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
+  __device__ __forceinline__ uint32_t le32(uint32_t i) const {
+    return u8(i) | (u8(i + 1) << 8) | (u8(i + 2) << 16) | (u8(i + 3) << 24);
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v = (v << 8) | u8(i + j);
+    return v;
+  }
+};
+
+// 4 bytes starting at byte offset x of a 4-byte-aligned LDS buffer.
+__device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
+  const uint32_t i = x >> 2;
+  return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
+}
+
+// Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
+// store when whole, else conditional whole-dword stores plus at most three bytes at each
+// end (closed-form; a wave pays ~10 stores for its partial lanes, not 16 byte stores).
+__device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t lo, uint32_t hi) {
+  if (lo == 0 && hi == 16) {
+    u32x4 q = {v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<u32x4*>(dst) = q;
+    return;
+  }
+  const uint32_t lo4 = (lo + 3) >> 2, hi4 = hi >> 2;  // whole dwords [lo4, hi4)
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+  for (uint32_t d = 0; d < 4; ++d)
+    if (d >= lo4 && d < hi4) d32[d] = v[d];
+  // head bytes [lo, min(hi, 4 lo4)) and tail bytes [max(lo, 4 hi4), hi); when the range lies
+  // inside one dword both describe the same bytes: only the head copy writes them
+  const uint32_t he = min(hi, 4 * lo4), ts = max(max(lo, 4 * hi4), he);
+  const uint32_t hw = v[min(lo >> 2, 3u)], tw = v[min(hi4, 3u)];
+#pragma unroll
+  for (uint32_t i = 0; i < 3; ++i) {
+    const uint32_t x = lo + i;
+    if (x < he) dst[x] = uint8_t(hw >> (8 * (x & 3)));
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < 3; ++i) {
+    const uint32_t x = ts + i;
+    if (x < hi) dst[x] = uint8_t(tw >> (8 * (x & 3)));
+  }
+}
+}  // namespace
+
+struct lsmblk_ctx {
+  int device = 0;
+  std::mutex mu;
+  uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket, [2] emit big-block count
+  uint32_t* dec_agg = nullptr;   // (entries, key bytes, value bytes) per block
+  uint64_t dec_cap = 0;
+  void* crc_tabs = nullptr;      // CrcTabs: CRC-32 slicing + zero-extension tables (first CRC call)
+  uint64_t* tile_sum = nullptr;  // 3 per 64-block tile
+  uint64_t* tile_pre = nullptr;
+  uint64_t tile_cap = 0;
+  uint64_t* seg_agg = nullptr;   // 2 granules per segment
+  uint64_t* seg_inc = nullptr;
+  uint64_t seg_cap = 0;
+  uint32_t* rec_first = nullptr; // n+1
+  uint32_t* blk_first = nullptr;
+  uint32_t* ent = nullptr;       // 3 per entry: rec, alcp, block sizes (plan passes)
+  uint32_t* big_list = nullptr;  // n+1: blocks for emit_big_kernel
+  uint64_t rec_cap = 0;
+  uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
+  uint32_t poll = 0;             // look-back poll protocol (see gload)
+  uint32_t skip = 0;             // decode ablation mask (timing experiments only)
+  bool timing = false;           // record HIP events around every kernel (diagnostics)
+  hipEvent_t ev[8] = {};         // decode: 0 count 1 scan 2 decode 3 | encode: 4 plan 5 emit 6
+  bool dec_timed = false, enc_timed = false;
+  // BlockMeta sections (lsmblk_block_meta_batch)
+  uint32_t* meta_rec = nullptr;     // nblk
+  uint64_t* meta_pos = nullptr;     // nblk + 1
+  uint64_t meta_blk_cap = 0;
+  uint64_t* meta_tile = nullptr;    // 2 per tile: sums, prefixes
+  uint64_t meta_tile_cap = 0;
+  uint32_t* meta_crc = nullptr;     // nseg
+  uint64_t meta_seg_cap = 0;
+  uint64_t* meta_cstats = nullptr;  // crc_kernel stats of the section CRC pass
+  // compaction filter (lsmblk_compact_filter_batch)
+  uint32_t* filt_keep = nullptr;    // n
+  uint64_t filt_cap = 0;
+  uint64_t* filt_tile = nullptr;    // 6 per tile: sums, prefixes
+  uint64_t filt_tile_cap = 0;
+  // merge / compaction pipeline (lsmblk_compact.hip): one arena, carved per call
+  uint8_t* cws = nullptr;
+  uint64_t cws_cap = 0;
+};
+
+namespace {
+
+// Look-back status granules live in uncached device memory: every poll and publish goes to
+// the coherence point, so no XCD's L2 can hold a stale copy (MI355X L2s are per XCD and not
+// coherent with each other).
+constexpr unsigned kStatusFlags = hipDeviceMallocUncached;
+
+template <typename T>
+int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per, unsigned flags = 0) {
+  if (need <= *cap) return LSMBLK_OK;
+  uint64_t nc = need + need / 4 + 1024;
+  if (*p) {
+    if (hipDeviceSynchronize() != hipSuccess) return LSMBLK_E_HIP;
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  const hipError_t e = flags ? hipExtMallocWithFlags(reinterpret_cast<void**>(p), nc * per * sizeof(T), flags)
+                            : hipMalloc(reinterpret_cast<void**>(p), nc * per * sizeof(T));
+  if (e != hipSuccess) {
+    *cap = 0;
+    return LSMBLK_E_NOMEM;
+  }
+  if (hipMemset(*p, 0, nc * per * sizeof(T)) != hipSuccess) return LSMBLK_E_HIP;
+  *cap = nc;
+  return LSMBLK_OK;
+}
+}  // namespace
+
+namespace {
+// Make `dev` current for one ABI call and restore the caller's device afterwards: the library
+// never changes which device the calling thread's later allocations land on.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+}  // namespace
+
+// Internal entry points shared between translation units (called with ctx->mu held).
+namespace lsmblk_impl {
+// lsmblk_encode_batch with optional device-side entry count (dn) and segment count (dnseg):
+// in->n and nseg are then upper bounds that size the grids and the workspace.
+int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
+                  const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
+                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st);
+// lsmblk_encode_segment_blocks for the encode that just ran on this context.
+int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
+                          uint32_t* seg_blk, hipStream_t st);
+}  // namespace lsmblk_impl

@@ -23,283 +23,10 @@
 //                   flushed with 16-B stores.
 // Blocks or batches that exceed the LDS fast paths take per-entry-lane "simple" paths
 // that read/write global memory directly (same results, slower).
-#include <hip/hip_runtime.h>
-
-#include <cstdint>
-#include <cstdlib>
-#include <cstring>
-#include <mutex>
-#include <new>
-
-#include "lsmblk.h"
+#include "lsmblk_dev.hpp"
 
 namespace {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-constexpr uint32_t kSpinLimit = 1u << 22;  // look-back bound (~seconds); never reached when correct
-
-// ---------------------------------------------------------------- wave primitives
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-  return (uint64_t(uni(uint32_t(x >> 32))) << 32) | uni(uint32_t(x));
-}
-// lane j's x (readlane returns int: both halves go through uint32_t, no sign extension)
-__device__ __forceinline__ uint64_t lane64(uint64_t x, uint32_t j) {
-  return (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), j))) << 32) |
-         uint32_t(__builtin_amdgcn_readlane(uint32_t(x), j));
-}
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-// Wave64 inclusive scan / sum of u32 with DPP (row_shr 1,2,4,8 then row_bcast 15 / 31):
-// pure VALU, no ds_bpermute traffic through the LDS crossbar.
-#define LSM_DPP(v, ctrl, rmask) __builtin_amdgcn_update_dpp(0u, (v), (ctrl), (rmask), 0xF, false)
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
-  v += LSM_DPP(v, 0x111, 0xF);  // row_shr:1
-  v += LSM_DPP(v, 0x112, 0xF);  // row_shr:2
-  v += LSM_DPP(v, 0x114, 0xF);  // row_shr:4
-  v += LSM_DPP(v, 0x118, 0xF);  // row_shr:8
-  v += LSM_DPP(v, 0x142, 0xA);  // row_bcast:15 -> rows 1, 3
-  v += LSM_DPP(v, 0x143, 0xC);  // row_bcast:31 -> rows 2, 3
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
-  v = max(v, LSM_DPP(v, 0x111, 0xF));
-  v = max(v, LSM_DPP(v, 0x112, 0xF));
-  v = max(v, LSM_DPP(v, 0x114, 0xF));
-  v = max(v, LSM_DPP(v, 0x118, 0xF));
-  v = max(v, LSM_DPP(v, 0x142, 0xA));
-  v = max(v, LSM_DPP(v, 0x143, 0xC));
-  return v;
-}
-// Inclusive min-scan of values <= 0x7FFFFFFF as the max-scan of 0x7FFFFFFF - v: DPP lanes
-// shifted in from outside a row read 0, the max identity.  (Measured on gfx950: an
-// update_dpp "old" of 0xFFFFFFFF does not reach those lanes, and ~max(~v) was folded away.)
-__device__ __forceinline__ uint32_t wave_incl_min31(uint32_t v) { return 0x7FFFFFFFu - wave_incl_max32(0x7FFFFFFFu - v); }
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
-  return __builtin_amdgcn_readlane(wave_incl_scan32(v), 63);
-}
-template <typename T>
-__device__ __forceinline__ T wave_incl_scan(T v) {
-  if constexpr (sizeof(T) == 4) {
-    return T(wave_incl_scan32(uint32_t(v)));
-  } else {
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      T t = __shfl_up(v, d, 64);
-      if (l >= d) v += t;
-    }
-    return v;
-  }
-}
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-  if constexpr (sizeof(T) == 4) {
-    return T(__builtin_amdgcn_readlane(wave_incl_scan32(uint32_t(v)), 63));
-  } else {
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-  }
-}
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p16, uint32_t nbytes) {
-  const uint32_t n = nbytes >= 0xFFFFFFF0u ? 0xFFFFFFFFu : (nbytes + 15) & ~15u;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p16), (short)0, (int)n, 0x00020000);
-}
-// Store descriptor with an exact byte bound: an access reaching past nbytes is dropped.
-__device__ __forceinline__ rsrc_t make_rsrc_exact(void* p16, uint32_t nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(p16, (short)0, (int)nbytes, 0x00020000);
-}
-__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFF) << 8) | ((v >> 8) & 0xFF); }
-
-// ---------------------------------------------------------------- look-back granules
-// 8-byte granule = value << 16 | epoch << 2 | flag  (flag 1 = aggregate, 2 = inclusive).
-// Written by one relaxed agent-scope store (global_store sc1), read by relaxed agent-scope
-// loads: the value and its tag travel in one naturally aligned 8-byte word, so no fence is
-// needed (MI355X_MICROARCH.md, "granule" hand-off).
-// Poll protocol (kernel argument `poll`): 0 = sc1 loads; 1 = sc1 loads + agent acquire
-// fence between polls; 2 = agent-scope atomic RMW (fetch_or 0) polls and atomic-swap
-// publishes, performed at the coherence point.
-__device__ __forceinline__ uint64_t gload(const uint64_t* p, uint32_t poll) {
-  if (poll == 2)
-    return __hip_atomic_fetch_or(const_cast<uint64_t*>(p), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gstore(uint64_t* p, uint64_t v, uint32_t poll) {
-  if (poll == 2)
-    (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int NQ>
-__device__ __forceinline__ void publish(uint64_t* arr, uint64_t idx, const uint64_t (&v)[NQ],
-                                        uint32_t tag, uint32_t flag, uint32_t poll) {
-  const uint32_t l = lane_id();
-  if (l < NQ) {
-    uint64_t x = v[0];
-    if (NQ > 1 && l == 1) x = v[1 % NQ];
-    if (NQ > 2 && l == 2) x = v[2 % NQ];
-    gstore(arr + idx * NQ + l, (x << 16) | (uint64_t(tag) << 2) | flag, poll);
-  }
-}
-
-// Wave-parallel decoupled look-back: lane j inspects predecessor (pred - j).  Returns false
-// on timeout (then excl is garbage and the caller raises LSMBLK_ERR_TIMEOUT).
-template <int NQ>
-__device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self, uint32_t tag,
-                         uint32_t poll, uint64_t (&excl)[NQ]) {
-  const uint32_t l = lane_id();
-  const uint64_t want_agg = (uint64_t(tag) << 2) | 1, want_inc = (uint64_t(tag) << 2) | 2;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) excl[q] = 0;
-  int64_t pred = int64_t(self) - 1;
-  uint32_t spins = 0;
-  while (pred >= 0) {
-    const int64_t idx = pred - int64_t(l);
-    uint64_t vi[NQ], va[NQ];
-    bool li = idx < 0, la = false;  // lanes before block 0 read as "inclusive 0"
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) vi[q] = va[q] = 0;
-    uint32_t round = 0;
-    for (;;) {
-      // Only lanes still unresolved poll.  A granule carrying the current epoch tag is the
-      // value its producer wrote (each is written once per epoch), so a ready observation
-      // is final; only not-ready observations are re-polled (first round plain sc1 loads,
-      // later rounds the protocol `poll`).
-      const uint32_t pm = round == 0 ? 0u : poll;
-      if (!li && !la) {
-        bool ri = true;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          vi[q] = gload(inc + idx * NQ + q, pm);
-          ri = ri && ((vi[q] & 0xFFFF) == want_inc);
-        }
-        li = ri;
-        if (!ri) {
-          bool ra = true;
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            va[q] = gload(agg + idx * NQ + q, pm);
-            ra = ra && ((va[q] & 0xFFFF) == want_agg);
-          }
-          la = ra;
-        }
-      }
-      const uint64_t im = __ballot(li);
-      const uint64_t rm = __ballot(li || la);
-      const uint32_t first = im ? uint32_t(__builtin_ctzll(im)) : 64u;
-      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-      if ((rm & need) == need) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const uint64_t c = l < first ? (va[q] >> 16) : (l == first ? (vi[q] >> 16) : 0);
-          excl[q] += wave_sum(c);
-        }
-        if (first < 64) return true;
-        pred -= 64;
-        break;
-      }
-      ++round;
-      if (++spins > kSpinLimit) return false;
-      if (poll == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  return true;
-}
-
-__device__ __forceinline__ uint32_t take_ticket(uint32_t* ctr) {
-  uint32_t t = 0;
-  if (lane_id() == 0) t = atomicAdd(ctr, 1u);
-  return uni(__shfl(t, 0, 64));
-}
-
-__device__ __forceinline__ void raise_err(uint64_t* stats, uint32_t err) {
-  if (err && lane_id() == 0) atomicOr(reinterpret_cast<unsigned long long*>(stats + 3), (unsigned long long)err);
-}
-
-// ---------------------------------------------------------------- byte sources
-// An "image" is a block's bytes addressed block-relative; LdsImg reads the LDS staging copy,
-// GlbImg reads global memory through a bounds-checked buffer descriptor (OOB reads = 0).
-// Decode reads the (unswizzled) LDS image with unaligned ds_read_u16/b32/b64/b128 (the gfx9
-// unaligned access mode): one instruction per field instead of one per byte.
-struct LdsImg {
-  const uint8_t* base;  // LDS image; block byte 0 is image byte lead
-  uint32_t lead;
-  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return base[lead + i]; }
-  __device__ __forceinline__ uint32_t u16(uint32_t i) const {
-    return bswap16(*reinterpret_cast<const uint16_t*>(base + lead + i));
-  }
-  __device__ __forceinline__ uint32_t le32(uint32_t i) const {
-    return *reinterpret_cast<const uint32_t*>(base + lead + i);
-  }
-  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
-    const u32x2 q = *reinterpret_cast<const u32x2*>(base + lead + i);
-    return __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
-  }
-};
-struct GlbImg {
-  rsrc_t r;
-  uint32_t lead;  // rsrc base = block start - lead
-  __device__ __forceinline__ uint32_t u8(uint32_t i) const {
-    return __builtin_amdgcn_raw_buffer_load_b8(r, lead + i, 0, 0);
-  }
-  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
-  __device__ __forceinline__ uint32_t le32(uint32_t i) const {
-    return u8(i) | (u8(i + 1) << 8) | (u8(i + 2) << 16) | (u8(i + 3) << 24);
-  }
-  __device__ __forceinline__ uint64_t u64(uint32_t i) const {
-    uint64_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v = (v << 8) | u8(i + j);
-    return v;
-  }
-};
-
-// 4 bytes starting at byte offset x of a 4-byte-aligned LDS buffer.
-__device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
-  const uint32_t i = x >> 2;
-  return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
-}
-
-// Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
-// store when whole, else conditional whole-dword stores plus at most three bytes at each
-// end (closed-form; a wave pays ~10 stores for its partial lanes, not 16 byte stores).
-__device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t lo, uint32_t hi) {
-  if (lo == 0 && hi == 16) {
-    u32x4 q = {v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<u32x4*>(dst) = q;
-    return;
-  }
-  const uint32_t lo4 = (lo + 3) >> 2, hi4 = hi >> 2;  // whole dwords [lo4, hi4)
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-#pragma unroll
-  for (uint32_t d = 0; d < 4; ++d)
-    if (d >= lo4 && d < hi4) d32[d] = v[d];
-  // head bytes [lo, min(hi, 4 lo4)) and tail bytes [max(lo, 4 hi4), hi); when the range lies
-  // inside one dword both describe the same bytes: only the head copy writes them
-  const uint32_t he = min(hi, 4 * lo4), ts = max(max(lo, 4 * hi4), he);
-  const uint32_t hw = v[min(lo >> 2, 3u)], tw = v[min(hi4, 3u)];
-#pragma unroll
-  for (uint32_t i = 0; i < 3; ++i) {
-    const uint32_t x = lo + i;
-    if (x < he) dst[x] = uint8_t(hw >> (8 * (x & 3)));
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < 3; ++i) {
-    const uint32_t x = ts + i;
-    if (x < hi) dst[x] = uint8_t(tw >> (8 * (x & 3)));
-  }
-}
 
 // ================================================================ decode
 struct DecodeArgs {
@@ -1051,7 +778,16 @@ struct PlanArgs {
   uint64_t* inc;
   uint32_t tag;
   uint32_t poll;
+  const uint64_t* dn;      // optional: n read from device memory (overrides n)
+  const uint32_t* dnseg;   // optional: nseg read from device memory (overrides nseg)
 };
+
+__device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
+  PlanArgs a = a0;
+  if (a.dn) a.n = uni64(*a.dn);
+  if (a.dnseg) a.nseg = uni(*a.dnseg);
+  return a;
+}
 
 constexpr uint32_t kAlcpUnsorted = 0x80000000u;
 constexpr uint32_t kAlcpLcp = 0x7FFFFFFFu;
@@ -1096,7 +832,8 @@ __device__ __forceinline__ uint32_t key_lcp(const PlanKeys& K, uint32_t pp, uint
   return lcp;
 }
 
-__global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a) {
+__global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a0) {
+  const PlanArgs a = resolve(a0);
   const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   uint32_t err = 0;
   const PlanKeys K = plan_keys(a);
@@ -1121,7 +858,8 @@ __global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a) {
 
 constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
 
-__global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a) {
+__global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
+  const PlanArgs a = resolve(a0);
   __shared__ uint32_t crec[4][kWalk], calcp[4][kWalk];
   uint32_t* CR = crec[threadIdx.x >> 6];
   uint32_t* CA = calcp[threadIdx.x >> 6];
@@ -1276,7 +1014,14 @@ struct EmitArgs {
   uint32_t* big_cnt;
   uint32_t skip;  // ablation mask (timing experiments only): 16 entry-lane byte writes,
                   // 32 bulk value copy, 64 flush, 128 LCP
+  const uint64_t* dn;  // optional: n read from device memory (overrides n)
 };
+
+__device__ __forceinline__ EmitArgs resolve(const EmitArgs& a0) {
+  EmitArgs a = a0;
+  if (a.dn) a.n = uni64(*a.dn);
+  return a;
+}
 
 constexpr uint32_t kEmitWaves = 4;
 constexpr uint32_t kEmitKCap = 1088;
@@ -1394,7 +1139,8 @@ struct EmitMeta {
 // metadata, the key/value staging loads and the first 64 entries' offsets/ts of block i+1
 // are already in flight (the wave is latency-bound otherwise: ~3 dependent global round
 // trips per block).  LDS caps occupancy at 3 waves/SIMD, so the prefetch registers are free.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void emit_kernel(EmitArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void emit_kernel(EmitArgs a0) {
+  const EmitArgs a = resolve(a0);
   __shared__ EmitLds lds[kEmitWaves];
   EmitLds& L = lds[threadIdx.x >> 6];
   const uint32_t l = lane_id();
@@ -1671,7 +1417,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
 }
 
 // The blocks emit_kernel listed as beyond its LDS image, one wave per block.
-__global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a) {
+__global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
+  const EmitArgs a = resolve(a0);
   const uint32_t cnt = uni(*a.big_cnt);
   const uint32_t nw = gridDim.x * 4;
   uint32_t err = 0;
@@ -2344,75 +2091,9 @@ __global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
 }
 
 // ================================================================ host side
-struct lsmblk_ctx {
-  int device = 0;
-  std::mutex mu;
-  uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket, [2] emit big-block count
-  uint32_t* dec_agg = nullptr;   // (entries, key bytes, value bytes) per block
-  uint64_t dec_cap = 0;
-  CrcTabs* crc_tabs = nullptr;   // CRC-32 slicing + zero-extension tables (first CRC call)
-  uint64_t* tile_sum = nullptr;  // 3 per 64-block tile
-  uint64_t* tile_pre = nullptr;
-  uint64_t tile_cap = 0;
-  uint64_t* seg_agg = nullptr;   // 2 granules per segment
-  uint64_t* seg_inc = nullptr;
-  uint64_t seg_cap = 0;
-  uint32_t* rec_first = nullptr; // n+1
-  uint32_t* blk_first = nullptr;
-  uint32_t* ent = nullptr;       // 3 per entry: rec, alcp, block sizes (plan passes)
-  uint32_t* big_list = nullptr;  // n+1: blocks for emit_big_kernel
-  uint64_t rec_cap = 0;
-  uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
-  uint32_t poll = 0;             // look-back poll protocol (see gload)
-  uint32_t skip = 0;             // decode ablation mask (timing experiments only)
-  bool timing = false;           // record HIP events around every kernel (diagnostics)
-  hipEvent_t ev[8] = {};         // decode: 0 count 1 scan 2 decode 3 | encode: 4 plan 5 emit 6
-  bool dec_timed = false, enc_timed = false;
-  // BlockMeta sections (lsmblk_block_meta_batch)
-  uint32_t* meta_rec = nullptr;     // nblk
-  uint64_t* meta_pos = nullptr;     // nblk + 1
-  uint64_t meta_blk_cap = 0;
-  uint64_t* meta_tile = nullptr;    // 2 per tile: sums, prefixes
-  uint64_t meta_tile_cap = 0;
-  uint32_t* meta_crc = nullptr;     // nseg
-  uint64_t meta_seg_cap = 0;
-  uint64_t* meta_cstats = nullptr;  // crc_kernel stats of the section CRC pass
-  // compaction filter (lsmblk_compact_filter_batch)
-  uint32_t* filt_keep = nullptr;    // n
-  uint64_t filt_cap = 0;
-  uint64_t* filt_tile = nullptr;    // 6 per tile: sums, prefixes
-  uint64_t filt_tile_cap = 0;
-};
-
 namespace {
 
-// Look-back status granules live in uncached device memory: every poll and publish goes to
-// the coherence point, so no XCD's L2 can hold a stale copy (MI355X L2s are per XCD and not
-// coherent with each other).
-constexpr unsigned kStatusFlags = hipDeviceMallocUncached;
-
-template <typename T>
-int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per, unsigned flags = 0) {
-  if (need <= *cap) return LSMBLK_OK;
-  uint64_t nc = need + need / 4 + 1024;
-  if (*p) {
-    if (hipDeviceSynchronize() != hipSuccess) return LSMBLK_E_HIP;
-    (void)hipFree(*p);
-    *p = nullptr;
-  }
-  const hipError_t e = flags ? hipExtMallocWithFlags(reinterpret_cast<void**>(p), nc * per * sizeof(T), flags)
-                            : hipMalloc(reinterpret_cast<void**>(p), nc * per * sizeof(T));
-  if (e != hipSuccess) {
-    *cap = 0;
-    return LSMBLK_E_NOMEM;
-  }
-  if (hipMemset(*p, 0, nc * per * sizeof(T)) != hipSuccess) return LSMBLK_E_HIP;
-  *cap = nc;
-  return LSMBLK_OK;
-}
-
 int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t segs) {
-  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
   int rc;
   uint64_t cap;
   if (blocks > c->dec_cap) {
@@ -2478,7 +2159,8 @@ int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
   if (!c) return LSMBLK_E_NOMEM;
   c->device = device;
   if (const char* e = getenv("LSMBLK_POLL_MODE")) c->poll = uint32_t(atoi(e));
-  if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->counters, 2048) != hipSuccess) {
+  DeviceGuard dg(device);
+  if (!dg.ok || hipMalloc(&c->counters, 2048) != hipSuccess) {
     delete c;
     return LSMBLK_E_HIP;
   }
@@ -2488,7 +2170,7 @@ int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
 
 void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceGuard dg(c->device);
   (void)hipDeviceSynchronize();
   (void)hipFree(c->counters);
   (void)hipFree(c->dec_agg);
@@ -2508,6 +2190,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->meta_cstats);
   (void)hipFree(c->filt_keep);
   (void)hipFree(c->filt_tile);
+  (void)hipFree(c->cws);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2522,7 +2205,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->skip = value;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->ev[0]) {
-      if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+      DeviceGuard dg(c->device);
+      if (!dg.ok) return LSMBLK_E_HIP;
       for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) return LSMBLK_E_HIP;
     }
@@ -2555,6 +2239,8 @@ int lsmblk_ctx_kernel_times(lsmblk_ctx* c, float* ms) {
 int lsmblk_ctx_reserve(lsmblk_ctx* c, uint64_t max_blocks, uint64_t max_entries, uint64_t max_segments) {
   if (!c) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
   return reserve_locked(c, max_blocks, max_entries, max_segments);
 }
 
@@ -2564,6 +2250,8 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   if (!aligned16(out->keys) || !aligned16(out->vals) || !out->key_off || !out->val_off) return LSMBLK_E_INVAL;
   if (nblk >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc = reserve_locked(c, nblk, 0, 0);
   if (rc) return rc;
@@ -2624,7 +2312,19 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   if (in->n >= 0xFFFFFFFFull || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
   if (block_size == 0) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  return lsmblk_impl::encode_locked(c, in, nullptr, seg_start, nullptr, nseg, block_size, out, out_cap, blk_off,
+                                    blk_cap, stats, reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"
+
+namespace lsmblk_impl {
+int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
+                  const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
+                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st) {
+  // in->n (and nseg) are upper bounds when dn (dnseg) point at the device-side values
   int rc = reserve_locked(c, 0, in->n, nseg);
   if (rc) return rc;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
@@ -2659,6 +2359,8 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   p.inc = c->seg_inc;
   p.tag = c->epoch;
   p.poll = c->poll;
+  p.dn = dn;
+  p.dnseg = dnseg;
   c->enc_timed = c->timing;
   if (c->timing) (void)hipEventRecord(c->ev[4], st);
   if (in->n) {
@@ -2684,6 +2386,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   e.big_list = c->big_list;
   e.big_cnt = c->counters + 2;
   e.skip = c->skip;
+  e.dn = dn;
   if (hipMemsetAsync(e.big_cnt, 0, sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -2697,11 +2400,22 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
+int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
+                          uint32_t* seg_blk, hipStream_t st) {
+  hipLaunchKernelGGL(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg_max) + 256) / 256)), dim3(256), 0, st,
+                     c->blk_first, enc_stats, seg_start, nseg_max, seg_blk);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+}  // namespace lsmblk_impl
+
+extern "C" {
+
 int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                        uint32_t* crc, uint64_t* stats, void* stream) {
   if (!c || !blk_off || !stats || (nblk && !crc)) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
   int rc = ensure_crc_tabs(c);
   if (rc) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -2714,7 +2428,8 @@ int lsmblk_encode_segment_blocks(lsmblk_ctx* c, const uint32_t* seg_start, uint3
                                  uint32_t* seg_blk, void* stream) {
   if (!c || !seg_start || !enc_stats || !seg_blk) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
   if (!c->blk_first) return LSMBLK_E_INVAL;  // no encode ran on this context
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg) + 256) / 256)), dim3(256), 0, st,
@@ -2728,7 +2443,8 @@ int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t
   if (!c || !blk_off || !seg_blk || !meta_off || !stats || !meta || meta_cap < 16) return LSMBLK_E_INVAL;
   if (nseg == 0 || nblk >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
   int rc = ensure_crc_tabs(c);
   if (rc) return rc;
   const uint64_t ntiles = (nblk + kMetaTile - 1) / kMetaTile;
@@ -2784,7 +2500,8 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
   if (nprefix && (!prefixes || !prefix_off)) return LSMBLK_E_INVAL;
   if (in->n >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return LSMBLK_E_HIP;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
   const uint64_t n = in->n, ntiles = (n + kFiltTile - 1) / kFiltTile;
   int rc;
   if ((rc = grow(&c->filt_keep, &c->filt_cap, n + 1, 1))) return rc;
@@ -2843,7 +2560,7 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
   a.nblk = nblk;
   a.tail = tail;
   a.crc = crc;
-  a.tabs = c->crc_tabs;
+  a.tabs = static_cast<const CrcTabs*>(c->crc_tabs);
   a.stats = stats;
   // persistent: as many workgroups as are resident at once (4 KiB tables + 4 x 4 KiB staging)
   int cus = 256, per_cu = 0;

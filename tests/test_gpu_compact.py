@@ -1,0 +1,123 @@
+"""GPU parity of the compaction path (merge, rules, SST rotation, fused pipeline) through the C
+ABI against the oracle: MergeIterator / compact_generate_sst restated line by line
+(oracle/pyref.py) and their C forms (oracle/lsmblk_oracle.c).  Bit-exact bar."""
+import numpy as np
+import pytest
+import torch
+
+from lsm_amd import batch, synth
+from lsm_amd._lib import LSMBLK_E_INVAL, LSMBLK_E_MALFORMED, LsmBlkError
+from oracle import oracle as O
+from oracle import pyref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+def kv_runs(runs):
+    ents = [e for r in runs for e in r]
+    rs = np.zeros(len(runs) + 1, np.uint32)
+    rs[1:] = np.cumsum([len(r) for r in runs])
+    return O.KV.from_entries(ents), rs
+
+
+def to_dev(kv: O.KV):
+    return batch.KVStream.from_numpy(kv.keys, kv.key_off, kv.vals, kv.val_off, kv.ts)
+
+
+def dev_entries(d: batch.KVStream):
+    keys, ko, vals, vo, ts = d.to_numpy()
+    return [(bytes(keys[ko[i]:ko[i + 1]]), int(ts[i]), bytes(vals[vo[i]:vo[i + 1]])) for i in range(d.n)]
+
+
+def assert_kv_equal(d: batch.KVStream, ref: O.KV):
+    keys, ko, vals, vo, ts = d.to_numpy()
+    assert d.n == ref.n
+    np.testing.assert_array_equal(ko, ref.key_off)
+    np.testing.assert_array_equal(vo, ref.val_off)
+    np.testing.assert_array_equal(ts, ref.ts)
+    np.testing.assert_array_equal(keys, ref.keys[:ref.key_off[-1]])
+    np.testing.assert_array_equal(vals, ref.vals[:ref.val_off[-1]])
+
+
+def gpu_merge(runs):
+    kv, rs = kv_runs(runs)
+    return dev_entries(batch.merge_runs(to_dev(kv), rs))
+
+
+def kvs(pairs):
+    return [(k.encode(), 0, v.encode()) for k, v in pairs]
+
+
+def random_runs(rng, nrun, nkeys, max_versions=3, maxlen=6):
+    space = sorted({bytes(rng.integers(97, 100, int(rng.integers(1, maxlen)), dtype=np.uint8)) for _ in range(nkeys)})
+    runs = []
+    for r in range(nrun):
+        take = sorted(rng.choice(len(space), size=int(rng.integers(0, len(space) + 1)), replace=False))
+        run = []
+        for i in take:
+            for t in sorted(rng.choice(1000, size=int(rng.integers(1, max_versions + 1)), replace=False), reverse=True):
+                run.append((space[i], int(t), b"" if rng.random() < 0.2 else b"r%d-%d" % (r, t)))
+        runs.append(run)
+    return runs
+
+
+# ---------------------------------------------------------------- merge
+def test_merge_week1_day2_fixtures():
+    i1 = kvs([("a", "1.1"), ("b", "2.1"), ("c", "3.1"), ("e", "")])
+    i2 = kvs([("a", "1.2"), ("b", "2.2"), ("c", "3.2"), ("d", "4.2")])
+    i3 = kvs([("b", "2.3"), ("c", "3.3"), ("d", "4.3")])
+    assert gpu_merge([i1, i2, i3]) == kvs([("a", "1.1"), ("b", "2.1"), ("c", "3.1"), ("d", "4.2"), ("e", "")])
+    assert gpu_merge([i3, i1, i2]) == kvs([("a", "1.1"), ("b", "2.3"), ("c", "3.3"), ("d", "4.3"), ("e", "")])
+    j1 = kvs([("a", "1.1"), ("b", "2.1"), ("c", "3.1")])
+    j2 = kvs([("d", "1.2"), ("e", "2.2"), ("f", "3.2"), ("g", "4.2")])
+    j3 = kvs([("h", "1.3"), ("i", "2.3"), ("j", "3.3"), ("k", "4.3")])
+    assert gpu_merge([j2, [], j3, j1]) == j1 + j2 + j3
+    assert gpu_merge([j1, []]) == j1
+    assert gpu_merge([[], []]) == []
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_merge_random_runs_vs_heap_restatement(seed):
+    rng = np.random.default_rng(seed)
+    runs = random_runs(rng, int(rng.integers(1, 12)), int(rng.integers(1, 400)), maxlen=8)
+    assert gpu_merge(runs) == pyref.merge_runs(runs)
+
+
+@pytest.mark.parametrize("nrun,versions", [(8, 1), (5, 3), (64, 1), (1, 2)])
+def test_merge_synthetic_runs_vs_c_oracle(nrun, versions):
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(60000 // versions, nrun=nrun, seed=nrun, versions=versions)
+    kv = O.KV(keys, ko, vals, vo, ts)
+    src = O.merge_runs(kv, rs)
+    assert_kv_equal(batch.merge_runs(to_dev(kv), rs), O.gather(kv, src))
+
+
+def test_merge_big_tiles_global_path():
+    """Tiles beyond the LDS tables: one key with thousands of versions in several runs, long
+    keys (> the LDS key image), many short runs."""
+    rng = np.random.default_rng(3)
+    hot = b"hot-key"
+    runs = []
+    for r in range(6):
+        run = [(b"a%05d" % i, 5, b"v") for i in sorted(rng.choice(3000, 200, replace=False))]
+        run += [(hot, int(t), b"h%d" % r) for t in range(3000 - r, 0, -1)]
+        run += [(b"z" * 300 + b"%04d" % i, 1, b"w") for i in sorted(rng.choice(2000, 150, replace=False))]
+        runs.append(run)
+    assert gpu_merge(runs) == pyref.merge_runs_rule(runs)
+
+
+def test_merge_errors():
+    kv, rs = kv_runs([kvs([("a", "1")]), kvs([("b", "2")])])
+    d = to_dev(kv)
+    with pytest.raises(LsmBlkError) as e:
+        batch.merge_runs(d, np.array([0, 2, 1], np.uint32))  # decreasing run table
+    assert e.value.status == LSMBLK_E_INVAL
+    bad, rs = kv_runs([kvs([("b", "1"), ("a", "2")]), kvs([("c", "3")])])  # an unsorted run
+    with pytest.raises(LsmBlkError) as e:
+        batch.merge_runs(to_dev(bad), rs)
+    assert e.value.status == LSMBLK_E_MALFORMED
