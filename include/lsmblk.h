@@ -249,6 +249,48 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uin
 int lsmblk_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                        const lsmblk_kv_stream* out, uint64_t* stats, void* stream);
 
+/* SST rotation of compact_generate_sst (src/compact.rs:278-289) over `in`, the stream of entries
+ * handed to SsTableBuilder::add (one key's versions newest first): a new SST starts before entry e
+ * when the open SST's estimate_size() -- its finished blocks plus a 4-byte CRC each
+ * (src/table/builder.rs:105-123) -- is >= target_sst_size and key(e) differs from key(e-1).  The
+ * blocks are BlockBuilder's greedy packing of block_size restarted at every SST start, so this
+ * is exactly the segment table under which lsmblk_encode_batch reproduces the compaction's SSTs.
+ * sst_start (device u32[sst_cap]) receives the nsst SST first entries and then in->n.  stats: [0]
+ * nsst [3] error flags (CAPACITY: sst_cap < nsst + 1).  Asynchronous. */
+int lsmblk_sst_rotation_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uint32_t block_size,
+                              uint64_t target_sst_size, uint32_t* sst_start, uint32_t sst_cap, uint64_t* stats,
+                              void* stream);
+
+/* Options of lsmblk_compact_batch: the compaction rules (src/compact.rs:239-276) and the SST
+ * layout (LsmStorageOptions::block_size / target_sst_size, src/lsm_storage.rs:68-94). */
+typedef struct {
+  uint64_t watermark;          /* LsmMvccInner::watermark() */
+  int32_t bottom_level;        /* compact_to_bottom_level: drop tombstones at or below the watermark */
+  uint32_t nprefix;            /* CompactionFilter::Prefix filters (device memory) */
+  const uint8_t* prefixes;
+  const uint32_t* prefix_off;  /* u32[nprefix+1] */
+  uint32_t block_size;
+  uint64_t target_sst_size;
+} lsmblk_compact_opts;
+
+#define LSMBLK_COMPACT_STATS_WORDS 8
+/* compact_generate_sst (src/compact.rs:223-311) on the device for sorted runs already decoded
+ * into `in` (run_start as for lsmblk_merge_batch): MergeIterator merge -> keep/drop rules -> SST
+ * rotation -> SsTableBuilder block packing.  `kept` receives the entries handed to
+ * SsTableBuilder::add (capacities as for decode); the blocks of every SST are written packed to
+ * `out` (16-byte aligned) with blk_off (u64[blk_cap], nblk+1 values), as lsmblk_encode_batch writes
+ * them; sst_start / sst_blk (u32[sst_cap], sst_cap >= 2) receive each SST's first kept entry / first
+ * block, then kept count / nblk.  Per-block CRCs and BlockMeta sections follow from
+ * lsmblk_crc32_batch / lsmblk_block_meta_batch with seg_blk = sst_blk.  When nothing is kept the
+ * result is zero SSTs (the reference panics building an empty SST).  stats (u64[8]): [0] blocks
+ * [1] bytes [2] SSTs [3] error flags [4] merged entries [5] kept entries [6] kept key bytes
+ * [7] kept value bytes.  Asynchronous; allocates workspace on the context (~45 B per input entry
+ * plus 8 B per entry per rotation level). */
+int lsmblk_compact_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                         const lsmblk_compact_opts* opts, const lsmblk_kv_stream* kept, uint8_t* out,
+                         uint64_t out_cap, uint64_t* blk_off, uint64_t blk_cap, uint32_t* sst_start,
+                         uint32_t* sst_blk, uint32_t sst_cap, uint64_t* stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

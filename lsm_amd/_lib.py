@@ -36,6 +36,11 @@ class KVStreamC(ctypes.Structure):
                 ("n", U64), ("entry_cap", U64), ("key_cap", U64), ("val_cap", U64)]
 
 
+class CompactOptsC(ctypes.Structure):
+    _fields_ = [("watermark", U64), ("bottom_level", ctypes.c_int32), ("nprefix", U32), ("prefixes", P),
+                ("prefix_off", P), ("block_size", U32), ("target_sst_size", U64)]
+
+
 # (name, restype, argtypes) for every symbol of include/lsmblk.h
 SIGNATURES = [
     ("lsmblk_abi_version", I, []),
@@ -76,6 +81,9 @@ SIGNATURES = [
     ("lsmblk_compact_filter_batch", I, [P, ctypes.POINTER(KVStreamC), U64, I, P, P, U32,
                                         ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_merge_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_sst_rotation_batch", I, [P, ctypes.POINTER(KVStreamC), U32, U64, P, U32, P, P]),
+    ("lsmblk_compact_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
+                                 ctypes.POINTER(KVStreamC), P, U64, P, U64, P, P, U32, P, P]),
 ]
 
 

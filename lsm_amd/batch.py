@@ -22,7 +22,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ._lib import KVStreamC, LSMBLK_E_CAPACITY, LsmBlkError, check, lib
+from ._lib import CompactOptsC, KVStreamC, LSMBLK_E_CAPACITY, LsmBlkError, check, lib
 
 STATS_WORDS = 4
 _ctx_lock = threading.Lock()
@@ -425,3 +425,85 @@ def merge_runs(kv: KVStream, run_start, stream=None) -> KVStream:
         raise LsmBlkError(st, "merge_runs")
     out.n = int(stats[0].item())
     return out
+
+
+def sst_rotation(kv: KVStream, block_size: int, target_sst_size: int, stream=None):
+    """SST cut points of compact_generate_sst (reference src/compact.rs:278-289) over the stream
+    handed to SsTableBuilder::add -> u32 numpy array of SST first entries, then kv.n."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    kv.check(dev.index, "kv")
+    cap = kv.n + 2
+    starts = torch.zeros(cap, dtype=torch.int32, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    c = kv._c()
+    check(lib().lsmblk_sst_rotation_batch(_ctx(dev.index, stream), ctypes.byref(c), block_size, target_sst_size,
+                                          starts.data_ptr(), cap, stats.data_ptr(), _stream_ptr(stream, dev.index)),
+          "lsmblk_sst_rotation_batch")
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "sst_rotation")
+    ns = int(stats[0].item())
+    return starts[:ns + 1].cpu().numpy().view(np.uint32)
+
+
+class CompactBuffers:
+    """Preallocated outputs of lsmblk_compact_batch for an input of n entries / K key bytes /
+    V value bytes (worst case: every entry kept, every entry its own block and SST)."""
+
+    def __init__(self, n, key_bytes, val_bytes, device, sst_cap=None):
+        self.kept = KVStream.empty(n, key_bytes, val_bytes, device)
+        self.out_cap = key_bytes + val_bytes + 18 * n + 16
+        self.out = _aligned_empty(self.out_cap, device)
+        self.blk_cap = n + 2
+        self.blk_off = torch.zeros(self.blk_cap, dtype=torch.int64, device=device)
+        self.sst_cap = sst_cap or (n + 2)
+        self.sst_start = torch.zeros(self.sst_cap, dtype=torch.int32, device=device)
+        self.sst_blk = torch.zeros(self.sst_cap, dtype=torch.int32, device=device)
+        self.stats = torch.zeros(8, dtype=torch.int64, device=device)
+
+
+def compact_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, buf: CompactBuffers, stream=None,
+                 _keep=None):
+    """Asynchronous lsmblk_compact_batch into preallocated buffers (no host sync)."""
+    dev = _dev_index(run_start)
+    kv.check(dev, "kv")
+    _need(run_start, torch.int32, "run_start", dev, nrun + 1)
+    pfx, pfo = opts["_pfx"]
+    o = CompactOptsC(opts.get("watermark", 0), int(bool(opts.get("bottom_level", False))), opts["_npfx"],
+                     pfx.data_ptr(), pfo.data_ptr(), opts["block_size"], opts["target_sst_size"])
+    ci, ck = kv._c(), buf.kept._c(*buf.kept.caps())
+    check(lib().lsmblk_compact_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun, ctypes.byref(o),
+                                     ctypes.byref(ck), buf.out.data_ptr(), buf.out_cap, buf.blk_off.data_ptr(),
+                                     buf.blk_cap, buf.sst_start.data_ptr(), buf.sst_blk.data_ptr(), buf.sst_cap,
+                                     buf.stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_compact_batch")
+
+
+def compact_opts(watermark=0, bottom_level=False, prefixes=(), block_size=4096, target_sst_size=2 << 20,
+                 device="cuda"):
+    """Options of lsmblk_compact_batch (prefix tables staged on the device once)."""
+    return dict(watermark=watermark, bottom_level=bottom_level, block_size=block_size,
+                target_sst_size=target_sst_size, _pfx=_prefix_tables(prefixes, torch.device(device)),
+                _npfx=len(prefixes))
+
+
+def compact_runs(kv: KVStream, run_start, watermark=0, bottom_level=False, prefixes=(), block_size=4096,
+                 target_sst_size=2 << 20, stream=None):
+    """compact_generate_sst (reference src/compact.rs:223-311) on the device over the sorted runs
+    of kv (run 0 = highest priority): MergeIterator merge, keep/drop rules, SST rotation, block
+    packing.  Returns dict(kept KVStream, blocks, blk_off, sst_start, sst_blk, stats)."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    rs = _u32_table(run_start, dev)
+    kb, vb = kv.byte_sizes()
+    buf = CompactBuffers(kv.n, kb, vb, dev)
+    opts = compact_opts(watermark, bottom_level, prefixes, block_size, target_sst_size, dev)
+    compact_into(kv, rs, rs.numel() - 1, opts, buf, stream)
+    torch.cuda.synchronize(dev)
+    st = _status(buf.stats)
+    if st:
+        raise LsmBlkError(st, "compact_runs")
+    s = buf.stats.cpu().tolist()
+    nblk, nbytes, nsst = s[0], s[1], s[2]
+    buf.kept.n = s[5]
+    return dict(kept=buf.kept, blocks=buf.out[:nbytes], blk_off=buf.blk_off[:nblk + 1],
+                sst_start=buf.sst_start[:nsst + 1], sst_blk=buf.sst_blk[:nsst + 1], stats=s)

@@ -647,11 +647,253 @@ __global__ void merge_empty_kernel(uint64_t* mstats, uint32_t* okey_off, uint32_
   }
 }
 
+// ---------------------------------------------------------------- SST rotation
+// compact_generate_sst starts a new SST before adding entry e when the open SsTableBuilder's
+// estimate_size() >= target_sst_size and key(e) differs from the last key (src/compact.rs:278-289).
+// estimate_size() is data.len(): the finished blocks plus their 4-byte CRCs
+// (src/table/builder.rs:105-123), so it grows only when a block is finished -- while adding the
+// first entry of the next block.  With blocks j = [s_j, s_{j+1}) of an SST starting at g and
+// D_j = sum over i < j of (size_i + 4), the check at entry e in (s_j, s_{j+1}] sees D_j; the SST
+// therefore ends at F(g) = the first key change after s_{j*}, j* = min{ j : D_j >= target }.
+// F depends on the greedy packing from g only, so it is computed for EVERY entry g in
+// parallel, by pointer doubling over nxt(s) = the greedy end of a block starting at s:
+//   rot_adj_kernel     rec = klen + vlen, alcp = LCP with the predecessor (+ unsorted / same-key
+//                      bits), as plan_adj_kernel
+//   rot_next_kernel    J0[s] = nxt(s), S0[s] = size of block [s, nxt(s)) + 4 (LCP against the
+//                      block's first key = running min of alcp for sorted keys, direct
+//                      compares after an unsorted pair; BlockBuilder::add's reject rule)
+//   rot_double_kernel  J_k = J_{k-1} o J_{k-1}, S_k = S_{k-1} + S_{k-1} o J_{k-1} (until every
+//                      chain reaches the target or the end)
+//   rot_f_kernel       F(g) by binary lifting over the levels, then the next key change
+//   rot_chain_kernel   the SST chain 0, F(0), F(F(0)), ... by doubling F (level k appends
+//                      chain elements [2^k, 2^(k+1)) and squares F)
+//   rot_finish_kernel  sst_start[] and the SST count.
+// The kept stream's versions of a key must be newest first (as MergeIterator yields SST data);
+// then "same as last key" is "same key as the previous kept entry" (DESIGN.md).
+constexpr uint32_t kRotSame = 0x40000000u;      // alcp bit: key equals the predecessor's
+constexpr uint32_t kRotUnsorted = 0x80000000u;  // alcp bit: predecessor's key is greater
+constexpr uint32_t kRotLcp = 0x3FFFFFFFu;
+constexpr uint32_t kRotMaxLevels = 32;
+
+struct RotArgs {
+  const uint8_t* keys;
+  const uint32_t* key_off;
+  const uint32_t* val_off;
+  const uint64_t* dn;       // device: entries of the stream
+  uint64_t n_max;           // grid bound
+  uint32_t block_size;
+  uint64_t target;
+  uint32_t* rec;            // n_max + 1
+  uint32_t* alcp;           // n_max + 1
+  uint32_t* J;              // levels x (n_max + 1)
+  uint32_t* S;              // levels x (n_max + 1)
+  uint32_t levels;          // levels allocated for J / S
+  uint32_t* F0;             // n_max + 1: F, then the doubling ping-pong
+  uint32_t* F1;
+  uint32_t* need;           // kRotMaxLevels: level k still has a chain short of target and end
+  uint32_t* chain_end;      // [0] set once the SST chain reached the end
+  uint32_t* starts;         // sst_cap: SST start entries (the chain), then n
+  uint32_t sst_cap;
+  uint32_t* nsst;           // device: SST count handed to the encode (0 after an error)
+  uint64_t* stats;          // [0] SSTs [3] error flags
+};
+
+__device__ __forceinline__ uint64_t rot_n(const RotArgs& a) { return uni64(*a.dn); }
+
+// LCP of keys (pp, pl) and (kp, kl) through the descriptor; *less = key p < key k (byte order)
+__device__ __forceinline__ uint32_t glcp(const GKeys& K, uint32_t pp, uint32_t pl, uint32_t kp, uint32_t kl,
+                                         int* order) {
+  const uint32_t m = pl < kl ? pl : kl;
+  for (uint32_t i = 0; i < m; i += 4) {
+    uint32_t x = K.dw(pp + i), y = K.dw(kp + i);
+    if (m - i < 4) {
+      const uint32_t mk = (1u << (8 * (m - i))) - 1;
+      x &= mk;
+      y &= mk;
+    }
+    if (x != y) {
+      const uint32_t z = __builtin_ctz(x ^ y) & ~7u;
+      if (order) *order = ((x >> z) & 0xFF) < ((y >> z) & 0xFF) ? -1 : 1;
+      return i + (z >> 3);
+    }
+  }
+  if (order) *order = pl < kl ? -1 : (pl > kl ? 1 : 0);
+  return m;
+}
+
+__global__ __launch_bounds__(256) void rot_adj_kernel(RotArgs a) {
+  const uint64_t n = rot_n(a);
+  const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
+  a.rec[e] = kl + (a.val_off[e + 1] - a.val_off[e]);
+  uint32_t al = 0;
+  if (e > 0) {
+    const GKeys K = gkeys(a.keys, a.key_off[n]);
+    const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
+    int ord = 0;
+    const uint32_t lcp = glcp(K, pp, pl, kp, kl, &ord);
+    al = (lcp < kRotLcp ? lcp : kRotLcp) | (ord > 0 ? kRotUnsorted : 0u) | (ord == 0 ? kRotSame : 0u);
+  }
+  a.alcp[e] = al;
+}
+
+__device__ __forceinline__ void or_need(uint32_t* flag, bool v) {
+  if (__ballot(v) && lane_id() == 0) atomicOr(flag, 1u);
+}
+
+__global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
+  const uint64_t n = rot_n(a);
+  const uint64_t s = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  bool short_chain = false;
+  if (s < n) {
+    const uint64_t bs = a.block_size;
+    uint64_t before = 2 + uint64_t(a.rec[s]) + 16;  // entry s always accepted, prefix 0
+    uint32_t pmin = kRotLcp;
+    bool direct = false;
+    uint32_t sp = 0, sl = 0;
+    GKeys K;
+    uint64_t e = s + 1;
+    for (; e < n; ++e) {
+      const uint32_t r = a.rec[e], al = a.alcp[e];
+      if (before + r + 14 > bs) break;  // BlockBuilder::add rejects (builder.rs:56-60)
+      uint32_t p;
+      if (!direct && (al & kRotUnsorted)) {  // LCP vs the first key directly from here on
+        direct = true;
+        K = gkeys(a.keys, a.key_off[n]);
+        sp = a.key_off[s];
+        sl = a.key_off[s + 1] - sp;
+      }
+      if (!direct) {
+        pmin = min(pmin, al & kRotLcp);
+        p = pmin;
+      } else {
+        const uint32_t kp = a.key_off[e];
+        p = glcp(K, sp, sl, kp, a.key_off[e + 1] - kp, nullptr);
+      }
+      before += uint64_t(r) + 16 - p;
+    }
+    const uint64_t sz = before + 4;
+    a.J[s] = uint32_t(e);
+    a.S[s] = sz > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(sz);
+    short_chain = e < n && sz < a.target;
+  } else if (s == n) {
+    a.J[s] = uint32_t(n);
+    a.S[s] = 0;
+  }
+  or_need(a.need + 0, short_chain);
+}
+
+__global__ __launch_bounds__(256) void rot_double_kernel(RotArgs a, uint32_t k) {
+  if (!*(volatile uint32_t*)(a.need + k - 1)) return;  // every chain done one level down
+  const uint64_t n = rot_n(a);
+  const uint64_t s = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t N1 = a.n_max + 1;
+  bool short_chain = false;
+  if (s <= n) {
+    const uint32_t* J0 = a.J + (k - 1) * N1;
+    const uint32_t* S0 = a.S + (k - 1) * N1;
+    const uint32_t j = J0[s];
+    const uint32_t jj = J0[j];
+    const uint64_t ss = uint64_t(S0[s]) + S0[j];
+    a.J[k * N1 + s] = jj;
+    a.S[k * N1 + s] = ss > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(ss);
+    short_chain = jj < n && ss < a.target;
+  }
+  or_need(a.need + k, short_chain);
+}
+
+__global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
+  const uint64_t n = rot_n(a);
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (g > n) return;
+  if (g == n) {
+    a.F0[g] = uint32_t(n);
+    return;
+  }
+  const uint64_t N1 = a.n_max + 1;
+  uint32_t kc = 1;  // levels computed: 0 .. kc-1
+  while (kc < a.levels && a.need[kc - 1]) ++kc;
+  uint64_t pos = g, acc = 0;
+  const uint32_t top = kc - 1;
+  // lifting: the longest chain prefix from g whose data stays below the target
+  while (pos < n && acc + a.S[top * N1 + pos] < a.target) {
+    acc += a.S[top * N1 + pos];
+    pos = a.J[top * N1 + pos];
+  }
+  for (int k = int(top) - 1; k >= 0; --k) {
+    if (pos < n && acc + a.S[uint64_t(k) * N1 + pos] < a.target) {
+      acc += a.S[uint64_t(k) * N1 + pos];
+      pos = a.J[uint64_t(k) * N1 + pos];
+    }
+  }
+  uint64_t f = n;
+  if (pos < n) {
+    const uint64_t sj = a.J[pos];  // s_{j*}: the first block start whose entries see D >= target
+    if (sj < n) {
+      f = sj + 1;
+      while (f < n && (a.alcp[f] & kRotSame)) ++f;  // the first key change after it
+    }
+  }
+  a.F0[g] = uint32_t(f);
+}
+
+// Level k: chain elements [2^k, 2^(k+1)) from [0, 2^k) through F^(2^k) (= cur), then
+// nxt = cur o cur.  Skipped once the chain has reached the end.
+__global__ __launch_bounds__(256) void rot_chain_kernel(RotArgs a, uint32_t k, const uint32_t* cur, uint32_t* nxt) {
+  if (*(volatile uint32_t*)a.chain_end) return;
+  const uint64_t n = rot_n(a);
+  const uint64_t s = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t h = 1ull << k;
+  if (s < h && h + s < a.sst_cap) {
+    const uint32_t c = a.starts[s];
+    a.starts[h + s] = c < n ? cur[c] : uint32_t(n);
+  }
+  if (s <= n) nxt[s] = cur[cur[s]];
+}
+
+// After each level: has the last chain element computed so far reached the end?
+__global__ void rot_chain_check_kernel(RotArgs a, uint32_t k) {
+  if (threadIdx.x || *(volatile uint32_t*)a.chain_end) return;
+  const uint64_t n = rot_n(a);
+  const uint64_t last = (2ull << k) - 1;  // elements [0, 2^(k+1)) are computed now
+  // the array is full (rot_finish_kernel then decides whether the chain ended) or it ended
+  if (last >= a.sst_cap || a.starts[last] >= n) *a.chain_end = k + 1;
+}
+
+__global__ __launch_bounds__(256) void rot_finish_kernel(RotArgs a) {
+  const uint64_t n = rot_n(a);
+  __shared__ uint32_t s_ns;
+  if (threadIdx.x == 0) {
+    // SST count: the computed chain elements below n (increasing, then n), by binary search
+    const uint32_t done = *a.chain_end;
+    uint32_t lo = 0, hi = done ? uint32_t(min<uint64_t>(a.sst_cap, 1ull << done)) : 1u;
+    if (n == 0) {
+      hi = 0;
+    } else {
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.starts[mid] < n) lo = mid + 1;
+        else hi = mid;
+      }
+    }
+    s_ns = lo;
+    uint32_t err = 0;
+    if (uint64_t(lo) + 1 > a.sst_cap) err |= LSMBLK_ERR_CAPACITY;  // the chain did not end in the array
+    a.stats[0] = lo;
+    *a.nsst = err ? 0u : lo;
+    if (err) atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)err);
+  }
+  __syncthreads();
+  for (uint32_t i = s_ns + threadIdx.x; i < a.sst_cap; i += 256) a.starts[i] = uint32_t(n);
+}
+
 // ---------------------------------------------------------------- host side
 // Carve the context's compaction arena (grown on demand, which synchronizes).
 struct Carve {
   uint8_t* base;
   uint64_t off = 0;
+  Carve(uint8_t* b, uint64_t o = 0) : base(b), off(o) {}
   template <typename T>
   T* take(uint64_t count) {
     T* p = reinterpret_cast<T*>(base + off);
@@ -762,6 +1004,90 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
+__global__ void set_u64_kernel(uint64_t* p, uint64_t v) {
+  if (threadIdx.x == 0) *p = v;
+}
+
+// The kept-entry count the rotation and the encode see: 0 after any merge / rules error.
+__global__ void gate_kernel(const uint64_t* fst, uint64_t* dn) {
+  if (threadIdx.x == 0) *dn = fst[3] ? 0ull : fst[0];
+}
+
+uint32_t rot_levels(uint64_t target) {
+  // a block and its CRC take >= 23 bytes (4 + 1 + 8 + 2 + 2 + 2 + 4), so an SST reaches the
+  // target within ceil(target / 23) blocks: 2^(levels-1) hops cover it
+  const uint64_t j = target / 23 + 2;
+  uint32_t k = 1;
+  while (k < kRotMaxLevels && (1ull << (k - 1)) < j) ++k;
+  return k;
+}
+
+struct RotPlan {
+  RotArgs r;
+  uint64_t* dn;     // device n for the rotation
+  uint64_t bytes;
+};
+
+RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target) {
+  RotPlan P{};
+  Carve cv{base, off};
+  const uint64_t N1 = n_max + 1;
+  const uint32_t L = rot_levels(target);
+  P.r.n_max = n_max;
+  P.r.target = target;
+  P.r.levels = L;
+  P.r.rec = cv.take<uint32_t>(N1);
+  P.r.alcp = cv.take<uint32_t>(N1);
+  P.r.J = cv.take<uint32_t>(N1 * L);
+  P.r.S = cv.take<uint32_t>(N1 * L);
+  P.r.F0 = cv.take<uint32_t>(N1);
+  P.r.F1 = cv.take<uint32_t>(N1);
+  P.r.need = cv.take<uint32_t>(kRotMaxLevels + 2);
+  P.r.chain_end = P.r.need + kRotMaxLevels;
+  P.r.nsst = P.r.need + kRotMaxLevels + 1;
+  P.dn = cv.take<uint64_t>(2);
+  P.bytes = cv.off;
+  return P;
+}
+
+// SST cut points of the stream (keys, key_off, val_off; *dn entries, <= n_max) into starts[]
+int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
+  (void)c;
+  if (hipMemsetAsync(r.need, 0, (kRotMaxLevels + 2) * sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipMemsetAsync(r.starts, 0, sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
+  const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
+  hipLaunchKernelGGL(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
+  hipLaunchKernelGGL(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
+  for (uint32_t k = 1; k < r.levels; ++k) hipLaunchKernelGGL(rot_double_kernel, dim3(g), dim3(256), 0, st, r, k);
+  hipLaunchKernelGGL(rot_f_kernel, dim3(g), dim3(256), 0, st, r);
+  uint32_t* cur = r.F0;
+  uint32_t* nxt = r.F1;
+  for (uint32_t k = 0; k < 32 && (1ull << k) < r.sst_cap; ++k) {
+    hipLaunchKernelGGL(rot_chain_kernel, dim3(g), dim3(256), 0, st, r, k, cur, nxt);
+    hipLaunchKernelGGL(rot_chain_check_kernel, dim3(1), dim3(64), 0, st, r, k);
+    uint32_t* t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  hipLaunchKernelGGL(rot_finish_kernel, dim3(1), dim3(256), 0, st, r);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+// Final stats of lsmblk_compact_batch from the stage stats.
+__global__ void compact_stats_kernel(uint64_t* stats, const uint64_t* fst, const uint64_t* rst, const uint64_t* est,
+                                     const uint64_t* mst) {
+  if (threadIdx.x) return;
+  const uint64_t err = fst[3] | rst[3] | est[3];
+  stats[0] = err ? 0 : est[0];
+  stats[1] = err ? 0 : est[1];
+  stats[2] = rst[0];
+  stats[3] = err;
+  stats[4] = mst[0];
+  stats[5] = fst[0];
+  stats[6] = fst[1];
+  stats[7] = fst[2];
+}
+
 int check_merge_args(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                      const lsmblk_kv_stream* out, const uint64_t* stats) {
   if (!c || !in || !run_start || !out || !stats || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
@@ -783,6 +1109,84 @@ int lsmblk_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t
   if (!dg.ok) return LSMBLK_E_HIP;
   return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, out, stats,
                              reinterpret_cast<hipStream_t>(stream), nullptr);
+}
+
+int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_t block_size,
+                              uint64_t target_sst_size, uint32_t* sst_start, uint32_t sst_cap, uint64_t* stats,
+                              void* stream) {
+  if (!c || !in || !sst_start || !stats || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
+  if (block_size == 0 || target_sst_size == 0 || sst_cap == 0 || in->n >= 0xFFFFFFF0ull) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  RotPlan P = plan_rot(nullptr, 0, in->n, target_sst_size);
+  int rc = ensure_ws(c, P.bytes);
+  if (rc) return rc;
+  P = plan_rot(c->cws, 0, in->n, target_sst_size);
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  hipLaunchKernelGGL(set_u64_kernel, dim3(1), dim3(64), 0, st, P.dn, uint64_t(in->n));
+  RotArgs r = P.r;
+  r.keys = in->keys;
+  r.key_off = in->key_off;
+  r.val_off = in->val_off;
+  r.dn = P.dn;
+  r.block_size = block_size;
+  r.starts = sst_start;
+  r.sst_cap = sst_cap;
+  r.stats = stats;
+  return rotation_locked(c, r, st);
+}
+
+int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                         const lsmblk_compact_opts* o, const lsmblk_kv_stream* kept, uint8_t* out, uint64_t out_cap,
+                         uint64_t* blk_off, uint64_t blk_cap, uint32_t* sst_start, uint32_t* sst_blk, uint32_t sst_cap,
+                         uint64_t* stats, void* stream) {
+  int rc = check_merge_args(c, in, run_start, nrun, kept, stats);
+  if (rc) return rc;
+  if (!o || !out || !blk_off || !sst_start || !sst_blk || sst_cap < 2 || blk_cap == 0) return LSMBLK_E_INVAL;
+  if (o->block_size == 0 || o->target_sst_size == 0 || (o->nprefix && (!o->prefixes || !o->prefix_off)))
+    return LSMBLK_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t n = in->n;
+  // workspace: merge + gather, then rotation, then the stage stats
+  MergePlan M = plan_merge(nullptr, n, nrun);
+  RotPlan R = plan_rot(nullptr, M.bytes, n, o->target_sst_size);
+  const uint64_t stats_off = (R.bytes + 255) & ~uint64_t(255);
+  if ((rc = ensure_ws(c, stats_off + 4 * 64))) return rc;
+  uint64_t* sts = reinterpret_cast<uint64_t*>(c->cws + stats_off);
+  uint64_t *fst = sts, *rst = sts + 8, *est = sts + 16;
+  if (hipMemsetAsync(sts, 0, 4 * 64, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipMemsetAsync(stats, 0, LSMBLK_COMPACT_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  MergePlan MP{};
+  if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
+                                o->nprefix, kept, fst, st, &MP)))
+    return rc;
+  R = plan_rot(c->cws, M.bytes, n, o->target_sst_size);
+  hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
+  RotArgs r = R.r;
+  r.keys = kept->keys;
+  r.key_off = kept->key_off;
+  r.val_off = kept->val_off;
+  r.dn = R.dn;  // kept entries (0 after a merge / rules error)
+  r.block_size = o->block_size;
+  r.starts = sst_start;
+  r.sst_cap = sst_cap;
+  r.stats = rst;
+  if ((rc = rotation_locked(c, r, st))) return rc;
+  lsmblk_kv_stream ks = *kept;
+  ks.n = n;  // bound; the encode reads the kept count from fst[0]
+  if ((rc = lsmblk_impl::encode_locked(c, &ks, R.dn, sst_start, r.nsst, sst_cap - 1, o->block_size, out, out_cap,
+                                       blk_off, blk_cap, est, st)))
+    return rc;
+  if ((rc = lsmblk_impl::segment_blocks_locked(c, sst_start, sst_cap - 1, est, sst_blk, st))) return rc;
+  hipLaunchKernelGGL(compact_stats_kernel, dim3(1), dim3(64), 0, st, stats, fst, rst, est, MP.m.mstats);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
 }  // extern "C"
