@@ -3,22 +3,34 @@
 One step = decode the whole resident batch of encoded blocks into the SoA KV stream, then
 re-encode that stream into blocks from the segment (SST) starts alone (the anti-shortcut
 rule of SURVEY.md section 8(d)): the reference's Block::decode + BlockIterator walk
-followed by SsTableBuilder::add / BlockBuilder over every SST.  The re-encoded bytes are
-checked equal to the input after the timed region.
+followed by SsTableBuilder::add / BlockBuilder over every SST.  After the timed region the
+re-encoded bytes are checked equal to the input, and the whole batch is checked against the
+C oracle (oracle/lsmblk_oracle.c): oracle encode of the synthetic KV == the input blocks,
+oracle decode == the GPU decode, oracle re-encode == the GPU re-encode (oracle_checked_blocks).
 
 Default workload (configs[1]): 1,048,576 x 4 KiB blocks per GPU, uniform sorted 16-B keys,
-100-B values, 40-bit ts, 2 MiB segments.  --config Z / M select the other single-GPU configs.
+100-B values, 40-bit ts, 2 MiB segments.  --config Z / M / C select the other configs:
+  Z  Zipf shared-prefix keys, 4 KiB blocks (configs[2])
+  M  8 B - 4 KiB values, 64 KiB blocks (configs[3])
+  C  compaction-shaped (configs[4] at one-GPU scale): 8 overlapping sorted runs of 2 MiB SSTs,
+     one step = decode every input block + MergeIterator merge + compaction rules + SST
+     rotation + block packing (lsmblk_compact_batch), checked against compact_generate_sst
+With N=1 and the default config, Z, M and C also run (fewer steps) and are reported under
+"extra_configs".
 
-  python bench.py --gpus N --steps K --warmup W          (N>1: torchrun, one rank per GPU)
+  python bench.py --gpus N --steps K --warmup W
 
-Prints ONE JSON line on rank 0.  `value` = encoded-block GiB processed per second by all
-ranks (weak scaling: every rank owns its own 1 Mi blocks; no collective on the data path,
-only the timing barrier / max-reduce).
+N>1: started by torchrun (RANK/WORLD_SIZE/LOCAL_RANK in the environment), or, without those,
+this script starts the N rank processes itself (the parent never touches a GPU).  Prints ONE
+JSON line on rank 0.  `value` = encoded-block GiB processed per second by all ranks (weak
+scaling: every rank owns its own batch; no collective on the data path, only the timing
+barrier / max-reduce).
 """
 import argparse
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -40,24 +52,56 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="U", choices=["U", "Z", "M"])
-    p.add_argument("--blocks", type=int, default=None, help="blocks per GPU (default 1 Mi for U/Z, 64 Ki for M)")
+    p.add_argument("--config", default="U", choices=["U", "Z", "M", "C"])
+    p.add_argument("--blocks", type=int, default=None, help="blocks per GPU (default 1 Mi for U/Z/C, 64 Ki for M)")
     p.add_argument("--segment-bytes", type=int, default=2 << 20)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="skip the Z / M / C extra configs at N=1")
+    p.add_argument("--no-oracle-check", action="store_true")
     p.add_argument("--pcie", action="store_true", help="also time the H2D+D2H-inclusive rate (DESIGN.md)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher self-test: ranks join a gloo group and report the world, no GPU work")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------------------------
+# launcher: N rank processes from a parent that never initialises a GPU
+def launch(args):
+    import socket
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    out, _ = procs[0].communicate()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
+
+
+def dist_env():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+# ---------------------------------------------------------------------------------------------
 def build_workload(cfg, nblk, seg_bytes, seed, dev):
-    """Synthetic KV stream -> GPU-encoded blocks truncated to exactly nblk blocks."""
+    """Synthetic KV stream -> GPU-encoded blocks truncated to exactly nblk blocks.  Also returns
+    the host KV of exactly those entries and their segment table (for the oracle check)."""
     bs = synth.BLOCK_SIZE[cfg]
     per_block = {"U": 31.0, "Z": 34.5, "M": 95.0}[cfg]
     n = int(nblk * per_block * 1.03) + 1024
@@ -65,7 +109,6 @@ def build_workload(cfg, nblk, seg_bytes, seed, dev):
     keys, ko, vals, vo, ts = synth.GENERATORS[cfg](n, seed=seed)
     seg = synth.segments_by_bytes(ko, vo, seg_bytes)
     d = batch.KVStream.from_numpy(keys, ko, vals, vo, ts, device=dev)
-    del keys, vals
     blocks, blk_off = batch.encode_kv(d, seg, bs)
     del d
     total_blocks = blk_off.numel() - 1
@@ -77,31 +120,42 @@ def build_workload(cfg, nblk, seg_bytes, seed, dev):
     kv = batch.decode_blocks(blocks, blk_off)            # exactly the entries of the kept blocks
     seg = seg[seg < kv.n]
     seg = np.concatenate([seg, [kv.n]]).astype(np.uint32)
+    host = (keys[:int(ko[kv.n])], ko[:kv.n + 1], vals[:int(vo[kv.n])], vo[:kv.n + 1], ts[:kv.n])
     log(f"[rank] workload {cfg}: {nblk} blocks, {kv.n} entries, {end / GiB:.3f} GiB encoded, "
         f"{len(seg) - 1} segments, setup {time.time() - t:.1f}s")
-    return blocks, blk_off, kv, seg, bs
+    return blocks, blk_off, kv, seg, bs, host
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} != --gpus {args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
-    cfg = args.config
+def oracle_check_blocks(host, seg, bs, blocks, blk_off, out_kv, n, out_blocks, out_off, nblk):
+    """The whole batch against the C oracle: the oracle's encode of the synthetic KV must equal
+    the input blocks (so the GPU-made input is independently pinned), the oracle's decode of the
+    input must equal the GPU decode, and the GPU re-encode must equal both.  Returns the number
+    of blocks checked (0 on any mismatch)."""
+    from oracle import oracle as O
+    t = time.time()
+    kv = O.KV(*host)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, bs)
+    hb = blocks.cpu().numpy()
+    ok = rc == 0 and len(ref_off) == nblk + 1 and np.array_equal(ref_blocks, hb)
+    ok = ok and np.array_equal(ref_off, blk_off.cpu().numpy().view(np.uint64))
+    ok = ok and np.array_equal(out_blocks[:len(hb)].cpu().numpy(), ref_blocks)
+    ok = ok and np.array_equal(out_off[:nblk + 1].cpu().numpy().view(np.uint64), ref_off)
+    if ok:
+        rc, dkv = O.decode_blocks(ref_blocks, ref_off)
+        keys, ko, vals, vo, ts = batch.KVStream(out_kv.keys, out_kv.key_off, out_kv.vals, out_kv.val_off,
+                                                out_kv.ts, n).to_numpy()
+        ok = rc == 0 and dkv.n == n and np.array_equal(ko, dkv.key_off) and np.array_equal(vo, dkv.val_off)
+        ok = ok and np.array_equal(ts, dkv.ts) and np.array_equal(keys, dkv.keys) and np.array_equal(vals, dkv.vals)
+    log(f"[rank] oracle check of {nblk} blocks: {'ok' if ok else 'MISMATCH'} ({time.time() - t:.1f}s)")
+    return nblk if ok else 0
+
+
+def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
+    """U / Z / M: decode + re-encode of the resident batch.  Returns the result dict (rank 0)."""
     nblk = args.blocks or (65536 if cfg == "M" else 1 << 20)
-
-    blocks, blk_off, kv, seg, bs = build_workload(cfg, nblk, args.segment_bytes, 1000 + rank, dev)
+    blocks, blk_off, kv, seg, bs, host = build_workload(cfg, nblk, args.segment_bytes, 1000 + rank, dev)
     E = int(blocks.numel())
-    K = int(kv.key_off[kv.n].item()) & 0xFFFFFFFF
-    V = int(kv.val_off[kv.n].item()) & 0xFFFFFFFF
+    K, V = kv.byte_sizes()
     n = kv.n
     D = K + V + 16 * n  # decoded SoA bytes: key + value + u64 ts + u32 key_off + u32 val_off
 
@@ -115,9 +169,9 @@ def main():
     seg_t = torch.from_numpy(seg.view(np.int32)).to(dev)
     st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
     st_enc = torch.zeros(4, dtype=torch.int64, device=dev)
-    ctx = batch._ctx(local, torch.cuda.current_stream(dev))
-    check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
     stream = torch.cuda.current_stream(dev)
+    ctx = batch._ctx(local, stream)
+    check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
 
     def step(ev=None):
         if ev is not None:
@@ -129,7 +183,7 @@ def main():
         if ev is not None:
             ev[2].record(stream)
 
-    if args.ablate is not None:
+    if args.ablate is not None and not extra:
         if args.ablate >= 16:  # encode-side masks: per-kernel times with the mask applied
             res = {}
             for mask in (0, 16, 32, 64, 112, 128, 240):
@@ -138,25 +192,10 @@ def main():
                 res[mask] = kernel_times(ctx, step, dev, reps=2)["emit"]
             check(lib().lsmblk_debug_set(ctx, 1, 0))
             print(json.dumps({"ablation_emit_ms_by_skip_mask": res}), flush=True)
-            return 0
-        return ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    dec_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    enc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+            return None
+        ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream)
+        return None
+    elapsed, (dec_ms, enc_ms) = timed(step, steps, warmup, world, dev)
 
     # correctness of the last step: re-encoded bytes == input bytes
     sd, se = st_dec.cpu().tolist(), st_enc.cpu().tolist()
@@ -164,67 +203,280 @@ def main():
           and torch.equal(out_blocks[:E], blocks) and torch.equal(out_off[:nblk + 1], blk_off))
     if not ok:
         log(f"ROUND TRIP MISMATCH dec_stats={sd} enc_stats={se}")
-
-    t_max = elapsed
-    ok_all = ok
-    if world > 1:
-        tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max, ok_all = float(tt[0].item()), tt[1].item() == 0.0
+    checked = 0
+    if ok and not args.no_oracle_check:
+        checked = oracle_check_blocks(host, seg, bs, blocks, blk_off, out_kv, n, out_blocks, out_off, nblk)
+        ok = checked == nblk
+    t_max, ok_all, checked_all = reduce_ranks(elapsed, ok, checked, world, dev)
 
     # per-kernel durations: a short profiling pass after the timed region, HIP events recorded
     # by liblsmblk.so on the launch stream around every kernel (diagnostics only, not timed)
     kms = kernel_times(ctx, step, dev, reps=3)
+    if rank != 0:
+        return None
+    value = world * E * steps / t_max / GiB
+    ms_per_step = t_max / steps * 1e3
+    # algorithmic bytes per launch of each kernel (DESIGN.md "Kernels")
+    hdr = 8 * (nblk + 1) + 2 * nblk + 8 * n          # count: blk_off, trailers, offsets + entry headers
+    algo = {"dec_count": hdr, "dec_scan": 0, "decode": E + D + 8 * (nblk + 1) + 12 * nblk,
+            "plan": 8 * (n + 1) + K + 8 * nblk, "emit": D + E + 16 * (nblk + 1)}
+    dom = max(kms, key=lambda k: kms[k])
+    achieved = algo[dom] / (kms[dom] * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("workload") == cfg and tj.get("blocks") == nblk:
+            traffic = tj.get("bytes_per_launch", {}).get(dom)
+    desc = {"U": "16-B uniform keys, 100-B values", "Z": "Zipf 12-B prefixes, 100-B values",
+            "M": "16-B keys, 8 B-4 KiB values"}[cfg]
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"{cfg}: {nblk} blocks/GPU x block_size {bs}, decode + re-encode ({desc})",
+                   "blocks_per_gpu": nblk, "entries_per_gpu": n, "encoded_bytes_per_gpu": E,
+                   "decoded_bytes_per_gpu": D, "block_size": bs, "segments_per_gpu": len(seg) - 1,
+                   "parallelism": f"block-sharded x{world} (no data-path collective)",
+                   "rccl_world": world, "roundtrip_bit_exact": bool(ok_all),
+                   "oracle_checked_blocks": int(checked_all)},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_launch": algo[dom], "launch_ms": round(kms[dom], 4),
+                     "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
+                     "stage_ms": {"decode": round(dec_ms, 4), "encode": round(enc_ms, 4)},
+                     "step_algorithmic_bytes": algo["decode"] + algo["emit"],
+                     "step_frac": round((algo["decode"] + algo["emit"]) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "cpu_baseline": None,
+    }
+    if extra:
+        return result
+    result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
+    result["framing_meta"] = framing_meta(out_blocks, out_off, nblk, seg_t, st_enc, dev, stream)
+    result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
+    if world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
+    if args.pcie:
+        result["pcie_inclusive_gib_s"] = pcie_inclusive(blocks, blk_off, E, out_kv, n, K, V, seg_t, seg, bs,
+                                                        out_blocks, out_cap, out_off, blk_cap, nblk, dev)
+    return result
 
-    result = None
-    if rank == 0:
-        value = world * E * args.steps / t_max / GiB
-        ms_per_step = t_max / args.steps * 1e3
-        # algorithmic bytes per launch of each kernel (DESIGN.md "Kernels")
-        hdr = 8 * (nblk + 1) + 2 * nblk + 8 * n          # count: blk_off, trailers, offsets + entry headers
-        algo = {"dec_count": hdr, "dec_scan": 0, "decode": E + D + 8 * (nblk + 1) + 12 * nblk,
-                "plan": 8 * (n + 1) + K + 8 * nblk, "emit": D + E + 16 * (nblk + 1)}
-        dom = max(kms, key=lambda k: kms[k])
-        achieved = algo[dom] / (kms[dom] * 1e-3) / 1e9
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            tj = json.load(open(tpath))
-            if tj.get("workload") == cfg and tj.get("blocks") == nblk:
-                traffic = tj.get("bytes_per_launch", {}).get(dom)
-        result = {
-            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic",
-            "config": {"workload": f"{cfg}: {nblk} blocks/GPU x block_size {bs}, decode + re-encode "
-                                   f"({'16-B uniform keys, 100-B values' if cfg == 'U' else ('Zipf 12-B prefixes, 100-B values' if cfg == 'Z' else '16-B keys, 8 B-4 KiB values')})",
-                       "blocks_per_gpu": nblk, "entries_per_gpu": n, "encoded_bytes_per_gpu": E,
-                       "decoded_bytes_per_gpu": D, "block_size": bs, "segments_per_gpu": len(seg) - 1,
-                       "parallelism": f"block-sharded x{world} (no data-path collective)",
-                       "roundtrip_bit_exact": bool(ok_all)},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_launch": algo[dom], "launch_ms": round(kms[dom], 4),
-                         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
-                         "stage_ms": {"decode": round(dec_ms, 4), "encode": round(enc_ms, 4)},
-                         "step_algorithmic_bytes": algo["decode"] + algo["emit"]},
-            "cpu_baseline": None,
-        }
-        result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
-        result["framing_meta"] = framing_meta(out_blocks, out_off, nblk, seg_t, st_enc, dev, stream)
-        result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
-        if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
-        if args.pcie:
-            result["pcie_inclusive_gib_s"] = pcie_inclusive(blocks, blk_off, E, out_kv, n, K, V, seg_t, seg, bs,
-                                                            out_blocks, out_cap, out_off, blk_cap, nblk, dev)
+
+def timed(step, steps, warmup, world, dev):
+    """warmup, barrier + sync, exactly `steps` timed steps, barrier + sync.  Returns the elapsed
+    seconds and the mean (first-stage, second-stage) ms from HIP events on the launch stream."""
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
     if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    a = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    b = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    return elapsed, (a, b)
+
+
+def reduce_ranks(elapsed, ok, checked, world, dev):
+    """max elapsed, all-ok, and the sum of oracle-checked units over the ranks."""
+    if world == 1:
+        return elapsed, ok, checked
+    import torch.distributed as dist
+    tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    cc = torch.tensor([checked], dtype=torch.int64, device=dev)
+    dist.all_reduce(cc, op=dist.ReduceOp.SUM)
+    return float(tt[0].item()), tt[1].item() == 0.0, int(cc.item())
+
+
+# ---------------------------------------------------------------------------------------------
+# config C: compaction-shaped decode -> merge -> rules -> rotation -> encode
+def build_runs(nblk, nrun, seg_bytes, seed, dev, key_lo=0, key_hi=None):
+    """nrun overlapping sorted runs (L0 SSTs of seg_bytes each), about nblk 4 KiB blocks in all,
+    encoded on the device; returns the concatenated input blocks, their offsets, the per-run
+    entry starts, and the host KV (for the oracle)."""
+    t = time.time()
+    n_keys = int(nblk * 31.0 / 1.1)
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(n_keys, nrun=nrun, seed=seed)
+    parts, offs, base = [], [], 0
+    for r in range(nrun):
+        a, b = int(rs[r]), int(rs[r + 1])
+        rk = keys[int(ko[a]):int(ko[b])]
+        rv = vals[int(vo[a]):int(vo[b])]
+        rko, rvo = ko[a:b + 1] - ko[a], vo[a:b + 1] - vo[a]
+        seg = synth.segments_by_bytes(rko, rvo, seg_bytes)
+        d = batch.KVStream.from_numpy(rk, rko, rv, rvo, ts[a:b], device=dev)
+        blk, off = batch.encode_kv(d, seg, 4096)
+        parts.append(blk)
+        offs.append(off[:-1] + base if r < nrun - 1 else off + base)
+        base += int(blk.numel())
+        del d
+    blocks = torch.cat(parts)
+    blk_off = torch.cat(offs)
+    log(f"[rank] workload C: {nrun} runs, {len(ts)} entries, {blk_off.numel() - 1} blocks, "
+        f"{blocks.numel() / GiB:.3f} GiB encoded, setup {time.time() - t:.1f}s")
+    return blocks, blk_off, rs, (keys, ko, vals, vo, ts)
+
+
+def oracle_check_compaction(host, rs, opts, buf, stats):
+    """GPU compaction == compact_generate_sst restated in C (orc_merge_runs + orc_compact) over the
+    whole batch: blocks, block offsets, SST first entries / first blocks, kept entries."""
+    from oracle import oracle as O
+    t = time.time()
+    kv = O.KV(*host)
+    src = O.merge_runs(kv, rs)
+    want = O.compact(kv, src, opts["watermark"], opts["bottom_level"], (), opts["block_size"],
+                     opts["target_sst_size"])
+    nblk, nbytes, nsst = stats[0], stats[1], stats[2]
+    ok = (stats[4] == len(src) and stats[5] == len(want["kept"]) and nblk == len(want["blk_off"]) - 1
+          and nsst == len(want["sst_blk"]) - 1)
+    ok = ok and np.array_equal(buf.out[:nbytes].cpu().numpy(), want["blocks"])
+    ok = ok and np.array_equal(buf.blk_off[:nblk + 1].cpu().numpy().view(np.uint64), want["blk_off"])
+    ok = ok and np.array_equal(buf.sst_start[:nsst + 1].cpu().numpy().view(np.uint32), want["sst_ent"])
+    ok = ok and np.array_equal(buf.sst_blk[:nsst + 1].cpu().numpy().view(np.uint32), want["sst_blk"])
+    log(f"[rank] oracle check of the compaction ({nblk} output blocks, {nsst} SSTs): "
+        f"{'ok' if ok else 'MISMATCH'} ({time.time() - t:.1f}s)")
+    return nblk if ok else 0
+
+
+def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
+    nblk_in = args.blocks or (1 << 20)
+    nrun = 8
+    blocks, blk_off, rs, host = build_runs(nblk_in, nrun, args.segment_bytes, 2000 + rank, dev)
+    nblk = blk_off.numel() - 1
+    E = int(blocks.numel())
+    n = int(rs[-1])
+    K, V = len(host[0]), len(host[2])
+    kv = batch.KVStream.empty(n, K, V, dev)
+    st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
+    rs_t = torch.from_numpy(rs.view(np.int32)).to(dev)
+    buf = batch.CompactBuffers(n, K, V, dev, target_sst_size=args.segment_bytes)
+    ts = host[4]
+    opts = batch.compact_opts(watermark=int(ts.max()) // 2, bottom_level=True, block_size=4096,
+                              target_sst_size=args.segment_bytes, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ctx = batch._ctx(local, stream)
+    check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, buf.sst_cap))
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        batch.decode_into(blocks, blk_off, nblk, kv, st_dec, n, K + 16, V + 16)
+        kv.n = n
+        if ev is not None:
+            ev[1].record(stream)
+        batch.compact_into(kv, rs_t, nrun, opts, buf)
+        if ev is not None:
+            ev[2].record(stream)
+
+    elapsed, (dec_ms, cmp_ms) = timed(step, steps, warmup, world, dev)
+    s = buf.stats.cpu().tolist()
+    sd = st_dec.cpu().tolist()
+    ok = sd[3] == 0 and s[3] == 0 and sd[0] == n
+    if not ok:
+        log(f"COMPACTION FAILED dec_stats={sd} stats={s}")
+    checked = 0
+    if ok and not args.no_oracle_check:
+        checked = oracle_check_compaction(host, rs, opts, buf, s)
+        ok = checked == s[0]
+    t_max, ok_all, checked_all = reduce_ranks(elapsed, ok, checked, world, dev)
+    if rank != 0:
+        return None
+    ms = t_max / steps * 1e3
+    Dk = s[6] + s[7] + 16 * s[5]
+    D = K + V + 16 * n
+    return {
+        "metric": METRIC, "value": round(world * E * steps / t_max / GiB, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"C: compaction-shaped, {nrun} overlapping sorted runs of {args.segment_bytes >> 20} MiB "
+                               f"SSTs ({nblk} x 4 KiB input blocks/GPU, ~10% overwrites, 2% tombstones): decode + "
+                               "MergeIterator merge + compaction rules (bottom level, watermark) + SST rotation + "
+                               "block packing", "input_blocks_per_gpu": nblk, "input_entries_per_gpu": n,
+                   "encoded_bytes_per_gpu": E, "merged_entries": s[4], "kept_entries": s[5],
+                   "output_blocks": s[0], "output_bytes": s[1], "output_ssts": s[2],
+                   "target_sst_size": args.segment_bytes, "parallelism": f"key-range sharded x{world}",
+                   "rccl_world": world, "compaction_bit_exact": bool(ok_all),
+                   "oracle_checked_blocks": int(checked_all)},
+        "stage_ms": {"decode": round(dec_ms, 4), "compact": round(cmp_ms, 4)},
+        "step_algorithmic_bytes": {"decode": E + D, "merge_gather": 2 * D + 4 * n, "encode": Dk + s[1]},
+    }
+
+
+def dry_run(rank, world, local):
+    """The launcher's contract without a GPU: every rank joins one gloo group; rank 0 reports the
+    world size the collective saw and the ranks it heard from."""
+    import torch.distributed as dist
+    seen = world
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.tensor([1 << rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        seen = dist.get_world_size()
+        mask = int(t.item())
+        dist.destroy_process_group()
+    else:
+        mask = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "collective_world": seen, "rank_mask": mask,
+                          "local_rank": local}), flush=True)
+    return 0
+
+
+# ---------------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    if "RANK" not in os.environ and args.gpus > 1:
+        return launch(args)
+    rank, world, local = dist_env()
+    if world != args.gpus:
+        log(f"refusing to run: WORLD_SIZE={world} but --gpus {args.gpus}")
+        return 2
+    if args.dry_run:
+        return dry_run(rank, world, local)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            log(f"refusing to run: RCCL world {dist.get_world_size()} != --gpus {args.gpus}")
+            return 2
+    if args.config == "C":
+        result = run_compaction(args, args.steps, args.warmup, rank, world, local, dev)
+    else:
+        result = run_blocks(args, args.config, args.steps, args.warmup, rank, world, local, dev)
+    if args.ablate is not None:
+        return 0
+    if world == 1 and args.config == "U" and not args.no_extras and args.blocks is None:
+        extras = {}
+        for cfg in ("Z", "M"):
+            torch.cuda.empty_cache()
+            extras[cfg] = run_blocks(args, cfg, 5, 2, rank, world, local, dev, extra=True)
+        torch.cuda.empty_cache()
+        extras["C"] = run_compaction(args, 3, 1, rank, world, local, dev, extra=True)
+        result["extra_configs"] = extras
+    ok = True
+    if world > 1:
+        import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
     if result is not None:
+        cfg = result["config"]
+        ok = cfg.get("roundtrip_bit_exact", cfg.get("compaction_bit_exact", False))
         print(json.dumps(result), flush=True)
-    return 0 if ok_all else 1
+    return 0 if ok else 1
 
 
 KERNELS = ["dec_count", "dec_scan", "decode", "plan", "emit"]

@@ -451,13 +451,17 @@ class CompactBuffers:
     """Preallocated outputs of lsmblk_compact_batch for an input of n entries / K key bytes /
     V value bytes (worst case: every entry kept, every entry its own block and SST)."""
 
-    def __init__(self, n, key_bytes, val_bytes, device, sst_cap=None):
+    def __init__(self, n, key_bytes, val_bytes, device, sst_cap=None, target_sst_size=None):
         self.kept = KVStream.empty(n, key_bytes, val_bytes, device)
         self.out_cap = key_bytes + val_bytes + 18 * n + 16
         self.out = _aligned_empty(self.out_cap, device)
         self.blk_cap = n + 2
         self.blk_off = torch.zeros(self.blk_cap, dtype=torch.int64, device=device)
-        self.sst_cap = sst_cap or (n + 2)
+        if sst_cap is None:
+            # every SST but the last holds >= target bytes of blocks + CRCs, and the blocks take at
+            # most klen + vlen + 22 bytes per entry (header, ts, offset slot, trailer, CRC)
+            sst_cap = n + 2 if not target_sst_size else min(n + 2, (key_bytes + val_bytes + 22 * n) // target_sst_size + 3)
+        self.sst_cap = sst_cap
         self.sst_start = torch.zeros(self.sst_cap, dtype=torch.int32, device=device)
         self.sst_blk = torch.zeros(self.sst_cap, dtype=torch.int32, device=device)
         self.stats = torch.zeros(8, dtype=torch.int64, device=device)
@@ -495,7 +499,7 @@ def compact_runs(kv: KVStream, run_start, watermark=0, bottom_level=False, prefi
     dev = torch.device("cuda", _dev_index(kv.key_off))
     rs = _u32_table(run_start, dev)
     kb, vb = kv.byte_sizes()
-    buf = CompactBuffers(kv.n, kb, vb, dev)
+    buf = CompactBuffers(kv.n, kb, vb, dev, target_sst_size=target_sst_size)
     opts = compact_opts(watermark, bottom_level, prefixes, block_size, target_sst_size, dev)
     compact_into(kv, rs, rs.numel() - 1, opts, buf, stream)
     torch.cuda.synchronize(dev)

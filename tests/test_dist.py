@@ -65,3 +65,31 @@ def test_gloo_world2_exchange():
     assert s0 == s1 and len(s0) == 1
     # the splitter lies inside the union of both runs
     assert b"key000000" < s0[0] < b"key002000"
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_launcher_starts_world_ranks(world):
+    """`bench.py --gpus N` without torchrun starts N rank processes itself (the parent touches no
+    GPU); in --dry-run every rank joins one gloo group and rank 0 reports what it saw."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run"],
+                       capture_output=True, text=True, timeout=170, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["collective_world"] == world
+    assert line["rank_mask"] == (1 << world) - 1
+
+
+def test_bench_refuses_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and r.stdout == ""
