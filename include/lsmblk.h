@@ -59,6 +59,7 @@ enum {
   LSMBLK_E_TIMEOUT = -6,   /* a device-side look-back wait exceeded its bound (must not happen) */
   LSMBLK_E_OVERFLOW = -7,  /* a batch total does not fit the u32 KV-stream offsets */
   LSMBLK_E_INTERNAL = -8,  /* device self-check failed */
+  LSMBLK_E_CHECKSUM = -9,  /* a block's framing CRC does not match (read_block, src/table.rs:228-230) */
 };
 
 int lsmblk_abi_version(void);
@@ -139,6 +140,7 @@ typedef struct {
 #define LSMBLK_ERR_SEGMENTS 16u
 #define LSMBLK_ERR_INTERNAL 32u
 #define LSMBLK_ERR_EMPTY_KEY 64u
+#define LSMBLK_ERR_CHECKSUM 128u
 /* Map a stats[3] error-flag word (copied to the host) to an LSMBLK_E_* status. */
 int lsmblk_stats_status(uint64_t error_flags);
 
@@ -170,6 +172,18 @@ int lsmblk_ctx_kernel_times(lsmblk_ctx* ctx, float* ms);
 int lsmblk_decode_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off,
                         uint64_t nblk, const lsmblk_kv_stream* out, uint64_t* stats,
                         void* stream);
+
+/* Decode of an SST data section as SsTable::read_block reads it (src/table.rs:213-233): block b =
+ * blocks[blk_off[b] .. blk_off[b+1] - tail) -- tail = 4 over a framed data section addressed by its
+ * BlockMeta offsets (block_len = offset_end - offset - 4), 0 for packed blocks.  With
+ * LSMBLK_DECODE_VERIFY_CRC (tail must be 4) the u32 BE after every block is checked against its
+ * crc32fast; a mismatch sets LSMBLK_ERR_CHECKSUM ("block checksum mismatched").  blk_ent (device
+ * u64[nblk+1], optional) receives every block's first entry index in `out` and then the total, e.g.
+ * the run boundaries for lsmblk_merge_batch.  Otherwise as lsmblk_decode_batch. */
+#define LSMBLK_DECODE_VERIFY_CRC 1u
+int lsmblk_decode_batch_ex(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
+                           uint32_t tail, uint32_t flags, const lsmblk_kv_stream* out, uint64_t* blk_ent,
+                           uint64_t* stats, void* stream);
 
 /* Encode the SoA stream `in` greedily into blocks of `block_size`, restarting the block
  * packing at every segment start (seg_start u32[nseg+1], seg_start[0] = 0, seg_start[nseg]

@@ -22,6 +22,8 @@ LSMBLK_E_HIP = -5
 LSMBLK_E_TIMEOUT = -6
 LSMBLK_E_OVERFLOW = -7
 LSMBLK_E_INTERNAL = -8
+LSMBLK_E_CHECKSUM = -9
+LSMBLK_DECODE_VERIFY_CRC = 1
 
 
 class LsmBlkError(RuntimeError):
@@ -74,6 +76,7 @@ SIGNATURES = [
     ("lsmblk_debug_set", I, [P, I, U32]),
     ("lsmblk_ctx_kernel_times", I, [P, ctypes.POINTER(ctypes.c_float)]),
     ("lsmblk_decode_batch", I, [P, P, P, U64, ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_decode_batch_ex", I, [P, P, P, U64, U32, U32, ctypes.POINTER(KVStreamC), P, P, P]),
     ("lsmblk_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, P, U64, P, U64, P, P]),
     ("lsmblk_crc32_batch", I, [P, P, P, U64, U32, P, P, P]),
     ("lsmblk_encode_segment_blocks", I, [P, P, U32, P, P, P]),

@@ -22,7 +22,8 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ._lib import CompactOptsC, KVStreamC, LSMBLK_E_CAPACITY, LsmBlkError, check, lib
+from ._lib import (CompactOptsC, KVStreamC, LSMBLK_DECODE_VERIFY_CRC, LSMBLK_E_CAPACITY, LsmBlkError, check,
+                   lib)
 
 STATS_WORDS = 4
 _ctx_lock = threading.Lock()
@@ -191,19 +192,48 @@ def decode_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_cap,
                                     stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_decode_batch")
 
 
-def decode_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None) -> KVStream:
-    """Decode blocks[blk_off[b]:blk_off[b+1]] for every b into a KVStream (synchronizes)."""
+def decode_ex_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_cap, val_cap, tail=0, verify=False,
+                   blk_ent=None, stream=None):
+    """Asynchronous lsmblk_decode_batch_ex: framed ranges (tail), CRC verification, block entry index."""
+    dev = _dev_index(blk_off)
+    _need(blk_off, torch.int64, "blk_off", dev, nblk + 1)
+    if nblk:
+        _need(blocks, torch.uint8, "blocks", dev)
+    _need(stats, torch.int64, "stats", dev, STATS_WORDS)
+    if blk_ent is not None:
+        _need(blk_ent, torch.int64, "blk_ent", dev, nblk + 1)
+    out.check(dev, "out", 0)
+    if out.key_off.numel() < entry_cap + 1 or out.ts.numel() < entry_cap or out.keys.numel() < key_cap \
+            or out.vals.numel() < val_cap:
+        raise ValueError("decode_ex_into: capacities exceed the output tensors")
+    c = out._c(entry_cap, key_cap, val_cap)
+    check(lib().lsmblk_decode_batch_ex(_ctx(dev, stream), _ptr(blocks), _ptr(blk_off), nblk, tail,
+                                       LSMBLK_DECODE_VERIFY_CRC if verify else 0, ctypes.byref(c), _ptr(blk_ent),
+                                       stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_decode_batch_ex")
+
+
+def decode_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None, tail: int = 0, verify: bool = False,
+                  with_blk_ent: bool = False):
+    """Decode blocks[blk_off[b]:blk_off[b+1] - tail] for every b into a KVStream (synchronizes).
+    tail=4 reads a framed SST data section by its BlockMeta offsets (SsTable::read_block,
+    reference src/table.rs:213-233); verify=True checks every block's stored crc32fast.
+    with_blk_ent: also return the first entry index of every block (int64[nblk+1])."""
     dev = torch.device("cuda", _dev_index(blk_off))
     nblk = blk_off.numel() - 1
     total = int(blocks.numel())
     entry_cap = total // 16 + 1
     key_cap, val_cap = total + 16, total + 16
+    blk_ent = torch.zeros(nblk + 1, dtype=torch.int64, device=dev) if with_blk_ent else None
     for _ in range(2):
         out = KVStream(_aligned_empty(key_cap, dev), torch.empty(entry_cap + 1, dtype=torch.int32, device=dev),
                        _aligned_empty(val_cap, dev), torch.empty(entry_cap + 1, dtype=torch.int32, device=dev),
                        torch.empty(max(entry_cap, 1), dtype=torch.int64, device=dev), 0)
         stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
-        decode_into(blocks, blk_off, nblk, out, stats, entry_cap, key_cap, val_cap, stream)
+        if tail or verify or with_blk_ent:
+            decode_ex_into(blocks, blk_off, nblk, out, stats, entry_cap, key_cap, val_cap, tail, verify, blk_ent,
+                           stream)
+        else:
+            decode_into(blocks, blk_off, nblk, out, stats, entry_cap, key_cap, val_cap, stream)
         torch.cuda.synchronize(dev)
         st = _status(stats)
         s = stats.cpu().tolist()
@@ -213,7 +243,7 @@ def decode_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None) -> K
         if st:
             raise LsmBlkError(st, "decode_blocks")
         out.n = s[0]
-        return out
+        return (out, blk_ent) if with_blk_ent else out
     raise LsmBlkError(LSMBLK_E_CAPACITY, "decode_blocks")
 
 

@@ -33,10 +33,10 @@
 
 namespace {
 
-constexpr uint32_t kMS = 64;        // every kMS-th entry of a run is a merge candidate
+constexpr uint32_t kMS = 128;       // every kMS-th entry of a run is a merge candidate
 constexpr uint32_t kMaxRuns = 64;   // runs per merge (one lane per run in the tile kernels)
-constexpr uint32_t kMTE = 512;      // tile entries with LDS tables
-constexpr uint32_t kMTK = 8192;     // tile key bytes staged in LDS
+constexpr uint32_t kMTE = 1024;     // tile entries with LDS tables (larger tiles: global path)
+constexpr uint32_t kMTT = 128;      // threads per tile workgroup
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------- key access
@@ -94,7 +94,7 @@ struct MergeArgs {
   uint32_t nrun;
   uint32_t nc_max;          // bound on candidates (= tiles)
   uint32_t* cand;           // nc_max: sorted candidate -> input index
-  uint32_t* bounds;         // nrun rows of nc_max + 1: tile t's first entry in run r
+  uint32_t* bounds;         // (nc_max + 1) x nrun: tile t's first entry in run r
   uint32_t* mrank;          // n: in-tile merged rank of a surviving entry, kNone if dropped
   uint32_t* sp;             // n: survivor prefix (tiles too large for LDS)
   uint32_t* tcnt;           // nc_max: survivors per tile
@@ -169,9 +169,9 @@ __global__ __launch_bounds__(256) void bounds_kernel(MergeArgs a) {
   const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   const uint32_t t = uint32_t(i / a.nrun), r = uint32_t(i % a.nrun);
   if (t > NC) return;
-  uint32_t* row = a.bounds + uint64_t(r) * (a.nc_max + 1);
+  uint32_t* out = a.bounds + uint64_t(t) * a.nrun + r;  // tile-major: a tile's bounds share a line
   if (t == NC) {
-    row[t] = s_rs[r + 1];
+    *out = s_rs[r + 1];
     return;
   }
   const GKeys K = gkeys(a.keys, a.key_off[a.n]);
@@ -190,215 +190,277 @@ __global__ __launch_bounds__(256) void bounds_kernel(MergeArgs a) {
     if (key_cmp(K, qp, a.key_off[mid + 1] - qp, xp, xl) < 0) e0 = mid + 1;
     else e1 = mid;
   }
-  row[t] = e0;
+  *out = e0;
 }
 
-struct alignas(16) MTileLds {
-  uint32_t lo[kMaxRuns], tb[kMaxRuns + 1], kb[kMaxRuns + 1], kbeg[kMaxRuns];
-  uint32_t rsp[kMaxRuns], rsv[kMaxRuns];  // survivors before run r's sub-range / inside it
+struct TileHdr {
+  uint32_t lo[kMaxRuns], tb[kMaxRuns + 1];  // run r's sub-range start; tile index of its first entry
+  uint32_t rsp[kMaxRuns], rsv[kMaxRuns];   // survivors before run r's sub-range / inside it
   uint32_t total, nsurv;
-  uint32_t koff[kMTE];
-  uint32_t sp[kMTE + 1];
-  uint16_t klen[kMTE];
+  uint32_t wsum[kMTT / 64];
+};
+struct alignas(16) MTileLds {
+  TileHdr h;
+  u32x4 kw[kMTE];          // first 16 key bytes as big-endian words, zero padded
+  uint32_t klen[kMTE];
+  uint16_t sp[kMTE + 1];   // survivor prefix over the tile (run-major order)
   uint8_t surv[kMTE];
-  uint8_t kimg[kMTK + 16];
 };
 
-// The tile's per-run sub-ranges into LDS: lane r holds run r's [lo, hi).  Each run's key bytes
-// are staged as the 16-B aligned arena chunks covering them (aligned buffer loads never
-// straddle the descriptor bound, which would zero a whole unaligned load): kbeg[r] = the
-// aligned descriptor offset of run r's first chunk, kb[r] = its LDS offset.
-__device__ __forceinline__ void tile_ranges(const MergeArgs& a, MTileLds& L, uint32_t t, uint32_t glead) {
+// The tile's per-run sub-ranges (wave 0; lane r = run r).
+__device__ __forceinline__ void tile_ranges(const MergeArgs& a, TileHdr& H, uint32_t t) {
   const uint32_t l = lane_id();
-  uint32_t lo = 0, hi = 0, A = 0, B = 0;
+  uint32_t lo = 0, hi = 0;
   if (l < a.nrun) {
-    const uint32_t* row = a.bounds + uint64_t(l) * (a.nc_max + 1);
-    lo = row[t];
-    hi = row[t + 1];
+    const uint32_t* row = a.bounds + uint64_t(t) * a.nrun;
+    lo = row[l];
+    hi = row[a.nrun + l];
     if (hi < lo) hi = lo;  // only with unsorted runs (output then unspecified, flagged by mflag)
-    if (hi > lo) {
-      A = (glead + a.key_off[lo]) & ~15u;
-      B = (glead + a.key_off[hi] + 15) & ~15u;
-    }
   }
-  const uint32_t m = hi - lo, kbytes = B - A;
-  const uint32_t mi = wave_incl_scan32(m), ki = wave_incl_scan32(kbytes);
+  const uint32_t m = hi - lo, mi = wave_incl_scan32(m);
   if (l < a.nrun) {
-    L.lo[l] = lo;
-    L.tb[l] = mi - m;
-    L.kb[l] = ki - kbytes;
-    L.kbeg[l] = A;
+    H.lo[l] = lo;
+    H.tb[l] = mi - m;
   }
   if (l == 63) {
-    L.total = mi;
-    L.tb[a.nrun] = mi;
-    L.kb[a.nrun] = ki;
+    H.total = mi;
+    H.tb[a.nrun] = mi;
   }
-  wave_sync();
 }
 
-// One wave per tile.  LDS mode: keys staged, tables in LDS.  Global mode (a tile of more than
-// kMTE entries or kMTK key bytes: many versions of one key, or many runs): keys read through
-// the descriptor, survival kept in mrank[] and the survivor prefix in sp[], both handed between
-// lanes through L2 (sc1 stores / loads, drained with vmcnt(0)).
-template <bool kLds>
-__device__ void merge_tile(const MergeArgs& a, MTileLds& L, uint32_t t) {
-  const uint32_t l = lane_id(), nrun = a.nrun, total = L.total;
-  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
-  const LKeys LK{L.kimg};
-  if constexpr (kLds) {
-    // stage every run's key bytes (16-B unaligned buffer loads -> unaligned LDS stores); a run's
-    // last piece may spill into the next run's bytes, which the next run then rewrites
-    for (uint32_t r = 0; r < nrun; ++r) {
-      const uint32_t kb = L.kb[r], nb = L.kb[r + 1] - kb, src = L.kbeg[r];
-      for (uint32_t o = 16 * l; o < nb; o += 1024) {
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(G.r, src + o, 0, 0);
-        *reinterpret_cast<u32x4*>(L.kimg + kb + o) = q;
-      }
-    }
-    for (uint32_t u = l; u < total; u += 64) {
-      const uint32_t r = find_run(L.tb, nrun, u), g = L.lo[r] + u - L.tb[r];
-      const uint32_t k0 = a.key_off[g];
-      L.koff[u] = L.kb[r] + G.lead + k0 - L.kbeg[r];
-      L.klen[u] = uint16_t(a.key_off[g + 1] - k0);
-    }
-    wave_sync();
+// First 16 bytes of the key at arena position pos (len bytes) as big-endian words, zero padded:
+// five aligned dword loads through the descriptor (none straddles its bound) and alignbytes.
+__device__ __forceinline__ u32x4 key16(const GKeys& G, uint32_t pos, uint32_t len) {
+  const uint32_t x = G.lead + pos, al = x & ~3u, b = x & 3;
+  uint32_t w[5];
+#pragma unroll
+  for (uint32_t j = 0; j < 5; ++j) w[j] = __builtin_amdgcn_raw_buffer_load_b32(G.r, al + 4 * j, 0, 0);
+  uint32_t o[4];
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    uint32_t v = __builtin_amdgcn_alignbyte(w[i + 1], w[i], b);
+    const int32_t keep = int32_t(len) - int32_t(4 * i);  // bytes of this word inside the key
+    if (keep < 4) v &= keep <= 0 ? 0u : (1u << (8 * keep)) - 1;
+    o[i] = __builtin_bswap32(v);
   }
-  // key of tile entry (run r, index k of its sub-range)
-  auto kpos = [&](uint32_t r, uint32_t k, uint32_t& len) -> uint32_t {
-    if constexpr (kLds) {
-      const uint32_t u = L.tb[r] + k;
-      len = L.klen[u];
-      return L.koff[u];
-    } else {
-      const uint32_t g = L.lo[r] + k, p = a.key_off[g];
-      len = a.key_off[g + 1] - p;
-      return p;
-    }
-  };
-  auto cmp = [&](uint32_t ap, uint32_t al, uint32_t bp, uint32_t bl) -> int {
-    if constexpr (kLds) return key_cmp(LK, ap, al, bp, bl);
-    else return key_cmp(G, ap, al, bp, bl);
-  };
-  // first index of run r's sub-range whose key is >= x
-  auto lower = [&](uint32_t r, uint32_t xp, uint32_t xl) -> uint32_t {
-    uint32_t lo = 0, hi = L.tb[r + 1] - L.tb[r];
+  return u32x4{o[0], o[1], o[2], o[3]};
+}
+
+// Key order on (16-byte prefix, length, global index): the prefixes decide unless equal and
+// both keys are longer than 16 bytes (then the tails are compared in global memory).
+__device__ __forceinline__ int kcmp16(const MergeArgs& a, const GKeys& G, const u32x4& x, uint32_t xl, uint32_t xg,
+                                      const u32x4& y, uint32_t yl, uint32_t yg) {
+  if (x.x != y.x) return x.x < y.x ? -1 : 1;
+  if (x.y != y.y) return x.y < y.y ? -1 : 1;
+  if (x.z != y.z) return x.z < y.z ? -1 : 1;
+  if (x.w != y.w) return x.w < y.w ? -1 : 1;
+  if (xl <= 16 || yl <= 16) return xl < yl ? -1 : (xl > yl ? 1 : 0);
+  return key_cmp(G, a.key_off[xg] + 16, xl - 16, a.key_off[yg] + 16, yl - 16);
+}
+
+// LDS fast path: 128 threads per tile; every key's first 16 bytes in LDS.
+__device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
+  TileHdr& H = L.h;
+  const uint32_t tid = threadIdx.x, l = lane_id(), w = tid >> 6, nrun = a.nrun, total = H.total;
+  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
+  for (uint32_t u = tid; u < total; u += kMTT) {
+    const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
+    const uint32_t p = a.key_off[g], len = a.key_off[g + 1] - p;
+    L.kw[u] = key16(G, p, len);
+    L.klen[u] = len;
+  }
+  __syncthreads();
+  // first index of run r2's sub-range whose key is >= (x, xl)
+  auto lower = [&](uint32_t r2, const u32x4& x, uint32_t xl, uint32_t xg) -> uint32_t {
+    const uint32_t b = H.tb[r2];
+    uint32_t lo = 0, hi = H.tb[r2 + 1] - b;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      uint32_t ml;
-      const uint32_t mp = kpos(r, mid, ml);
-      if (cmp(mp, ml, xp, xl) < 0) lo = mid + 1;
+      if (kcmp16(a, G, L.kw[b + mid], L.klen[b + mid], H.lo[r2] + mid, x, xl, xg) < 0) lo = mid + 1;
       else hi = mid;
     }
     return lo;
   };
-  auto set_surv = [&](uint32_t u, uint32_t g, uint32_t v) {
-    if constexpr (kLds) L.surv[u] = uint8_t(v);
-    else __hip_atomic_store(a.mrank + g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto get_surv = [&](uint32_t u, uint32_t g) -> uint32_t {
-    if constexpr (kLds) return L.surv[u];
-    else return __hip_atomic_load(a.mrank + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto set_sp = [&](uint32_t u, uint32_t g, uint32_t v) {
-    if constexpr (kLds) L.sp[u] = v;
-    else __hip_atomic_store(a.sp + g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto get_sp = [&](uint32_t u, uint32_t g) -> uint32_t {
-    if constexpr (kLds) return L.sp[u];
-    else return __hip_atomic_load(a.sp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto drain = [&]() {
-    if constexpr (!kLds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    wave_sync();
-  };
   // phase A: survival -- no lower-index run holds the key (MergeIterator advances those heads)
-  for (uint32_t u = l; u < total; u += 64) {
-    const uint32_t r = find_run(L.tb, nrun, u), k = u - L.tb[r], g = L.lo[r] + k;
-    uint32_t xl;
-    const uint32_t xp = kpos(r, k, xl);
-    uint32_t s = 1;
-    for (uint32_t r2 = 0; r2 < r && s; ++r2) {
-      const uint32_t p = lower(r2, xp, xl);
-      if (p < L.tb[r2 + 1] - L.tb[r2]) {
-        uint32_t ql;
-        const uint32_t qp = kpos(r2, p, ql);
-        if (cmp(qp, ql, xp, xl) == 0) s = 0;
+  for (uint32_t u = tid; u < total; u += kMTT) {
+    const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
+    const u32x4 x = L.kw[u];
+    const uint32_t xl = L.klen[u];
+    uint32_t sv = 1;
+    for (uint32_t r2 = 0; r2 < r && sv; ++r2) {
+      const uint32_t p = lower(r2, x, xl, g), b = H.tb[r2];
+      if (p < H.tb[r2 + 1] - b && kcmp16(a, G, L.kw[b + p], L.klen[b + p], H.lo[r2] + p, x, xl, g) == 0) sv = 0;
+    }
+    L.surv[u] = uint8_t(sv);
+  }
+  __syncthreads();
+  // survivor prefix over the tile
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < total; c0 += kMTT) {
+    const uint32_t u = c0 + tid;
+    const uint32_t sv = u < total ? L.surv[u] : 0u;
+    const uint32_t inc = wave_incl_scan32(sv);
+    if (l == 63) H.wsum[w] = inc;
+    __syncthreads();
+    const uint32_t before = w ? H.wsum[0] : 0u, tot = H.wsum[0] + H.wsum[1];
+    if (u < total) L.sp[u] = uint16_t(carry + before + inc - sv);
+    carry += tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    L.sp[total] = uint16_t(carry);
+    H.nsurv = carry;
+  }
+  __syncthreads();
+  if (tid < nrun) {
+    H.rsp[tid] = L.sp[H.tb[tid]];
+    H.rsv[tid] = L.sp[H.tb[tid + 1]] - L.sp[H.tb[tid]];
+  }
+  __syncthreads();
+  // phase B: merged rank inside the tile = survivors with a smaller key in every other run +
+  // survivors before this entry in its own run (its group's earlier versions included)
+  for (uint32_t u = tid; u < total; u += kMTT) {
+    const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
+    uint32_t rank = kNone;
+    if (L.surv[u]) {
+      const u32x4 x = L.kw[u];
+      const uint32_t xl = L.klen[u];
+      rank = L.sp[u] - H.rsp[r];
+      for (uint32_t r2 = 0; r2 < nrun; ++r2) {
+        if (r2 == r || H.tb[r2 + 1] == H.tb[r2]) continue;
+        const uint32_t p = lower(r2, x, xl, g);
+        rank += L.sp[H.tb[r2] + p] - H.rsp[r2];
       }
     }
-    set_surv(u, g, s);
+    a.mrank[g] = rank;
+  }
+  if (tid == 0) a.tcnt[t] = carry;
+}
+
+// Global path (a tile of more than kMTE entries: many versions of one key, or many runs), one
+// wave: keys compared in global memory, survival kept in mrank[] and the survivor prefix in
+// sp[], handed between lanes through L2 (sc1 stores / loads, drained with vmcnt(0)).
+__device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
+  const uint32_t l = lane_id(), nrun = a.nrun, total = H.total;
+  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
+  auto kpos = [&](uint32_t r, uint32_t k, uint32_t& len) -> uint32_t {
+    const uint32_t g = H.lo[r] + k, p = a.key_off[g];
+    len = a.key_off[g + 1] - p;
+    return p;
+  };
+  auto lower = [&](uint32_t r, uint32_t xp, uint32_t xl) -> uint32_t {
+    uint32_t lo = 0, hi = H.tb[r + 1] - H.tb[r];
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      uint32_t ml;
+      const uint32_t mp = kpos(r, mid, ml);
+      if (key_cmp(G, mp, ml, xp, xl) < 0) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  auto ld = [](const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto stv = [](uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto drain = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+  };
+  for (uint32_t u = l; u < total; u += 64) {  // phase A: survival
+    const uint32_t r = find_run(H.tb, nrun, u), k = u - H.tb[r];
+    uint32_t xl;
+    const uint32_t xp = kpos(r, k, xl);
+    uint32_t sv = 1;
+    for (uint32_t r2 = 0; r2 < r && sv; ++r2) {
+      const uint32_t p = lower(r2, xp, xl);
+      if (p < H.tb[r2 + 1] - H.tb[r2]) {
+        uint32_t ql;
+        const uint32_t qp = kpos(r2, p, ql);
+        if (key_cmp(G, qp, ql, xp, xl) == 0) sv = 0;
+      }
+    }
+    stv(a.mrank + H.lo[r] + k, sv);
   }
   drain();
-  // survivor prefix over the tile (run-major order), then per-run bases and counts
-  uint32_t carry = 0;
+  uint32_t carry = 0;  // survivor prefix
   for (uint32_t c0 = 0; c0 < total; c0 += 64) {
     const uint32_t u = c0 + l;
-    uint32_t s = 0, g = 0;
+    uint32_t sv = 0, g = 0;
     if (u < total) {
-      const uint32_t r = find_run(L.tb, nrun, u);
-      g = L.lo[r] + u - L.tb[r];
-      s = get_surv(u, g);
+      const uint32_t r = find_run(H.tb, nrun, u);
+      g = H.lo[r] + u - H.tb[r];
+      sv = ld(a.mrank + g);
     }
-    const uint32_t inc = wave_incl_scan32(s);
-    if (u < total) set_sp(u, g, carry + inc - s);
+    const uint32_t inc = wave_incl_scan32(sv);
+    if (u < total) stv(a.sp + g, carry + inc - sv);
     carry += __builtin_amdgcn_readlane(inc, 63);
   }
   drain();
+  auto sp_at = [&](uint32_t u) -> uint32_t {  // prefix at tile index u (u == total: all)
+    if (u >= total) return carry;
+    const uint32_t r = find_run(H.tb, nrun, u);
+    return ld(a.sp + H.lo[r] + u - H.tb[r]);
+  };
   if (l < nrun) {
-    const uint32_t u0 = L.tb[l], u1 = L.tb[l + 1];
-    const uint32_t b0 = u0 < total ? get_sp(u0, L.lo[l]) : carry;
-    const uint32_t b1 = u1 < total ? get_sp(u1, L.lo[find_run(L.tb, nrun, u1)] + u1 - L.tb[find_run(L.tb, nrun, u1)])
-                                   : carry;
-    L.rsp[l] = b0;
-    L.rsv[l] = u1 > u0 ? b1 - b0 : 0u;
+    const uint32_t b0 = sp_at(H.tb[l]), b1 = sp_at(H.tb[l + 1]);
+    H.rsp[l] = b0;
+    H.rsv[l] = b1 - b0;
   }
-  if (l == 0) L.nsurv = carry;
   wave_sync();
-  // phase B: merged rank inside the tile = survivors with a smaller key in every other run +
-  // survivors before this entry in its own run (its group's earlier versions included)
-  for (uint32_t u = l; u < total; u += 64) {
-    const uint32_t r = find_run(L.tb, nrun, u), k = u - L.tb[r], g = L.lo[r] + k;
+  for (uint32_t u = l; u < total; u += 64) {  // phase B: rank
+    const uint32_t r = find_run(H.tb, nrun, u), k = u - H.tb[r], g = H.lo[r] + k;
     uint32_t rank = kNone;
-    if (get_surv(u, g)) {
+    if (ld(a.mrank + g)) {
       uint32_t xl;
       const uint32_t xp = kpos(r, k, xl);
-      rank = get_sp(u, g) - L.rsp[r];
+      rank = ld(a.sp + g) - H.rsp[r];
       for (uint32_t r2 = 0; r2 < nrun; ++r2) {
-        if (r2 == r) continue;
-        const uint32_t m2 = L.tb[r2 + 1] - L.tb[r2];
-        if (m2 == 0) continue;
+        const uint32_t m2 = H.tb[r2 + 1] - H.tb[r2];
+        if (r2 == r || m2 == 0) continue;
         const uint32_t p = lower(r2, xp, xl);
-        rank += p == m2 ? L.rsv[r2] : get_sp(L.tb[r2] + p, L.lo[r2] + p) - L.rsp[r2];
+        rank += p == m2 ? H.rsv[r2] : ld(a.sp + H.lo[r2] + p) - H.rsp[r2];
       }
     }
     a.mrank[g] = rank;  // each lane reads and rewrites only its own entries' words here
   }
-  if (l == 0) a.tcnt[t] = L.nsurv;
+  if (l == 0) a.tcnt[t] = carry;
 }
 
-__global__ __launch_bounds__(64) void merge_tile_kernel(MergeArgs a) {
+__global__ __launch_bounds__(kMTT) void merge_tile_kernel(MergeArgs a) {
   __shared__ MTileLds L;
   const uint32_t t = blockIdx.x;
   if (t >= uni(uint32_t(a.mstats[1]))) return;
-  tile_ranges(a, L, t, uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15));
-  if (L.total == 0) {
-    if (lane_id() == 0) a.tcnt[t] = 0;
+  if (threadIdx.x < 64) tile_ranges(a, L.h, t);
+  __syncthreads();
+  const uint32_t total = L.h.total;
+  if (total == 0) {
+    if (threadIdx.x == 0) a.tcnt[t] = 0;
     return;
   }
-  if (L.total <= kMTE && L.kb[a.nrun] <= kMTK) merge_tile<true>(a, L, t);
-  else merge_tile<false>(a, L, t);
+  if (total <= kMTE) {
+    merge_tile_lds(a, L, t);
+  } else if (threadIdx.x < 64) {
+    merge_tile_global(a, L.h, t);
+  }
 }
 
-// One workgroup: exclusive scan of the tile survivor counts (coalesced rounds of 1024 tiles).
+// One workgroup: exclusive scan of the tile survivor counts (rounds of 1024 threads x 16
+// consecutive tiles).
 __global__ __launch_bounds__(1024) void tile_scan_kernel(MergeArgs a) {
+  constexpr uint32_t kPer = 16;
   const uint32_t t = threadIdx.x, w = t >> 6;
   const uint32_t NC = uint32_t(a.mstats[1]);
   __shared__ uint64_t wsum[16];
   uint64_t carry = 0;
-  for (uint32_t r = 0; r < NC; r += 1024) {
-    const uint32_t i = r + t;
-    const uint64_t v = i < NC ? a.tcnt[i] : 0;
-    const uint64_t inc = wave_incl_scan<uint64_t>(v);
+  for (uint32_t r = 0; r < NC; r += 1024 * kPer) {
+    const uint32_t i0 = r + t * kPer;
+    uint32_t v[kPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      v[j] = i0 + j < NC ? a.tcnt[i0 + j] : 0u;
+      sum += v[j];
+    }
+    const uint64_t inc = wave_incl_scan<uint64_t>(sum);
     if (lane_id() == 63) wsum[w] = inc;
     __syncthreads();
     uint64_t base = carry, tot = carry;
@@ -406,7 +468,12 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(MergeArgs a) {
       if (x < w) base += wsum[x];
       tot += wsum[x];
     }
-    if (i < NC) a.tpre[i] = base + inc - v;
+    uint64_t run = base + inc - sum;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      if (i0 + j < NC) a.tpre[i0 + j] = run;
+      run += v[j];
+    }
     carry = tot;
     __syncthreads();
   }
@@ -417,15 +484,17 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(MergeArgs a) {
 }
 
 __global__ __launch_bounds__(64) void perm_kernel(MergeArgs a) {
-  __shared__ MTileLds L;
+  __shared__ TileHdr H;
   const uint32_t t = blockIdx.x;
   if (t >= uni(uint32_t(a.mstats[1]))) return;
-  tile_ranges(a, L, t, uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15));
+  tile_ranges(a, H, t);
+  wave_sync();
   const uint64_t base = a.tpre[t];
-  for (uint32_t u = lane_id(); u < L.total; u += 64) {
-    const uint32_t r = find_run(L.tb, a.nrun, u), g = L.lo[r] + u - L.tb[r];
+  const uint32_t cnt = a.tcnt[t];
+  for (uint32_t u = lane_id(); u < H.total; u += 64) {
+    const uint32_t r = find_run(H.tb, a.nrun, u), g = H.lo[r] + u - H.tb[r];
     const uint32_t k = a.mrank[g];
-    if (k < a.tcnt[t]) a.perm[base + k] = g;
+    if (k < cnt) a.perm[base + k] = g;
   }
 }
 
@@ -602,15 +671,57 @@ __device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, uint
   }
 }
 
+// len bytes from global src into the LDS image at dst (any alignment): 16-B pieces, the last
+// overlapping the one before; shorter runs by overlapping 8/4-byte or single-byte stores.
+__device__ __forceinline__ void lds_put(uint8_t* dst, const uint8_t* src, uint32_t len) {
+  if (len >= 16) {
+    for (uint32_t o = 0;; o += 16) {
+      const uint32_t p = o + 16 <= len ? o : len - 16;
+      *reinterpret_cast<u32x4*>(dst + p) = *reinterpret_cast<const u32x4*>(src + p);
+      if (p == len - 16) break;
+    }
+  } else if (len >= 8) {
+    *reinterpret_cast<u32x2*>(dst) = *reinterpret_cast<const u32x2*>(src);
+    *reinterpret_cast<u32x2*>(dst + len - 8) = *reinterpret_cast<const u32x2*>(src + len - 8);
+  } else if (len >= 4) {
+    *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
+    *reinterpret_cast<uint32_t*>(dst + len - 4) = *reinterpret_cast<const uint32_t*>(src + len - 4);
+  } else {
+    for (uint32_t x = 0; x < len; ++x) dst[x] = src[x];
+  }
+}
+
+// LDS image [lo, lo + len) -> global bytes at gdst_aligned + lo (lo < 16): aligned 16-B stores,
+// only the two edge chunks byte-masked.
+__device__ __forceinline__ void flush_img(uint8_t* gdst_aligned, const uint8_t* img, uint32_t lo, uint32_t len) {
+  const uint32_t end = lo + len, nc = (end + 15) >> 4;
+  for (uint32_t c = threadIdx.x; c < nc; c += blockDim.x) {
+    const u32x4 q = *reinterpret_cast<const u32x4*>(img + 16 * c);
+    const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+    const uint32_t a0 = 16 * c < lo ? lo - 16 * c : 0u;
+    const uint32_t a1 = min(end - 16 * c, 16u);
+    store_chunk(gdst_aligned + 16 * c, v, a0, a1);
+  }
+}
+
+constexpr uint32_t kGKImg = 6144;   // LDS image of a round's keys
+constexpr uint32_t kGVImg = 28672;  // LDS image of a round's values
+
+// Kept entries in merged order -> the output stream.  Per round of 256 merged positions the
+// kept keys and values form one contiguous output range each: lanes copy their entry's bytes
+// into LDS images of those ranges, which are then flushed with aligned, coalesced 16-B stores
+// (rounds whose ranges exceed the images copy lane by lane straight to global memory).
 __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
   if (a.stats[3]) return;
   const uint64_t N = *a.nm;
   __shared__ uint64_t ws[4][3];
+  __shared__ __attribute__((aligned(16))) uint8_t kimg[kGKImg + 32], vimg[kGVImg + 32];
   const uint32_t w = threadIdx.x >> 6;
   uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)], a.tile_pre[3 * uint64_t(blockIdx.x) + 1],
                        a.tile_pre[3 * uint64_t(blockIdx.x) + 2]};
   for (uint32_t sub = 0; sub < kGTile / 256; ++sub) {
     const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + threadIdx.x;
+    if (uint64_t(blockIdx.x) * kGTile + sub * 256 >= N) break;  // uniform
     const bool k = j < N && a.keep[j];
     const uint32_t i = k ? a.perm[j] : 0u;
     const uint32_t kl = k ? a.key_off[i + 1] - a.key_off[i] : 0u;
@@ -621,13 +732,28 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
     __syncthreads();
     uint64_t o = carry[0] + ic - 1, ko = carry[1] + ik - kl, vo = carry[2] + iv - vl;
     for (uint32_t q = 0; q < w; ++q) o += ws[q][0], ko += ws[q][1], vo += ws[q][2];
+    const uint64_t K0 = carry[1], V0 = carry[2];
 #pragma unroll
     for (uint32_t q = 0; q < 3; ++q) carry[q] += ws[0][q] + ws[1][q] + ws[2][q] + ws[3][q];
-    __syncthreads();
+    const uint64_t K1 = carry[1], V1 = carry[2];
+    __syncthreads();  // ws is rewritten by the next round
     if (k) {
       a.okey_off[o] = uint32_t(ko);
       a.oval_off[o] = uint32_t(vo);
       a.ots[o] = a.ts[i];
+    }
+    const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
+    const bool staged = K1 - K0 + kb <= kGKImg && V1 - V0 + vb <= kGVImg;
+    if (staged) {
+      if (k) {
+        lds_put(kimg + kb + (ko - K0), a.keys + a.key_off[i], kl);
+        lds_put(vimg + vb + (vo - V0), a.vals + a.val_off[i], vl);
+      }
+      __syncthreads();
+      flush_img(a.okeys + (K0 - kb), kimg, kb, uint32_t(K1 - K0));
+      flush_img(a.ovals + (V0 - vb), vimg, vb, uint32_t(V1 - V0));
+      __syncthreads();
+    } else if (k) {
       lane_copy(a.okeys + ko, a.keys + a.key_off[i], kl);
       lane_copy(a.ovals + vo, a.vals + a.val_off[i], vl);
     }
@@ -738,8 +864,11 @@ __global__ __launch_bounds__(256) void rot_adj_kernel(RotArgs a) {
   a.alcp[e] = al;
 }
 
+// Raise a level flag: one atomic per wave at most, none once the flag reads as set (hundreds
+// of thousands of waves OR-ing one word serialise at the memory side, ~12 ns each).
 __device__ __forceinline__ void or_need(uint32_t* flag, bool v) {
-  if (__ballot(v) && lane_id() == 0) atomicOr(flag, 1u);
+  if (__ballot(v) && lane_id() == 0 && !__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicOr(flag, 1u);
 }
 
 __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
@@ -965,7 +1094,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   hipLaunchKernelGGL(cand_rank_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   const uint64_t nb = (uint64_t(nc) + 1) * nrun;
   hipLaunchKernelGGL(bounds_kernel, dim3(uint32_t((nb + 255) / 256)), dim3(256), 0, st, m);
-  hipLaunchKernelGGL(merge_tile_kernel, dim3(nc), dim3(64), 0, st, m);
+  hipLaunchKernelGGL(merge_tile_kernel, dim3(nc), dim3(kMTT), 0, st, m);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, m);
   hipLaunchKernelGGL(perm_kernel, dim3(nc), dim3(64), 0, st, m);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;

@@ -322,6 +322,9 @@ struct lsmblk_ctx {
   // merge / compaction pipeline (lsmblk_compact.hip): one arena, carved per call
   uint8_t* cws = nullptr;
   uint64_t cws_cap = 0;
+  // CRC-verified decode (lsmblk_decode_batch_ex): per-block CRCs
+  uint32_t* vcrc = nullptr;
+  uint64_t vcrc_cap = 0;
 };
 
 namespace {

@@ -42,6 +42,8 @@ struct DecodeArgs {
   uint64_t* stats;
   const uint32_t* agg;        // per-block (entries, key bytes, value bytes), from dec_count_kernel
   const uint64_t* tile_pre;   // per-tile exclusive prefix (entries, key bytes, value bytes)
+  uint32_t tail;              // bytes after each block inside its range (4: the framing CRC)
+  uint64_t* blk_ent;          // optional: first entry index of every block
   uint32_t skip;  // ablation mask (lsmblk_debug_set, timing experiments only): 2 keys,
                   // 4 values, 8 per-entry metadata, 16 value pass 2, 32 value pass 1
 };
@@ -460,8 +462,8 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   const uint64_t tp0 = a.tile_pre[3 * tb], tp1 = a.tile_pre[3 * tb + 1], tp2 = a.tile_pre[3 * tb + 2];
   const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
   uint32_t len = 0;
-  if (end < start || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
-  else len = uint32_t(end - start);
+  if (end < start + a.tail || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
+  else len = uint32_t(end - start) - a.tail;
   const uint8_t* bp = a.blocks + start;
   const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
   const uint8_t* abase = bp - lead;
@@ -545,6 +547,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   excl[2] = tp2 + wave_sum(cv);
   wave_sync();
   const uint64_t E0 = excl[0], K0 = excl[1], V0 = excl[2];
+  if (a.blk_ent && l == 0) a.blk_ent[b] = E0;
   const uint64_t Et = E0 + agg[0], Kt = K0 + agg[1], Vt = V0 + agg[2];
   if (Kt > 0xFFFFFFFFull || Vt > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
   if (Et > a.entry_cap || Kt > a.key_cap || Vt > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
@@ -584,6 +587,7 @@ struct CountArgs {
   uint32_t* agg;        // 3 per block
   uint64_t* tile_sum;   // 3 per tile
   uint64_t* stats;
+  uint32_t tail;        // bytes after each block inside its range (4: the framing CRC)
 };
 
 __device__ __forceinline__ uint32_t gb16(const uint8_t* p, uint32_t i) {
@@ -604,8 +608,8 @@ __global__ __launch_bounds__(256) void dec_count_kernel(CountArgs a) {
     bool ok = true;
     if (b < a.nblk) {
       const uint64_t start = a.blk_off[b], end = a.blk_off[b + 1];
-      ok = end >= start && end - start <= 0x7FFFFFF0ull;
-      const uint32_t len = ok ? uint32_t(end - start) : 0u;
+      ok = end >= start + a.tail && end - start <= 0x7FFFFFF0ull;
+      const uint32_t len = ok ? uint32_t(end - start) - a.tail : 0u;
       const uint8_t* p = a.blocks + start;
       ok = ok && len >= 2;
       if (ok) {
@@ -691,6 +695,8 @@ struct ScanArgs {
   uint32_t* val_off;
   uint64_t entry_cap, key_cap, val_cap;
   uint64_t* stats;
+  uint64_t* blk_ent;   // optional: [nblk] = total entries
+  uint64_t nblk;
 };
 
 __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
@@ -732,6 +738,7 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
   }
   if (t == 1023) {
     const uint64_t N = part[1023][0], K = part[1023][1], V = part[1023][2];
+    if (a.blk_ent) a.blk_ent[a.nblk] = N;
     a.stats[0] = N;
     a.stats[1] = K;
     a.stats[2] = V;
@@ -1429,6 +1436,25 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
     emit_big(a, s, e - s, O, size, err);
   }
   raise_err(a.stats, err);
+}
+
+// read_block's check (src/table.rs:226-230): the BE u32 after every block must equal the
+// block's crc32fast.  A mismatch raises LSMBLK_ERR_CHECKSUM in the decode stats.
+__global__ __launch_bounds__(256) void crc_verify_kernel(const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
+                                                         const uint32_t* crc, const uint64_t* cstats, uint64_t* stats) {
+  const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  uint32_t err = 0;
+  if (b == 0 && cstats[3]) err |= LSMBLK_ERR_MALFORMED;
+  if (b < nblk) {
+    const uint64_t e = blk_off[b + 1];
+    if (e >= blk_off[b] + 4) {
+      const uint8_t* q = blocks + e - 4;
+      const uint32_t stored = (uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | q[3];
+      if (stored != crc[b]) err |= LSMBLK_ERR_CHECKSUM;
+    }
+  }
+  for (uint32_t d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
+  raise_err(stats, err);
 }
 
 __global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64_t cap) {
@@ -2191,6 +2217,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->filt_keep);
   (void)hipFree(c->filt_tile);
   (void)hipFree(c->cws);
+  (void)hipFree(c->vcrc);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2246,9 +2273,16 @@ int lsmblk_ctx_reserve(lsmblk_ctx* c, uint64_t max_blocks, uint64_t max_entries,
 
 int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
                         const lsmblk_kv_stream* out, uint64_t* stats, void* stream) {
+  return lsmblk_decode_batch_ex(c, blocks, blk_off, nblk, 0, 0, out, nullptr, stats, stream);
+}
+
+int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+                           uint32_t flags, const lsmblk_kv_stream* out, uint64_t* blk_ent, uint64_t* stats,
+                           void* stream) {
   if (!c || !blk_off || !out || !stats) return LSMBLK_E_INVAL;
   if (!aligned16(out->keys) || !aligned16(out->vals) || !out->key_off || !out->val_off) return LSMBLK_E_INVAL;
-  if (nblk >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
+  if (nblk >= 0xFFFFFFFFull || tail > 16) return LSMBLK_E_INVAL;
+  if ((flags & LSMBLK_DECODE_VERIFY_CRC) && tail != 4) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
   if (!dg.ok) return LSMBLK_E_HIP;
@@ -2258,7 +2292,21 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nblk == 0) {
     hipLaunchKernelGGL(finish_empty_decode, dim3(1), dim3(64), 0, st, out->key_off, out->val_off, out->entry_cap);
+    if (blk_ent && hipMemsetAsync(blk_ent, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  }
+  if (flags & LSMBLK_DECODE_VERIFY_CRC) {
+    // read_block's checksum test (src/table.rs:226-230) over the framed ranges, then the decode
+    if ((rc = ensure_crc_tabs(c))) return rc;
+    if ((rc = grow(&c->vcrc, &c->vcrc_cap, nblk + 1, 1))) return rc;
+    if (!c->meta_cstats && hipMalloc(reinterpret_cast<void**>(&c->meta_cstats), LSMBLK_STATS_WORDS * 8) != hipSuccess) {
+      c->meta_cstats = nullptr;
+      return LSMBLK_E_NOMEM;
+    }
+    if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    if ((rc = launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st))) return rc;
+    hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
+                       c->vcrc, c->meta_cstats, stats);
   }
   const uint64_t ntiles = (nblk + kTile - 1) / kTile;
   CountArgs ca;
@@ -2268,6 +2316,7 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   ca.agg = c->dec_agg;
   ca.tile_sum = c->tile_sum;
   ca.stats = stats;
+  ca.tail = tail;
   c->dec_timed = c->timing;
   if (c->timing) (void)hipEventRecord(c->ev[0], st);
   hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
@@ -2282,6 +2331,8 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   sa.key_cap = out->key_cap;
   sa.val_cap = out->val_cap;
   sa.stats = stats;
+  sa.blk_ent = blk_ent;
+  sa.nblk = nblk;
   hipLaunchKernelGGL(dec_scan_kernel, dim3(1), dim3(1024), 0, st, sa);
   if (c->timing) (void)hipEventRecord(c->ev[2], st);
   DecodeArgs a;
@@ -2299,6 +2350,8 @@ int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* bl
   a.stats = stats;
   a.agg = c->dec_agg;
   a.tile_pre = c->tile_pre;
+  a.tail = tail;
+  a.blk_ent = blk_ent;
   a.skip = c->skip;
   hipLaunchKernelGGL(decode_kernel, dim3(uint32_t(nblk)), dim3(64), 0, st, a);
   if (c->timing) (void)hipEventRecord(c->ev[3], st);

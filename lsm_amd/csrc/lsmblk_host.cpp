@@ -66,6 +66,7 @@ const char* lsmblk_strerror(int s) {
     case LSMBLK_E_TIMEOUT: return "device look-back timeout";
     case LSMBLK_E_OVERFLOW: return "batch exceeds u32 KV-stream offsets";
     case LSMBLK_E_INTERNAL: return "device self-check failed";
+    case LSMBLK_E_CHECKSUM: return "block checksum mismatched";
     default: return "unknown status";
   }
 }
@@ -75,6 +76,7 @@ int lsmblk_stats_status(uint64_t f) {
   if (f & LSMBLK_ERR_INTERNAL) return LSMBLK_E_INTERNAL;
   if (f & LSMBLK_ERR_SEGMENTS) return LSMBLK_E_INVAL;
   if (f & LSMBLK_ERR_EMPTY_KEY) return LSMBLK_E_INVAL;
+  if (f & LSMBLK_ERR_CHECKSUM) return LSMBLK_E_CHECKSUM;
   if (f & LSMBLK_ERR_MALFORMED) return LSMBLK_E_MALFORMED;
   if (f & LSMBLK_ERR_OVERFLOW) return LSMBLK_E_OVERFLOW;
   if (f & LSMBLK_ERR_CAPACITY) return LSMBLK_E_CAPACITY;

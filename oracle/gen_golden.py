@@ -42,6 +42,30 @@ def cases():
     yield "u16_wrap_oversize", O.KV.from_entries(ents), [0, 4], 4096
 
 
+def compaction_cases():
+    """Merge + compaction vectors from the line-by-line restatement (oracle/pyref.py:
+    MergeIterator, compact_generate_sst): runs, options, and every SST's blocks."""
+    from oracle import pyref
+    rng = np.random.default_rng(11)
+    space = sorted({b"k%04d" % int(rng.integers(0, 900)) + bytes(rng.integers(97, 100, int(rng.integers(0, 3)),
+                                                                              dtype=np.uint8))
+                    for _ in range(700)})
+    runs = []
+    for r in range(5):
+        take = sorted(rng.choice(len(space), size=int(rng.integers(100, len(space))), replace=False))
+        run = []
+        for i in take:
+            for t in sorted(rng.choice(1000, size=int(rng.integers(1, 4)), replace=False), reverse=True):
+                run.append((space[i], int(t) + 1000 * (5 - r), b"" if rng.random() < 0.15 else b"r%d-%d" % (r, t)))
+        runs.append(run)
+    for name, wm, bottom, pf, bs, target in (("compact_runs_bottom", 3500, True, (b"k00",), 256, 3000),
+                                              ("compact_runs_upper", 2500, False, (), 512, 6000)):
+        ssts = pyref.compact_generate_sst(pyref.MergeIterator([pyref.ListIter(x) for x in runs]), wm, bottom, pf,
+                                          bs, target)
+        yield name, runs, dict(watermark=wm, bottom_level=bottom, prefixes=[p.decode() for p in pf],
+                               block_size=bs, target_sst_size=target), ssts
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     meta = {}
@@ -55,6 +79,21 @@ def main():
                       "bytes": int(len(blocks)), "crc32": zlib.crc32(blocks.tobytes())}
     with open(os.path.join(OUT, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
+    cmeta = {}
+    for name, runs, opts, ssts in compaction_cases():
+        kv = O.KV.from_entries([e for r in runs for e in r])
+        rs = np.concatenate([[0], np.cumsum([len(r) for r in runs])]).astype(np.uint32)
+        blocks = [b for sst, _ in ssts for b in sst]
+        blk_off = np.concatenate([[0], np.cumsum([len(b) for b in blocks])]).astype(np.uint64)
+        sst_blk = np.concatenate([[0], np.cumsum([len(s) for s, _ in ssts])]).astype(np.uint32)
+        sst_ent = np.concatenate([[0], np.cumsum([len(e) for _, e in ssts])]).astype(np.uint32)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=kv.keys, key_off=kv.key_off, vals=kv.vals,
+                            val_off=kv.val_off, ts=kv.ts, run_start=rs,
+                            blocks=np.frombuffer(b"".join(blocks), np.uint8), blk_off=blk_off, sst_blk=sst_blk,
+                            sst_ent=sst_ent)
+        cmeta[name] = dict(opts, ssts=len(ssts), blocks=len(blocks), entries=int(kv.n))
+    with open(os.path.join(OUT, "golden_compaction.json"), "w") as f:
+        json.dump(cmeta, f, indent=1, sort_keys=True)
     src = "/root/reference/lsm.db/MANIFEST"
     if os.path.exists(src):
         shutil.copyfile(src, os.path.join(OUT, "lsm_db_MANIFEST.bin"))

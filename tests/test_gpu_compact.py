@@ -213,3 +213,43 @@ def test_compact_nothing_kept_and_capacity():
     batch.compact_into(d, batch._u32_table(rs, "cuda"), 3, batch.compact_opts(0, False, (), 4096, 4096), buf)
     torch.cuda.synchronize()
     assert batch._status(buf.stats) == -3  # LSMBLK_E_CAPACITY: more SSTs than sst_cap - 1
+
+
+def test_compaction_golden_fixtures_through_hip():
+    """tests/golden/compact_runs_*.npz (the line-by-line restatement's SSTs) through
+    lsmblk_compact_batch."""
+    import json
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    meta = json.load(open(os.path.join(g, "golden_compaction.json")))
+    for name, m in meta.items():
+        z = np.load(os.path.join(g, name + ".npz"))
+        kv = O.KV(z["keys"], z["key_off"], z["vals"], z["val_off"], z["ts"])
+        got = batch.compact_runs(to_dev(kv), z["run_start"], m["watermark"], m["bottom_level"],
+                                 [p.encode() for p in m["prefixes"]], m["block_size"], m["target_sst_size"])
+        np.testing.assert_array_equal(got["blocks"].cpu().numpy(), z["blocks"], err_msg=name)
+        np.testing.assert_array_equal(got["blk_off"].cpu().numpy().view(np.uint64), z["blk_off"])
+        np.testing.assert_array_equal(got["sst_blk"].cpu().numpy().view(np.uint32), z["sst_blk"])
+        np.testing.assert_array_equal(got["sst_start"].cpu().numpy().view(np.uint32), z["sst_ent"])
+
+
+def test_decode_runs_then_merge_with_block_entry_index():
+    """The compaction read path: every run's SSTs decoded in ONE call, run boundaries from the
+    decode's per-block entry index, then the merge (== C oracle)."""
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(40000, nrun=5, seed=4, versions=2)
+    kv = O.KV(keys, ko, vals, vo, ts)
+    parts, offs, run_blk, base = [], [], [0], 0
+    for r in range(5):
+        sub = O.gather(kv, np.arange(rs[r], rs[r + 1]))
+        rc, b, o = O.encode_segments(sub, synth.segments_by_bytes(sub.key_off, sub.val_off, 64 << 10), 4096)
+        parts.append(b)
+        offs.append(o[:-1] + base)
+        base += len(b)
+        run_blk.append(run_blk[-1] + len(o) - 1)
+    blocks = np.concatenate(parts)
+    blk_off = np.concatenate(offs + [np.array([base], np.uint64)])
+    db, do = torch.from_numpy(blocks).cuda(), torch.from_numpy(blk_off.view(np.int64)).cuda()
+    d, ent = batch.decode_blocks(db, do, with_blk_ent=True)
+    run_start = ent[torch.tensor(run_blk, device="cuda")].to(torch.int32)
+    np.testing.assert_array_equal(run_start.cpu().numpy(), rs.astype(np.int32))
+    assert_kv_equal(batch.merge_runs(d, run_start), O.gather(kv, O.merge_runs(kv, rs)))

@@ -476,3 +476,51 @@ def test_compact_filter_many_tiles_against_loop():
     pf = (ents[5][0][:1],)
     got = batch.compact_filter(to_dev(O.KV.from_entries(ents)), 1 << 19, True, pf)
     assert_kv_equal(got, O.KV.from_entries(pyref.compact_filter_loop(ents, 1 << 19, True, pf)))
+
+
+def test_golden_fixtures_through_hip():
+    """Every committed block fixture (tests/golden/*.npz) replayed through the HIP path: GPU encode
+    of the fixture's KV stream == its blocks, GPU decode of its blocks == the oracle's decode."""
+    import json
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    meta = json.load(open(os.path.join(g, "golden.json")))
+    for name, m in meta.items():
+        z = np.load(os.path.join(g, name + ".npz"))
+        kv = O.KV(z["keys"], z["key_off"], z["vals"], z["val_off"], z["ts"])
+        blocks, blk_off = batch.encode_kv(to_dev(kv), z["seg_start"], m["block_size"])
+        np.testing.assert_array_equal(blk_off.cpu().numpy().view(np.uint64), z["blk_off"], err_msg=name)
+        np.testing.assert_array_equal(blocks.cpu().numpy(), z["blocks"], err_msg=name)
+        # decode is compared with the oracle's decode of the blocks: an `as u16`-wrapped value
+        # length (u16_wrap_oversize) reads back shorter than it was written, as in the reference
+        rc, ref_kv = O.decode_blocks(z["blocks"], z["blk_off"])
+        assert rc == 0
+        db, do = dev_blocks(z["blocks"], z["blk_off"], 1)
+        assert_kv_equal(batch.decode_blocks(db, do), ref_kv)
+
+
+def test_decode_framed_section_verify_crc_and_block_entries():
+    """lsmblk_decode_batch_ex over a framed SST data section (block || BE u32 crc32fast, the
+    BlockMeta offsets): tail = 4, the read_block checksum test, and the per-block entry index."""
+    from lsm_amd._lib import LSMBLK_E_CHECKSUM
+    kv = O.KV(*synth.gen_uniform(30000, seed=19))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 256 << 10)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, 4096)
+    parts, off = [], [0]
+    for i in range(len(ref_off) - 1):
+        blk = ref_blocks[int(ref_off[i]):int(ref_off[i + 1])].tobytes()
+        parts.append(blk + zlib.crc32(blk).to_bytes(4, "big"))
+        off.append(off[-1] + len(parts[-1]))
+    framed = np.frombuffer(b"".join(parts), np.uint8).copy()
+    db, do = dev_blocks(framed, np.array(off, np.uint64), 7)
+    got, ent = batch.decode_blocks(db, do, tail=4, verify=True, with_blk_ent=True)
+    assert_kv_equal(got, kv)
+    counts = [int.from_bytes(ref_blocks[int(ref_off[i + 1]) - 2:int(ref_off[i + 1])].tobytes(), "big")
+              for i in range(len(ref_off) - 1)]
+    np.testing.assert_array_equal(ent.cpu().numpy(), np.concatenate([[0], np.cumsum(counts)]))
+    bad = framed.copy()
+    bad[off[17] - 1] ^= 0x40  # one stored checksum byte
+    db, do = dev_blocks(bad, np.array(off, np.uint64))
+    with pytest.raises(LsmBlkError) as e:
+        batch.decode_blocks(db, do, tail=4, verify=True)
+    assert e.value.status == LSMBLK_E_CHECKSUM

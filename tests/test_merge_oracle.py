@@ -167,3 +167,23 @@ def test_rotation_closed_form_on_kept_stream():
             kept = O.gather(kv, src[got["kept"]])
             seg = O.segment_like_compaction(kept, 4096, target)
             np.testing.assert_array_equal(seg, got["sst_ent"])
+
+
+def test_compaction_golden_fixtures_c_oracle():
+    """tests/golden/compact_runs_*.npz (made by oracle/gen_golden.py from the line-by-line
+    restatement) replayed through the C oracle."""
+    import json
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    meta = json.load(open(os.path.join(g, "golden_compaction.json")))
+    for name, m in meta.items():
+        z = np.load(os.path.join(g, name + ".npz"))
+        kv = O.KV(z["keys"], z["key_off"], z["vals"], z["val_off"], z["ts"])
+        src = O.merge_runs(kv, z["run_start"])
+        got = O.compact(kv, src, m["watermark"], m["bottom_level"], [p.encode() for p in m["prefixes"]],
+                        m["block_size"], m["target_sst_size"])
+        np.testing.assert_array_equal(got["blocks"], z["blocks"])
+        np.testing.assert_array_equal(got["blk_off"], z["blk_off"])
+        np.testing.assert_array_equal(got["sst_blk"], z["sst_blk"])
+        np.testing.assert_array_equal(got["sst_ent"], z["sst_ent"])
+        assert len(got["sst_blk"]) - 1 == m["ssts"]
