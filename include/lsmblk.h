@@ -305,6 +305,47 @@ int lsmblk_compact_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint
                          uint64_t out_cap, uint64_t* blk_off, uint64_t blk_cap, uint32_t* sst_start,
                          uint32_t* sst_blk, uint32_t sst_cap, uint64_t* stats, void* stream);
 
+/* ------------------------------------------------------------------ memtable (§8 f row 4, host) */
+/* MemTable (src/mem_table.rs:55-158): an ordered map keyed by the key bytes only (Key's Ord ignores
+ * the ts, src/key.rs:63-81), so put() of a present key replaces the entry; flush() (:131-136) yields
+ * the entries in key order -- the flush source the device encoder consumes (lsmblk_encode_batch,
+ * then lsmblk_sst_files_batch).  Host memory; thread-safe per memtable. */
+typedef struct lsmblk_memtable lsmblk_memtable;
+lsmblk_memtable* lsmblk_memtable_new(void);
+void lsmblk_memtable_free(lsmblk_memtable* m);
+int lsmblk_memtable_put(lsmblk_memtable* m, const uint8_t* key, size_t klen, uint64_t ts, const uint8_t* val,
+                        size_t vlen);                                                  /* :113-127 */
+/* 1 = found (*val valid until the next put), 0 = absent (:93-99). */
+int lsmblk_memtable_get(lsmblk_memtable* m, const uint8_t* key, size_t klen, const uint8_t** val, size_t* vlen,
+                        uint64_t* ts);
+size_t lsmblk_memtable_len(lsmblk_memtable* m);
+size_t lsmblk_memtable_approximate_size(lsmblk_memtable* m);                          /* :154-157 */
+/* The entries in key order as a SoA KV stream in host buffers (flush, :131-136); *n / *kbytes /
+ * *vbytes report the sizes (LSMBLK_E_CAPACITY when a buffer is too small). */
+int lsmblk_memtable_flush(lsmblk_memtable* m, uint8_t* keys, uint32_t* key_off, uint8_t* vals, uint32_t* val_off,
+                          uint64_t* ts, uint64_t entry_cap, uint64_t key_cap, uint64_t val_cap, uint64_t* n,
+                          uint64_t* kbytes, uint64_t* vbytes);
+
+/* ------------------------------------------------------------------ SST container (§8 f row 3) */
+/* Whole SST files as SsTableBuilder::build writes them (src/table/builder.rs:68-98), for the nsst
+ * SSTs of an encode or compaction: SST s = blocks [sst_blk[s], sst_blk[s+1]) of (blocks, blk_off)
+ * (packed, as lsmblk_encode_batch / lsmblk_compact_batch write them), holding the entries
+ * [sst_ent[s], sst_ent[s+1]) of `kv` -- the entries handed to SsTableBuilder::add, whose
+ * fingerprint32 hashes fill the bloom filter (:53, src/table/bloom.rs:72-101).  File s =
+ * files[file_off[s] .. file_off[s+1]) (file_off: device u64[nsst+1]):
+ *   every block followed by its BE u32 crc32fast | BlockMeta section | BE u32 meta_offset |
+ *   filter | k | BE u32 crc32fast(filter | k) | BE u32 bloom_offset.
+ * sst_blk / sst_ent: device u32[nsst+1].  stats: [0] nsst [1] bytes (required on CAPACITY)
+ * [3] error flags.  Synchronizes once (reads the key arena size to bound the workspace). */
+int lsmblk_sst_files_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
+                           const uint32_t* sst_blk, const uint32_t* sst_ent, uint32_t nsst,
+                           const lsmblk_kv_stream* kv, uint8_t* files, uint64_t files_cap, uint64_t* file_off,
+                           uint64_t* stats, void* stream);
+/* farmhash::fingerprint32 (the key hash of SsTableBuilder::add, src/table/builder.rs:53), host. */
+uint32_t lsmblk_fingerprint32(const uint8_t* key, size_t klen);
+/* Bloom::may_contain (src/table/bloom.rs:104-120) over a decoded filter, host. */
+int lsmblk_bloom_may_contain(const uint8_t* filter, size_t nbytes, uint32_t k, uint32_t h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SO = os.path.join(PKG, "liblsmblk.so")
-SOURCES = [os.path.join(PKG, "csrc", f) for f in ("lsmblk_gpu.hip", "lsmblk_compact.hip", "lsmblk_host.cpp")]
+SOURCES = [os.path.join(PKG, "csrc", f) for f in ("lsmblk_gpu.hip", "lsmblk_compact.hip", "lsmblk_sst.hip", "lsmblk_host.cpp")]
 HEADERS = [os.path.join(ROOT, "include", "lsmblk.h"), os.path.join(PKG, "csrc", "lsmblk_dev.hpp")]
 
 

@@ -87,6 +87,17 @@ SIGNATURES = [
     ("lsmblk_sst_rotation_batch", I, [P, ctypes.POINTER(KVStreamC), U32, U64, P, U32, P, P]),
     ("lsmblk_compact_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
                                  ctypes.POINTER(KVStreamC), P, U64, P, U64, P, P, U32, P, P]),
+    ("lsmblk_memtable_new", P, []),
+    ("lsmblk_memtable_free", None, [P]),
+    ("lsmblk_memtable_put", I, [P, P, S, U64, P, S]),
+    ("lsmblk_memtable_get", I, [P, P, S, PP, ctypes.POINTER(S), ctypes.POINTER(U64)]),
+    ("lsmblk_memtable_len", S, [P]),
+    ("lsmblk_memtable_approximate_size", S, [P]),
+    ("lsmblk_memtable_flush", I, [P, P, P, P, P, P, U64, U64, U64, ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                  ctypes.POINTER(U64)]),
+    ("lsmblk_sst_files_batch", I, [P, P, P, U64, P, P, U32, ctypes.POINTER(KVStreamC), P, U64, P, P, P]),
+    ("lsmblk_fingerprint32", U32, [P, S]),
+    ("lsmblk_bloom_may_contain", I, [P, S, U32, U32]),
 ]
 
 

@@ -281,6 +281,94 @@ __device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4]
 }
 }  // namespace
 
+
+// ---------------------------------------------------------------- CRC-32 (crc32fast) tables
+namespace {
+constexpr uint32_t kCrcChunk = 4096;
+constexpr uint32_t kCrcMats = 7;  // Z(., 64 << j), j = 0..5, and j = 6: a whole chunk
+constexpr uint32_t kCrcStage = 5 * 1024;  // five 1-KiB load pieces (lead + chunk <= 4111 B)
+struct alignas(16) CrcTabs {
+  uint32_t fold[8][16];              // R_0 after xoring a dword into the register: by nibble
+  uint32_t shift[kCrcMats][8][16];   // Z(., 64 << j) by nibble of the register
+  uint32_t nib[16];                  // one 4-bit step (leading odd bytes of a segment)
+};
+
+__device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[8][16], uint32_t x) {
+  return (m[0][x & 15] ^ m[1][(x >> 4) & 15]) ^ (m[2][(x >> 8) & 15] ^ m[3][(x >> 12) & 15]) ^
+         (m[4][(x >> 16) & 15] ^ m[5][(x >> 20) & 15]) ^ (m[6][(x >> 24) & 15] ^ m[7][x >> 28]);
+}
+
+// R over the chunk bytes p[0, sz) (LDS), 0 < sz <= kCrcChunk; the block's first chunk
+// starts from the CRC init.  Every lane returns the chunk's register.
+__device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p, uint32_t sz, bool first) {
+  const uint32_t l = lane_id();
+  const uint32_t nseg = (sz + 63) >> 6, l0 = 64 - nseg, r = sz - 64 * (nseg - 1);
+  uint32_t crc = 0;
+  if (l >= l0) {
+    const uint32_t so = l == l0 ? 0u : r + 64 * (l - l0 - 1), sn = l == l0 ? r : 64u;
+    crc = first && l == l0 ? 0xFFFFFFFFu : 0u;
+    const uint8_t* q = p + so;
+    const uint32_t nb = sn & 3;
+    for (uint32_t i = 0; i < nb; ++i) {
+      crc ^= q[i];
+      crc = T.nib[crc & 15] ^ (crc >> 4);
+      crc = T.nib[crc & 15] ^ (crc >> 4);
+    }
+#pragma unroll 4
+    for (uint32_t i = nb; i < sn; i += 4) crc = crc_apply(T.fold, crc ^ *reinterpret_cast<const uint32_t*>(q + i));
+    const uint32_t m = 63 - l;  // full segments after this one
+#pragma unroll
+    for (uint32_t j = 0; j < 6; ++j)
+      if ((m >> j) & 1) crc = crc_apply(T.shift[j], crc);
+  }
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) crc ^= __shfl_xor(crc, d, 64);
+  return crc;
+}
+
+// Persistent waves, one block at a time, the next chunk's loads in flight while the current
+// one is folded.  A block of len bytes has ceil(len / 4096) chunks; the first holds the
+// len mod 4096 remainder (or a full 4096), so every later chunk is full.
+}  // namespace
+namespace {
+// CRC tables (host).  Each linear map of the 32-bit register is tabulated by its columns
+// (the images of the 32 unit vectors), then as eight nibble tables.
+inline uint32_t crc_bit_step(uint32_t c) { return (c >> 1) ^ ((c & 1) ? 0xEDB88320u : 0u); }
+inline void crc_nibble_tables(const uint32_t (&col)[32], uint32_t (&m)[8][16]) {
+  for (uint32_t k = 0; k < 8; ++k)
+    for (uint32_t v = 0; v < 16; ++v) {
+      uint32_t y = 0;
+      for (uint32_t bit = 0; bit < 4; ++bit)
+        if ((v >> bit) & 1) y ^= col[4 * k + bit];
+      m[k][v] = y;
+    }
+}
+inline void crc_host_tables(CrcTabs& T) {
+  for (uint32_t v = 0; v < 16; ++v) {
+    uint32_t c = v;
+    for (int s = 0; s < 4; ++s) c = crc_bit_step(c);
+    T.nib[v] = c;
+  }
+  uint32_t col[32];
+  for (uint32_t bit = 0; bit < 32; ++bit) {  // fold: 32 bit steps (4 zero bytes after the xor)
+    uint32_t x = 1u << bit;
+    for (int s = 0; s < 32; ++s) x = crc_bit_step(x);
+    col[bit] = x;
+  }
+  crc_nibble_tables(col, T.fold);
+  for (uint32_t j = 0; j < kCrcMats; ++j) {  // Z(., 64 << j): 8 (64 << j) bit steps
+    const uint32_t steps = 8u * (64u << j);
+    for (uint32_t bit = 0; bit < 32; ++bit) {
+      uint32_t x = 1u << bit;
+      for (uint32_t s = 0; s < steps; ++s) x = crc_bit_step(x);
+      col[bit] = x;
+    }
+    crc_nibble_tables(col, T.shift[j]);
+  }
+}
+
+}  // namespace
+
 struct lsmblk_ctx {
   int device = 0;
   std::mutex mu;
@@ -325,6 +413,9 @@ struct lsmblk_ctx {
   // CRC-verified decode (lsmblk_decode_batch_ex): per-block CRCs
   uint32_t* vcrc = nullptr;
   uint64_t vcrc_cap = 0;
+  // SST files (lsmblk_sst.hip)
+  uint8_t* sws = nullptr;
+  uint64_t sws_cap = 0;
 };
 
 namespace {
@@ -383,4 +474,12 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
 // lsmblk_encode_segment_blocks for the encode that just ran on this context.
 int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
                           uint32_t* seg_blk, hipStream_t st);
+// CRC tables on the context (first use) and the crc_kernel launch over [blk_off[b], blk_off[b+1] - tail).
+int ensure_crc_tabs(lsmblk_ctx* c);
+int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+               uint32_t* crc, uint64_t* stats, hipStream_t st);
+// lsmblk_block_meta_batch with the context lock held.
+int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+                      const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off,
+                      uint64_t* stats, hipStream_t st);
 }  // namespace lsmblk_impl

@@ -1484,15 +1484,6 @@ __global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64
 // distinct banks (repeats broadcast), so lookups are conflict-free.  256-entry byte tables
 // put 64 random lanes on 32 banks and measured 1.6 TB/s; 4 KiB of nibble tables also leave
 // room for more resident workgroups.
-constexpr uint32_t kCrcChunk = 4096;
-constexpr uint32_t kCrcMats = 7;  // Z(., 64 << j), j = 0..5, and j = 6: a whole chunk
-constexpr uint32_t kCrcStage = 5 * 1024;  // five 1-KiB load pieces (lead + chunk <= 4111 B)
-struct alignas(16) CrcTabs {
-  uint32_t fold[8][16];              // R_0 after xoring a dword into the register: by nibble
-  uint32_t shift[kCrcMats][8][16];   // Z(., 64 << j) by nibble of the register
-  uint32_t nib[16];                  // one 4-bit step (leading odd bytes of a segment)
-};
-
 struct CrcArgs {
   const uint8_t* blocks;
   const uint64_t* blk_off;
@@ -1503,42 +1494,6 @@ struct CrcArgs {
   uint64_t* stats;
 };
 
-__device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[8][16], uint32_t x) {
-  return (m[0][x & 15] ^ m[1][(x >> 4) & 15]) ^ (m[2][(x >> 8) & 15] ^ m[3][(x >> 12) & 15]) ^
-         (m[4][(x >> 16) & 15] ^ m[5][(x >> 20) & 15]) ^ (m[6][(x >> 24) & 15] ^ m[7][x >> 28]);
-}
-
-// R over the chunk bytes p[0, sz) (LDS), 0 < sz <= kCrcChunk; the block's first chunk
-// starts from the CRC init.  Every lane returns the chunk's register.
-__device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p, uint32_t sz, bool first) {
-  const uint32_t l = lane_id();
-  const uint32_t nseg = (sz + 63) >> 6, l0 = 64 - nseg, r = sz - 64 * (nseg - 1);
-  uint32_t crc = 0;
-  if (l >= l0) {
-    const uint32_t so = l == l0 ? 0u : r + 64 * (l - l0 - 1), sn = l == l0 ? r : 64u;
-    crc = first && l == l0 ? 0xFFFFFFFFu : 0u;
-    const uint8_t* q = p + so;
-    const uint32_t nb = sn & 3;
-    for (uint32_t i = 0; i < nb; ++i) {
-      crc ^= q[i];
-      crc = T.nib[crc & 15] ^ (crc >> 4);
-      crc = T.nib[crc & 15] ^ (crc >> 4);
-    }
-#pragma unroll 4
-    for (uint32_t i = nb; i < sn; i += 4) crc = crc_apply(T.fold, crc ^ *reinterpret_cast<const uint32_t*>(q + i));
-    const uint32_t m = 63 - l;  // full segments after this one
-#pragma unroll
-    for (uint32_t j = 0; j < 6; ++j)
-      if ((m >> j) & 1) crc = crc_apply(T.shift[j], crc);
-  }
-#pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) crc ^= __shfl_xor(crc, d, 64);
-  return crc;
-}
-
-// Persistent waves, one block at a time, the next chunk's loads in flight while the current
-// one is folded.  A block of len bytes has ceil(len / 4096) chunks; the first holds the
-// len mod 4096 remainder (or a full 4096), so every later chunk is full.
 __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   __shared__ CrcTabs T;
   __shared__ __attribute__((aligned(16))) uint8_t stage[4][kCrcStage];
@@ -1615,43 +1570,7 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   raise_err(a.stats, err);
 }
 
-}  // namespace
-
-// CRC tables (host).  Each linear map of the 32-bit register is tabulated by its columns
-// (the images of the 32 unit vectors), then as eight nibble tables.
-static uint32_t crc_bit_step(uint32_t c) { return (c >> 1) ^ ((c & 1) ? 0xEDB88320u : 0u); }
-static void crc_nibble_tables(const uint32_t (&col)[32], uint32_t (&m)[8][16]) {
-  for (uint32_t k = 0; k < 8; ++k)
-    for (uint32_t v = 0; v < 16; ++v) {
-      uint32_t y = 0;
-      for (uint32_t bit = 0; bit < 4; ++bit)
-        if ((v >> bit) & 1) y ^= col[4 * k + bit];
-      m[k][v] = y;
-    }
-}
-static void crc_host_tables(CrcTabs& T) {
-  for (uint32_t v = 0; v < 16; ++v) {
-    uint32_t c = v;
-    for (int s = 0; s < 4; ++s) c = crc_bit_step(c);
-    T.nib[v] = c;
-  }
-  uint32_t col[32];
-  for (uint32_t bit = 0; bit < 32; ++bit) {  // fold: 32 bit steps (4 zero bytes after the xor)
-    uint32_t x = 1u << bit;
-    for (int s = 0; s < 32; ++s) x = crc_bit_step(x);
-    col[bit] = x;
-  }
-  crc_nibble_tables(col, T.fold);
-  for (uint32_t j = 0; j < kCrcMats; ++j) {  // Z(., 64 << j): 8 (64 << j) bit steps
-    const uint32_t steps = 8u * (64u << j);
-    for (uint32_t bit = 0; bit < 32; ++bit) {
-      uint32_t x = 1u << bit;
-      for (uint32_t s = 0; s < steps; ++s) x = crc_bit_step(x);
-      col[bit] = x;
-    }
-    crc_nibble_tables(col, T.shift[j]);
-  }
-}
+}  // namespace lsmblk_impl
 
 // ---------------------------------------------------------------- SST BlockMeta section
 // SsTableBuilder::build -> BlockMeta::encode_block_meta (src/table.rs:29-63), one section per
@@ -2169,11 +2088,8 @@ int next_epoch(lsmblk_ctx* c, hipStream_t st) {
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-int ensure_crc_tabs(lsmblk_ctx* c);
-int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
-               uint32_t* crc, uint64_t* stats, hipStream_t st);
 
-}  // namespace
+}  // namespace lsmblk_impl
 
 extern "C" {
 
@@ -2218,6 +2134,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->filt_tile);
   (void)hipFree(c->cws);
   (void)hipFree(c->vcrc);
+  (void)hipFree(c->sws);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2297,14 +2214,14 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   }
   if (flags & LSMBLK_DECODE_VERIFY_CRC) {
     // read_block's checksum test (src/table.rs:226-230) over the framed ranges, then the decode
-    if ((rc = ensure_crc_tabs(c))) return rc;
+    if ((rc = lsmblk_impl::ensure_crc_tabs(c))) return rc;
     if ((rc = grow(&c->vcrc, &c->vcrc_cap, nblk + 1, 1))) return rc;
     if (!c->meta_cstats && hipMalloc(reinterpret_cast<void**>(&c->meta_cstats), LSMBLK_STATS_WORDS * 8) != hipSuccess) {
       c->meta_cstats = nullptr;
       return LSMBLK_E_NOMEM;
     }
     if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-    if ((rc = launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st))) return rc;
+    if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st))) return rc;
     hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
                        c->vcrc, c->meta_cstats, stats);
   }
@@ -2469,12 +2386,12 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
   if (!dg.ok) return LSMBLK_E_HIP;
-  int rc = ensure_crc_tabs(c);
+  int rc = lsmblk_impl::ensure_crc_tabs(c);
   if (rc) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nblk == 0) return LSMBLK_OK;
-  return launch_crc(c, blocks, blk_off, nblk, tail, crc, stats, st);
+  return lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, crc, stats, st);
 }
 
 int lsmblk_encode_segment_blocks(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg, const uint64_t* enc_stats,
@@ -2498,7 +2415,17 @@ int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
   if (!dg.ok) return LSMBLK_E_HIP;
-  int rc = ensure_crc_tabs(c);
+  return lsmblk_impl::block_meta_locked(c, blocks, blk_off, nblk, tail, seg_blk, nseg, meta, meta_cap, meta_off,
+                                        stats, reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"
+
+namespace lsmblk_impl {
+int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+                      const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off,
+                      uint64_t* stats, hipStream_t st) {
+  int rc = lsmblk_impl::ensure_crc_tabs(c);
   if (rc) return rc;
   const uint64_t ntiles = (nblk + kMetaTile - 1) / kMetaTile;
   if (nblk + 1 > c->meta_blk_cap) {
@@ -2514,7 +2441,6 @@ int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t
     c->meta_cstats = nullptr;
     return LSMBLK_E_NOMEM;
   }
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   MetaArgs a;
   a.blocks = blocks;
@@ -2541,10 +2467,13 @@ int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   // section CRC over [meta_off[s] + 4, meta_off[s+1] - 4): blocks = meta + 4, tail = 8
   if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  if ((rc = launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st))) return rc;
+  if ((rc = lsmblk_impl::launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st))) return rc;
   hipLaunchKernelGGL(meta_crc_put_kernel, dim3(sg), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
+}  // namespace lsmblk_impl
+
+extern "C" {
 
 int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint64_t watermark, int bottom_level,
                                 const uint8_t* prefixes, const uint32_t* prefix_off, uint32_t nprefix,
@@ -2593,7 +2522,7 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
 
 }  // extern "C"
 
-namespace {
+namespace lsmblk_impl {
 int ensure_crc_tabs(lsmblk_ctx* c) {
   if (c->crc_tabs) return LSMBLK_OK;
   CrcTabs h;
@@ -2624,4 +2553,4 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
   hipLaunchKernelGGL(crc_kernel, dim3(uint32_t(want < cap ? want : cap)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
-}  // namespace
+}  // namespace lsmblk_impl lsmblk_impl

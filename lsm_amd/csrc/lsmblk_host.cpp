@@ -346,3 +346,101 @@ void lsmblk_iter_free(lsmblk_iter* it) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- memtable (flush source)
+// MemTable (src/mem_table.rs:55-158): a crossbeam SkipMap<KeyBytes, Bytes> whose key order
+// ignores the ts (src/key.rs:63-81), so a put of a key that is present replaces the entry (key,
+// ts and value); flush (:131-136) walks the map in key order into SsTableBuilder::add.  Here an
+// ordered map of byte strings (unsigned lexicographic order) held on the host: the memtable is
+// a random-insert structure; what it feeds -- the flush batch -- goes to the device encoder.
+#include <map>
+#include <mutex>
+#include <string>
+
+struct lsmblk_memtable {
+  struct Ent {
+    uint64_t ts;
+    std::string val;
+  };
+  std::map<std::string, Ent> map;
+  size_t approximate_size = 0;
+  std::mutex mu;
+};
+
+extern "C" {
+
+lsmblk_memtable* lsmblk_memtable_new(void) { return new (std::nothrow) lsmblk_memtable(); }
+void lsmblk_memtable_free(lsmblk_memtable* m) { delete m; }
+
+int lsmblk_memtable_put(lsmblk_memtable* m, const uint8_t* key, size_t klen, uint64_t ts, const uint8_t* val,
+                        size_t vlen) {
+  if (!m || (klen && !key) || (vlen && !val)) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  std::string k(reinterpret_cast<const char*>(key), klen);
+  auto& e = m->map[k];  // insert replaces the entry with an equal key (mem_table.rs:120-123)
+  e.ts = ts;
+  e.val.assign(reinterpret_cast<const char*>(val), vlen);
+  m->approximate_size += klen + 8 + vlen;  // key.raw_len() + value.len(), :119,124-125
+  return LSMBLK_OK;
+}
+
+int lsmblk_memtable_get(lsmblk_memtable* m, const uint8_t* key, size_t klen, const uint8_t** val, size_t* vlen,
+                        uint64_t* ts) {
+  if (!m || (klen && !key) || !val || !vlen) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  auto it = m->map.find(std::string(reinterpret_cast<const char*>(key), klen));
+  if (it == m->map.end()) {
+    *val = nullptr;
+    *vlen = 0;
+    return 0;
+  }
+  *val = reinterpret_cast<const uint8_t*>(it->second.val.data());
+  *vlen = it->second.val.size();
+  if (ts) *ts = it->second.ts;
+  return 1;
+}
+
+size_t lsmblk_memtable_len(lsmblk_memtable* m) {
+  if (!m) return 0;
+  std::lock_guard<std::mutex> g(m->mu);
+  return m->map.size();
+}
+
+size_t lsmblk_memtable_approximate_size(lsmblk_memtable* m) {
+  if (!m) return 0;
+  std::lock_guard<std::mutex> g(m->mu);
+  return m->approximate_size;
+}
+
+int lsmblk_memtable_flush(lsmblk_memtable* m, uint8_t* keys, uint32_t* key_off, uint8_t* vals, uint32_t* val_off,
+                          uint64_t* ts, uint64_t entry_cap, uint64_t key_cap, uint64_t val_cap, uint64_t* n,
+                          uint64_t* kbytes, uint64_t* vbytes) {
+  if (!m || !n || !kbytes || !vbytes) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  uint64_t N = m->map.size(), K = 0, V = 0;
+  for (const auto& kv : m->map) {
+    K += kv.first.size();
+    V += kv.second.val.size();
+  }
+  *n = N;
+  *kbytes = K;
+  *vbytes = V;
+  if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) return LSMBLK_E_OVERFLOW;
+  if (N > entry_cap || K > key_cap || V > val_cap || !key_off || !val_off || (N && !ts)) return LSMBLK_E_CAPACITY;
+  uint64_t i = 0, kp = 0, vp = 0;
+  for (const auto& kv : m->map) {  // key order (mem_table.rs:132-134)
+    key_off[i] = uint32_t(kp);
+    val_off[i] = uint32_t(vp);
+    ts[i] = kv.second.ts;
+    if (!kv.first.empty()) std::memcpy(keys + kp, kv.first.data(), kv.first.size());
+    if (!kv.second.val.empty()) std::memcpy(vals + vp, kv.second.val.data(), kv.second.val.size());
+    kp += kv.first.size();
+    vp += kv.second.val.size();
+    ++i;
+  }
+  key_off[N] = uint32_t(kp);
+  val_off[N] = uint32_t(vp);
+  return LSMBLK_OK;
+}
+
+}  // extern "C"

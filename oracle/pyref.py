@@ -415,3 +415,201 @@ def compact_filter_rule(entries, watermark, bottom_level, prefixes=()):
             continue
         out.append((key, ts, value))
     return out
+
+
+# ---------------------------------------------------------------- SST container (row 3)
+# farmhash 1.1.5 `fingerprint32` (the hash SsTableBuilder::add records, src/table/builder.rs:53)
+# = farmhashmk::Hash32 of Google's published FarmHash, restated here.  farmhash is not
+# importable in this image and the reference cannot run, so this function is PARITY UNPINNED
+# beyond its own self-consistency; the bloom arithmetic around it is pinned by the reference's
+# raw-integer unit test (src/table/bloom.rs:123-160).
+_C1, _C2, _M32 = 0xCC9E2D51, 0x1B873593, 0xFFFFFFFF
+
+
+def _rot32(v, s):  # Rotate32: a right rotation
+    return ((v >> s) | (v << (32 - s))) & _M32 if s else v
+
+
+def _fmix(h):
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & _M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & _M32
+    h ^= h >> 16
+    return h
+
+
+def _mur(a, h):
+    a = (a * _C1) & _M32
+    a = _rot32(a, 17)
+    a = (a * _C2) & _M32
+    h ^= a
+    h = _rot32(h, 19)
+    return (h * 5 + 0xE6546B64) & _M32
+
+
+def _f32(s, i):
+    return int.from_bytes(s[i:i + 4], "little")
+
+
+def fingerprint32(s: bytes) -> int:
+    n = len(s)
+    if n <= 4:
+        b, c = 0, 9
+        for x in s:
+            v = x - 256 if x >= 128 else x  # signed char
+            b = (b * _C1 + v) & _M32
+            c ^= b
+        return _fmix(_mur(b, _mur(n, c)))
+    if n <= 12:
+        a, b, c = n, n * 5, 9
+        d = b
+        a = (a + _f32(s, 0)) & _M32
+        b = (b + _f32(s, n - 4)) & _M32
+        c = (c + _f32(s, (n >> 1) & 4)) & _M32
+        return _fmix(_mur(c, _mur(b, _mur(a, d))))
+    if n <= 24:
+        a = _f32(s, (n >> 1) - 4)
+        b = _f32(s, 4)
+        c = _f32(s, n - 8)
+        d = _f32(s, n >> 1)
+        e = _f32(s, 0)
+        f = _f32(s, n - 4)
+        h = (d * _C1 + n) & _M32
+        a = (_rot32(a, 12) + f) & _M32
+        h = (_mur(c, h) + a) & _M32
+        a = (_rot32(a, 3) + c) & _M32
+        h = (_mur(e, h) + a) & _M32
+        a = (_rot32((a + f) & _M32, 12) + d) & _M32
+        h = (_mur(b, h) + a) & _M32
+        return _fmix(h)
+    h, g = n & _M32, (_C1 * n) & _M32
+    f = g
+
+    def a_(off):
+        return (_rot32((_f32(s, off) * _C1) & _M32, 17) * _C2) & _M32
+    a0, a1, a2, a3, a4 = a_(n - 4), a_(n - 8), a_(n - 16), a_(n - 12), a_(n - 20)
+    h ^= a0
+    h = (_rot32(h, 19) * 5 + 0xE6546B64) & _M32
+    h ^= a2
+    h = (_rot32(h, 19) * 5 + 0xE6546B64) & _M32
+    g ^= a1
+    g = (_rot32(g, 19) * 5 + 0xE6546B64) & _M32
+    g ^= a3
+    g = (_rot32(g, 19) * 5 + 0xE6546B64) & _M32
+    f = (f + a4) & _M32
+    f = (_rot32(f, 19) + 113) & _M32
+    iters, p = (n - 1) // 20, 0
+    while True:
+        a, b, c, d, e = (_f32(s, p + 4 * i) for i in range(5))
+        h = (h + a) & _M32
+        g = (g + b) & _M32
+        f = (f + c) & _M32
+        h = (_mur(d, h) + e) & _M32
+        g = (_mur(c, g) + a) & _M32
+        f = (_mur((b + e * _C1) & _M32, f) + d) & _M32
+        f = (f + g) & _M32
+        g = (g + f) & _M32
+        p += 20
+        iters -= 1
+        if iters == 0:
+            break
+    g = (_rot32(g, 11) * _C1) & _M32
+    g = (_rot32(g, 17) * _C1) & _M32
+    f = (_rot32(f, 11) * _C1) & _M32
+    f = (_rot32(f, 17) * _C1) & _M32
+    h = _rot32((h + g) & _M32, 19)
+    h = (h * 5 + 0xE6546B64) & _M32
+    h = (_rot32(h, 17) * _C1) & _M32
+    h = _rot32((h + f) & _M32, 19)
+    h = (h * 5 + 0xE6546B64) & _M32
+    h = (_rot32(h, 17) * _C1) & _M32
+    return h
+
+
+class Bloom:
+    """src/table/bloom.rs:7-120, line by line."""
+
+    def __init__(self, filt: bytes, k: int):
+        self.filter, self.k = bytes(filt), k
+
+    @staticmethod
+    def bloom_bits_per_key(entries, false_positive_rate):  # :72-77 (f64 arithmetic)
+        import math
+        size = -1.0 * entries * math.log(false_positive_rate) / (math.log(2) * math.log(2))
+        locs = math.ceil(size / entries) if entries else 0  # NaN `as usize` = 0
+        return int(locs)
+
+    @staticmethod
+    def build_from_key_hashes(keys, bits_per_key):  # :80-101
+        k = min(max(int(bits_per_key * 0.69), 1), 30)
+        nbits = max(len(keys) * bits_per_key, 64)
+        nbytes = (nbits + 7) // 8
+        nbits = nbytes * 8
+        filt = bytearray(nbytes)
+        for h in keys:
+            delta = ((h >> 17) | (h << 15)) & _M32
+            for _ in range(k):
+                bit = h % nbits
+                filt[bit // 8] |= 1 << (bit % 8)
+                h = (h + delta) & _M32
+        return Bloom(filt, k)
+
+    def encode(self) -> bytes:  # :63-69
+        import zlib
+        body = self.filter + bytes([self.k])
+        return body + zlib.crc32(body).to_bytes(4, "big")
+
+    @staticmethod
+    def decode(buf: bytes):  # :49-60
+        import zlib
+        if int.from_bytes(buf[-4:], "big") != zlib.crc32(buf[:-4]):
+            raise ValueError("checksum mismatched for bloom filters")
+        return Bloom(buf[:-5], buf[-5])
+
+    def may_contain(self, h: int) -> bool:  # :104-120
+        if self.k > 30:
+            return True
+        nbits = len(self.filter) * 8
+        delta = ((h >> 17) | (h << 15)) & _M32
+        for _ in range(self.k):
+            bit = h % nbits
+            if not (self.filter[bit // 8] >> (bit % 8)) & 1:
+                return False
+            h = (h + delta) & _M32
+        return True
+
+
+def sst_file(entries, block_size) -> bytes:
+    """SsTableBuilder::add* + build (src/table/builder.rs:48-98): the whole SST file --
+    blocks each followed by its BE u32 crc32fast | BlockMeta section | u32 meta_offset |
+    bloom (filter | k | crc) | u32 bloom_offset."""
+    import zlib
+    blocks = encode_segments(entries, [0, len(entries)], block_size)
+    data = b"".join(b + zlib.crc32(b).to_bytes(4, "big") for b in blocks)
+    meta = encode_block_meta(sst_block_metas(entries, block_size))
+    buf = data + meta + len(data).to_bytes(4, "big")
+    hashes = [fingerprint32(k) for k, _, _ in entries]
+    bloom = Bloom.build_from_key_hashes(hashes, Bloom.bloom_bits_per_key(len(hashes), 0.01))
+    return buf + bloom.encode() + len(buf).to_bytes(4, "big")
+
+
+def sst_open(buf: bytes):
+    """SsTable::open (src/table.rs:162-186): footer offsets, bloom (CRC checked), BlockMeta
+    (CRC checked) -> (metas, max_ts, bloom, meta_offset)."""
+    n = len(buf)
+    bloom_offset = int.from_bytes(buf[n - 4:], "big")
+    bloom = Bloom.decode(buf[bloom_offset:n - 4])
+    meta_offset = int.from_bytes(buf[bloom_offset - 4:bloom_offset], "big")
+    metas, max_ts = decode_block_meta(buf[meta_offset:bloom_offset - 4])
+    return metas, max_ts, bloom, meta_offset
+
+
+def memtable_flush(puts):
+    """MemTable::put + flush (src/mem_table.rs:113-136): a crossbeam SkipMap keyed by KeyBytes
+    whose Ord ignores the ts (src/key.rs:63-81), so a later put of a key replaces the entry (key
+    ts and value); flush yields the map in key order."""
+    m = {}
+    for key, ts, value in puts:
+        m[bytes(key)] = (bytes(key), ts, bytes(value))
+    return [m[k] for k in sorted(m)]
