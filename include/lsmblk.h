@@ -305,6 +305,62 @@ int lsmblk_compact_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint
                          uint64_t out_cap, uint64_t* blk_off, uint64_t blk_cap, uint32_t* sst_start,
                          uint32_t* sst_blk, uint32_t sst_cap, uint64_t* stats, void* stream);
 
+/* ------------------------------------------------------------------ key-range sharded compaction (§8 e) */
+/* One GPU's share of a compaction split by user-key range over W ranks (SURVEY.md §8 e): the
+ * concatenation of every rank's output is byte-identical to the single-stream compact_generate_sst
+ * (src/compact.rs:223-311) over all the input, SST boundaries included.  Per rank:
+ *   1. lsmblk_compact_merge_batch: merge + rules over the decoded input blocks, keeping only the
+ *      keys in [lo, hi) (blocks straddling a splitter are read by both neighbours);
+ *   2. the caller appends the halo -- the first lsmblk_shard_halo_entries(block_size) kept entries
+ *      of the ranks after this one -- to the kept stream (one small all-gather);
+ *   3. lsmblk_shard_rotation_prepare: everything of the SST rotation that does not depend on the
+ *      state entering the range (block chains, SST-end function, its powers);
+ *   4. lsmblk_shard_rotation_carry: the boundary carry, rank after rank (send/recv of 16 bytes):
+ *      carry = {p, D}: the open SST's next block starts at entry p of the receiving rank's range and
+ *      the SST's data section (blocks + CRCs) holds D bytes there (D = 0: an SST starts at p);
+ *      rank 0 receives {0, 0};
+ *   5. lsmblk_shard_encode_batch: this rank's SST cut points and blocks. */
+typedef struct {
+  const uint8_t* lo;  /* device bytes; used when has_lo */
+  const uint8_t* hi;  /* device bytes; used when has_hi (exclusive) */
+  uint32_t lo_len, hi_len;
+  uint32_t has_lo, has_hi;
+} lsmblk_key_range;
+
+/* Halo length: a block that starts before a range end can take at most block_size / 16 entries
+ * after it, plus the entry it rejects. */
+uint64_t lsmblk_shard_halo_entries(uint32_t block_size);
+
+/* lsmblk_compact_batch's merge + rules + gather, restricted to keys in *range (NULL: all keys):
+ * kept receives this range's entries handed to SsTableBuilder::add.  stats: [0] kept entries [1] key
+ * bytes [2] value bytes [3] error flags [4] merged entries.  Asynchronous. */
+int lsmblk_compact_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                               const lsmblk_compact_opts* opts, const lsmblk_key_range* range,
+                               const lsmblk_kv_stream* kept, uint64_t* stats, void* stream);
+
+/* Rotation state of one range over `ext` = its n_own kept entries followed by the halo (ext->n
+ * entries in all).  flags: LSMBLK_SHARD_LAST when ext ends where the whole compaction's stream ends
+ * (the last rank, or a halo that reached the end).  sst_cap bounds the SSTs that start in the range.
+ * The state stays on the context for the next two calls (same context, no other compaction call on
+ * it in between).  Asynchronous. */
+#define LSMBLK_SHARD_LAST 1u
+int lsmblk_shard_rotation_prepare(lsmblk_ctx* ctx, const lsmblk_kv_stream* ext, uint64_t n_own, uint32_t flags,
+                                  uint32_t block_size, uint64_t target_sst_size, uint32_t sst_cap, void* stream);
+
+/* carry_in (device u64[2]) -> carry_out (device u64[2]) for the next rank.  Asynchronous. */
+int lsmblk_shard_rotation_carry(lsmblk_ctx* ctx, const uint64_t* carry_in, uint64_t* carry_out, void* stream);
+
+/* The range's segments -- [p, first SST end, ..., last SST start, end), SST cut points of the whole
+ * compaction, the first segment continuing the previous rank's open SST when carry_in.D > 0 and the
+ * last one continued by the next rank when carry_out.D > 0 -- into seg_start (device u32[seg_cap]:
+ * nseg + 1 entry indices of ext) and their blocks, packed, into out / blk_off as lsmblk_encode_batch
+ * writes them; seg_blk (u32[seg_cap]) receives every segment's first block.  stats (u64[8]): [0]
+ * blocks [1] bytes [2] segments [3] error flags [4] first segment continues [5] last segment
+ * continues [6] first entry [7] end entry.  Asynchronous. */
+int lsmblk_shard_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* ext, uint8_t* out, uint64_t out_cap,
+                              uint64_t* blk_off, uint64_t blk_cap, uint32_t* seg_start, uint32_t* seg_blk,
+                              uint32_t seg_cap, uint64_t* stats, void* stream);
+
 /* ------------------------------------------------------------------ memtable (§8 f row 4, host) */
 /* MemTable (src/mem_table.rs:55-158): an ordered map keyed by the key bytes only (Key's Ord ignores
  * the ts, src/key.rs:63-81), so put() of a present key replaces the entry; flush() (:131-136) yields

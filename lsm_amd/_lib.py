@@ -24,6 +24,7 @@ LSMBLK_E_OVERFLOW = -7
 LSMBLK_E_INTERNAL = -8
 LSMBLK_E_CHECKSUM = -9
 LSMBLK_DECODE_VERIFY_CRC = 1
+LSMBLK_SHARD_LAST = 1
 
 
 class LsmBlkError(RuntimeError):
@@ -41,6 +42,10 @@ class KVStreamC(ctypes.Structure):
 class CompactOptsC(ctypes.Structure):
     _fields_ = [("watermark", U64), ("bottom_level", ctypes.c_int32), ("nprefix", U32), ("prefixes", P),
                 ("prefix_off", P), ("block_size", U32), ("target_sst_size", U64)]
+
+
+class KeyRangeC(ctypes.Structure):
+    _fields_ = [("lo", P), ("hi", P), ("lo_len", U32), ("hi_len", U32), ("has_lo", U32), ("has_hi", U32)]
 
 
 # (name, restype, argtypes) for every symbol of include/lsmblk.h
@@ -87,6 +92,12 @@ SIGNATURES = [
     ("lsmblk_sst_rotation_batch", I, [P, ctypes.POINTER(KVStreamC), U32, U64, P, U32, P, P]),
     ("lsmblk_compact_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
                                  ctypes.POINTER(KVStreamC), P, U64, P, U64, P, P, U32, P, P]),
+    ("lsmblk_shard_halo_entries", U64, [U32]),
+    ("lsmblk_compact_merge_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
+                                       ctypes.POINTER(KeyRangeC), ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_shard_rotation_prepare", I, [P, ctypes.POINTER(KVStreamC), U64, U32, U32, U64, U32, P]),
+    ("lsmblk_shard_rotation_carry", I, [P, P, P, P]),
+    ("lsmblk_shard_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U64, P, U64, P, P, U32, P, P]),
     ("lsmblk_memtable_new", P, []),
     ("lsmblk_memtable_free", None, [P]),
     ("lsmblk_memtable_put", I, [P, P, S, U64, P, S]),

@@ -22,8 +22,8 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ._lib import (CompactOptsC, KVStreamC, LSMBLK_DECODE_VERIFY_CRC, LSMBLK_E_CAPACITY, LsmBlkError, check,
-                   lib)
+from ._lib import (CompactOptsC, KVStreamC, KeyRangeC, LSMBLK_DECODE_VERIFY_CRC, LSMBLK_E_CAPACITY,
+                   LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
 
 STATS_WORDS = 4
 _ctx_lock = threading.Lock()
@@ -503,14 +503,18 @@ def compact_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, b
     dev = _dev_index(run_start)
     kv.check(dev, "kv")
     _need(run_start, torch.int32, "run_start", dev, nrun + 1)
-    pfx, pfo = opts["_pfx"]
-    o = CompactOptsC(opts.get("watermark", 0), int(bool(opts.get("bottom_level", False))), opts["_npfx"],
-                     pfx.data_ptr(), pfo.data_ptr(), opts["block_size"], opts["target_sst_size"])
+    o = _opts_c(opts)
     ci, ck = kv._c(), buf.kept._c(*buf.kept.caps())
     check(lib().lsmblk_compact_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun, ctypes.byref(o),
                                      ctypes.byref(ck), buf.out.data_ptr(), buf.out_cap, buf.blk_off.data_ptr(),
                                      buf.blk_cap, buf.sst_start.data_ptr(), buf.sst_blk.data_ptr(), buf.sst_cap,
                                      buf.stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_compact_batch")
+
+
+def _opts_c(opts):
+    pfx, pfo = opts["_pfx"]
+    return CompactOptsC(opts.get("watermark", 0), int(bool(opts.get("bottom_level", False))), opts["_npfx"],
+                        pfx.data_ptr(), pfo.data_ptr(), opts["block_size"], opts["target_sst_size"])
 
 
 def compact_opts(watermark=0, bottom_level=False, prefixes=(), block_size=4096, target_sst_size=2 << 20,
@@ -541,3 +545,65 @@ def compact_runs(kv: KVStream, run_start, watermark=0, bottom_level=False, prefi
     buf.kept.n = s[5]
     return dict(kept=buf.kept, blocks=buf.out[:nbytes], blk_off=buf.blk_off[:nblk + 1],
                 sst_start=buf.sst_start[:nsst + 1], sst_blk=buf.sst_blk[:nsst + 1], stats=s)
+
+
+# ------------------------------------------------------------------ key-range sharded compaction
+def key_range_c(lo, hi):
+    """lsmblk_key_range over device byte tensors (None: unbounded side).  Keep the tensors alive."""
+    r = KeyRangeC()
+    if lo is not None:
+        r.lo, r.lo_len, r.has_lo = _ptr(lo), lo.numel(), 1
+    if hi is not None:
+        r.hi, r.hi_len, r.has_hi = _ptr(hi), hi.numel(), 1
+    return r
+
+
+def compact_merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, key_range, kept: KVStream,
+                       stats, stream=None):
+    """Asynchronous lsmblk_compact_merge_batch: merge + rules restricted to key_range (a KeyRangeC
+    or None) into preallocated `kept`.  stats: int64[5] device."""
+    dev = _dev_index(run_start)
+    kv.check(dev, "kv")
+    _need(run_start, torch.int32, "run_start", dev, nrun + 1)
+    kept.check(dev, "kept", 0)
+    _need(stats, torch.int64, "stats", dev, 5)
+    o = _opts_c(opts)
+    ci, ck = kv._c(), kept._c(*kept.caps())
+    check(lib().lsmblk_compact_merge_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun,
+                                           ctypes.byref(o), ctypes.byref(key_range) if key_range is not None else None,
+                                           ctypes.byref(ck), stats.data_ptr(), _stream_ptr(stream, dev)),
+          "lsmblk_compact_merge_batch")
+
+
+def shard_prepare(ext: KVStream, n_own: int, last: bool, block_size: int, target_sst_size: int, sst_cap: int,
+                  stream=None):
+    dev = _dev_index(ext.key_off)
+    ext.check(dev, "ext")
+    c = ext._c()
+    check(lib().lsmblk_shard_rotation_prepare(_ctx(dev, stream), ctypes.byref(c), n_own,
+                                              LSMBLK_SHARD_LAST if last else 0, block_size, target_sst_size, sst_cap,
+                                              _stream_ptr(stream, dev)), "lsmblk_shard_rotation_prepare")
+
+
+def shard_carry(carry_in: torch.Tensor, carry_out: torch.Tensor, stream=None):
+    dev = _dev_index(carry_in)
+    _need(carry_in, torch.int64, "carry_in", dev, 2)
+    _need(carry_out, torch.int64, "carry_out", dev, 2)
+    check(lib().lsmblk_shard_rotation_carry(_ctx(dev, stream), carry_in.data_ptr(), carry_out.data_ptr(),
+                                            _stream_ptr(stream, dev)), "lsmblk_shard_rotation_carry")
+
+
+def shard_encode_into(ext: KVStream, out, out_cap, blk_off, blk_cap, seg_start, seg_blk, seg_cap, stats,
+                      stream=None):
+    dev = _dev_index(ext.key_off)
+    ext.check(dev, "ext")
+    _need(out, torch.uint8, "out", dev, out_cap)
+    _need(blk_off, torch.int64, "blk_off", dev, blk_cap)
+    _need(seg_start, torch.int32, "seg_start", dev, seg_cap)
+    _need(seg_blk, torch.int32, "seg_blk", dev, seg_cap)
+    _need(stats, torch.int64, "stats", dev, 8)
+    c = ext._c()
+    check(lib().lsmblk_shard_encode_batch(_ctx(dev, stream), ctypes.byref(c), out.data_ptr(), out_cap,
+                                          blk_off.data_ptr(), blk_cap, seg_start.data_ptr(), seg_blk.data_ptr(),
+                                          seg_cap, stats.data_ptr(), _stream_ptr(stream, dev)),
+          "lsmblk_shard_encode_batch")

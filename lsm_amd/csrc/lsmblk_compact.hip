@@ -531,7 +531,25 @@ struct GatherArgs {
   uint64_t* tile_pre;       // 3 per tile
   uint64_t* stats;          // [0] kept [1] key bytes [2] value bytes [3] error flags
   const uint64_t* merr;     // the merge stage's error flags (bad run table)
+  lsmblk_key_range range;   // key-range shard (has_lo / has_hi 0: unbounded)
 };
+
+// Byte order of key (x, xl) against a range bound (y, yl) in device memory: -1, 0, 1.
+__device__ __forceinline__ int bound_cmp(const uint8_t* x, uint32_t xl, const uint8_t* y, uint32_t yl) {
+  const uint32_t m = xl < yl ? xl : yl;
+  for (uint32_t t = 0; t < m; ++t)
+    if (x[t] != y[t]) return x[t] < y[t] ? -1 : 1;
+  return xl < yl ? -1 : (xl > yl ? 1 : 0);
+}
+
+// lo <= key < hi.  The bounds are user keys, so all the versions of a key fall on one side.
+__device__ __forceinline__ bool in_range(const GatherArgs& a, uint32_t i) {
+  if (!a.range.has_lo && !a.range.has_hi) return true;
+  const uint32_t k0 = a.key_off[i], kl = a.key_off[i + 1] - k0;
+  if (a.range.has_lo && bound_cmp(a.keys + k0, kl, a.range.lo, a.range.lo_len) < 0) return false;
+  if (a.range.has_hi && bound_cmp(a.keys + k0, kl, a.range.hi, a.range.hi_len) >= 0) return false;
+  return true;
+}
 
 __device__ __forceinline__ bool same_key_g(const GatherArgs& a, uint32_t i, uint32_t j) {
   const uint32_t a0 = a.key_off[i], al = a.key_off[i + 1] - a0;
@@ -593,7 +611,7 @@ __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
     const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + threadIdx.x;
     if (j < N) {
       bool k = false;
-      if (merged_in_order(a, j)) k = mkeep(a, j);
+      if (merged_in_order(a, j)) k = in_range(a, a.perm[j]) && mkeep(a, j);
       else atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)LSMBLK_ERR_MALFORMED);
       a.keep[j] = k;
       if (k) {
@@ -822,7 +840,17 @@ struct RotArgs {
   uint32_t sst_cap;
   uint32_t* nsst;           // device: SST count handed to the encode (0 after an error)
   uint64_t* stats;          // [0] SSTs [3] error flags
+  // key-range shard (lsmblk_shard_*): the stream is the range's own m entries, then the halo
+  uint64_t m;
+  uint32_t shard_last;      // the stream ends where the whole compaction's stream ends
+  uint32_t* FL;             // flevels x (n_max + 1): F^(2^k); level 0 is F
+  uint32_t flevels;
+  uint64_t* sstate;         // kShardWords: the carry step's result
 };
+
+// sstate words
+constexpr uint32_t kShP = 0, kShE1 = 1, kShCnt = 2, kShEnd = 3, kShD0 = 4, kShDout = 5, kShErr = 6, kShSegs = 7;
+constexpr uint32_t kShardWords = 16;  // [8, 12): the encode's stats
 
 __device__ __forceinline__ uint64_t rot_n(const RotArgs& a) { return uni64(*a.dn); }
 
@@ -932,20 +960,18 @@ __global__ __launch_bounds__(256) void rot_double_kernel(RotArgs a, uint32_t k) 
   or_need(a.need + k, short_chain);
 }
 
-__global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
-  const uint64_t n = rot_n(a);
-  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (g > n) return;
-  if (g == n) {
-    a.F0[g] = uint32_t(n);
-    return;
-  }
-  const uint64_t N1 = a.n_max + 1;
-  uint32_t kc = 1;  // levels computed: 0 .. kc-1
+// Highest block-chain level computed (J / S levels 0 .. top).
+__device__ __forceinline__ uint32_t rot_top(const RotArgs& a) {
+  uint32_t kc = 1;
   while (kc < a.levels && a.need[kc - 1]) ++kc;
-  uint64_t pos = g, acc = 0;
-  const uint32_t top = kc - 1;
-  // lifting: the longest chain prefix from g whose data stays below the target
+  return kc - 1;
+}
+
+// Lifting from block start pos with acc bytes of data section: the longest block chain prefix
+// whose data stays below the target.  Returns its last block start (acc updated).
+__device__ __forceinline__ uint64_t lift_target(const RotArgs& a, uint64_t pos, uint64_t& acc, uint64_t n,
+                                                uint32_t top) {
+  const uint64_t N1 = a.n_max + 1;
   while (pos < n && acc + a.S[top * N1 + pos] < a.target) {
     acc += a.S[top * N1 + pos];
     pos = a.J[top * N1 + pos];
@@ -956,15 +982,178 @@ __global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
       pos = a.J[uint64_t(k) * N1 + pos];
     }
   }
-  uint64_t f = n;
-  if (pos < n) {
-    const uint64_t sj = a.J[pos];  // s_{j*}: the first block start whose entries see D >= target
-    if (sj < n) {
-      f = sj + 1;
-      while (f < n && (a.alcp[f] & kRotSame)) ++f;  // the first key change after it
+  return pos;
+}
+
+// Lifting from block start pos < bound: the last block start below bound in its chain (acc
+// updated with the data of the blocks passed).
+__device__ __forceinline__ uint64_t lift_before(const RotArgs& a, uint64_t pos, uint64_t& acc, uint64_t bound,
+                                                uint32_t top) {
+  const uint64_t N1 = a.n_max + 1;
+  while (a.J[top * N1 + pos] < bound) {
+    acc += a.S[top * N1 + pos];
+    pos = a.J[top * N1 + pos];
+  }
+  for (int k = int(top) - 1; k >= 0; --k) {
+    if (a.J[uint64_t(k) * N1 + pos] < bound) {
+      acc += a.S[uint64_t(k) * N1 + pos];
+      pos = a.J[uint64_t(k) * N1 + pos];
     }
   }
-  a.F0[g] = uint32_t(f);
+  return pos;
+}
+
+// The SST end after the block start sj whose entries first see D >= target: the first key
+// change after sj (n when none).
+__device__ __forceinline__ uint64_t key_change_after(const RotArgs& a, uint64_t sj, uint64_t n) {
+  if (sj >= n) return n;
+  uint64_t f = sj + 1;
+  while (f < n && (a.alcp[f] & kRotSame)) ++f;
+  return f;
+}
+
+__global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
+  const uint64_t n = rot_n(a);
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (g > n) return;
+  if (g == n) {
+    a.F0[g] = uint32_t(n);
+    return;
+  }
+  uint64_t acc = 0;
+  // lifting: the longest chain prefix from g whose data stays below the target
+  const uint64_t pos = lift_target(a, g, acc, n, rot_top(a));
+  // s_{j*}: the first block start whose entries see D >= target
+  a.F0[g] = uint32_t(pos < n ? key_change_after(a, a.J[pos], n) : n);
+}
+
+// ---------------------------------------------------------------- key-range shard rotation
+// Range r of a compaction split by user key holds the merged stream's entries [m_0, m_1); its
+// rotation stream is those m entries followed by the halo (the next entries of the whole stream,
+// enough to finish any block that starts before m).  Everything above is independent of the state
+// the whole-stream rotation is in when it reaches the range, so it runs on every rank at once;
+// only that state -- carry {p, D}: the open SST's next block starts at entry p (relative to the
+// range), its data section holds D bytes there -- passes from rank to rank, and each rank turns its
+// carry-in into its carry-out with a few dozen dependent loads:
+//   E1 = the open SST's end: the first key change after the block start whose entries first see
+//        D >= target (lifting from p with acc = D; p itself when D >= target already)
+//   SSTs starting in the range: E1, F(E1), ... while < m, counted by lifting over F^(2^k)
+//   the last SST (or the carried one) either ends exactly at m (a key change: ranges split at user
+//   keys) -> carry-out {0, 0}, or continues: its block chain crosses m at block start b with data
+//   D_b -> carry-out {b - m, D_b}; the crossing block is this rank's (it reads the halo).
+// The rank's segments [p, E1, F(E1), ..., end) then encode exactly the whole stream's blocks.
+__global__ __launch_bounds__(256) void rot_flev_kernel(RotArgs a, uint32_t k) {
+  const uint64_t n = rot_n(a);
+  const uint64_t s = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (s > n) return;
+  const uint64_t N1 = a.n_max + 1;
+  const uint32_t* F = a.FL + uint64_t(k - 1) * N1;
+  a.FL[uint64_t(k) * N1 + s] = F[F[s]];
+}
+
+__global__ void shard_carry_kernel(RotArgs a, const uint64_t* cin, uint64_t* cout) {
+  if (threadIdx.x) return;
+  const uint64_t n = rot_n(a), m = a.m, N1 = a.n_max + 1;
+  const uint32_t top = rot_top(a);
+  const uint64_t p = cin[0], D0 = cin[1];
+  uint64_t err = 0, E1 = m, cnt = 0, end = m, pout = 0, Dout = 0, segs = 0;
+  // the range must end at a key change (all versions of a user key on one rank)
+  if (m > 0 && m < n && (a.alcp[m] & kRotSame)) err |= LSMBLK_ERR_SEGMENTS;
+  if (p >= m) {  // the crossing block from an earlier rank covers the whole range
+    pout = p - m;
+    Dout = D0;
+    end = m;
+  } else {
+    uint64_t sj = p;
+    if (D0 < a.target) {
+      uint64_t acc = D0;
+      const uint64_t pos = lift_target(a, p, acc, n, top);
+      sj = pos < n ? a.J[pos] : n;
+    }
+    E1 = key_change_after(a, sj, n);
+    uint64_t x = p, accx = D0, fl = E1;
+    if (E1 < m) {  // SSTs start in the range: E1 and its successors below m
+      x = E1;
+      cnt = 1;
+      for (int k = int(a.flevels) - 1; k >= 0; --k) {
+        const uint32_t y = a.FL[uint64_t(k) * N1 + x];
+        if (y < m) {
+          x = y;
+          cnt += 1ull << k;
+        }
+      }
+      fl = a.FL[x];
+      if (fl < m) err |= LSMBLK_ERR_CAPACITY;  // more SSTs than the levels cover
+      accx = 0;
+    }
+    segs = cnt + 1;
+    if (fl == m) {  // the last SST ends where the next range starts (or the stream ends)
+      end = m;
+    } else {        // it continues: its block chain crosses m
+      const uint64_t pos = lift_before(a, x, accx, m, top);
+      const uint64_t b = a.J[pos];
+      if (b >= n && !a.shard_last) err |= LSMBLK_ERR_SEGMENTS;  // the halo is too short
+      end = b;
+      pout = b - m;
+      Dout = b >= n ? 0 : accx + a.S[pos];  // the whole stream ends inside this SST: nothing continues
+    }
+  }
+  uint64_t* w = a.sstate;
+  w[kShP] = p;
+  w[kShE1] = E1;
+  w[kShCnt] = cnt;
+  w[kShEnd] = end;
+  w[kShD0] = D0;
+  w[kShDout] = Dout;
+  w[kShErr] = err;
+  w[kShSegs] = err ? 0 : segs;
+  cout[0] = pout;
+  cout[1] = Dout;
+}
+
+// Segment table of the range: [p, E1, F(E1), ..., end), then `end` up to seg_cap.
+__global__ __launch_bounds__(256) void shard_seg_kernel(RotArgs a, uint32_t* seg, uint32_t seg_cap,
+                                                        uint32_t* nseg) {
+  const uint64_t* w = a.sstate;
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  uint64_t segs = w[kShSegs];
+  if (segs + 1 > seg_cap) segs = 0;
+  const uint64_t N1 = a.n_max + 1;
+  if (i == 0) {
+    *nseg = uint32_t(segs);
+    if (w[kShSegs] + 1 > seg_cap) atomicOr(reinterpret_cast<unsigned long long*>(a.sstate + kShErr),
+                                           (unsigned long long)LSMBLK_ERR_CAPACITY);
+  }
+  if (i >= seg_cap) return;
+  if (segs == 0) {
+    seg[i] = uint32_t(w[kShEnd]);
+    return;
+  }
+  if (i == 0) {
+    seg[0] = uint32_t(w[kShP]);
+  } else if (i < segs) {  // chain element i - 1 = F^(i-1)(E1)
+    uint64_t x = w[kShE1];
+    const uint64_t q = i - 1;
+    for (uint32_t k = 0; k < a.flevels; ++k)
+      if ((q >> k) & 1) x = a.FL[uint64_t(k) * N1 + x];
+    seg[i] = uint32_t(x);
+  } else {
+    seg[i] = uint32_t(w[kShEnd]);
+  }
+}
+
+__global__ void shard_stats_kernel(uint64_t* stats, const uint64_t* est, const uint64_t* w) {
+  if (threadIdx.x) return;
+  const uint64_t err = est[3] | w[kShErr];
+  const uint64_t segs = w[kShSegs];
+  stats[0] = err ? 0 : est[0];
+  stats[1] = err ? 0 : est[1];
+  stats[2] = err ? 0 : segs;
+  stats[3] = err;
+  stats[4] = segs && w[kShD0] > 0;
+  stats[5] = segs && w[kShDout] > 0;
+  stats[6] = w[kShP];
+  stats[7] = w[kShEnd];
 }
 
 // Level k: chain elements [2^k, 2^(k+1)) from [0, 2^k) through F^(2^k) (= cur), then
@@ -1069,8 +1258,8 @@ int ensure_ws(lsmblk_ctx* c, uint64_t bytes) {
 // merge + (rules | keep all) + gather into `out`; stats as lsmblk_compact_filter_batch's.
 int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                         uint32_t rules, uint64_t wm, int bottom, const uint8_t* pfx, const uint32_t* pfx_off,
-                        uint32_t npfx, const lsmblk_kv_stream* out, uint64_t* stats, hipStream_t st,
-                        MergePlan* plan_out) {
+                        uint32_t npfx, const lsmblk_key_range* range, const lsmblk_kv_stream* out, uint64_t* stats,
+                        hipStream_t st, MergePlan* plan_out) {
   const uint64_t n = in->n;
   MergePlan P = plan_merge(nullptr, n, nrun);
   int rc = ensure_ws(c, P.bytes);
@@ -1126,6 +1315,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   g.tile_pre = P.gtile + 3 * P.gtiles;
   g.stats = stats;
   g.merr = m.mstats + 3;
+  g.range = range ? *range : lsmblk_key_range{};
   const uint32_t gt = uint32_t((n + kGTile - 1) / kGTile);
   hipLaunchKernelGGL(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
   hipLaunchKernelGGL(mscan_kernel, dim3(1), dim3(1024), 0, st, g);
@@ -1157,7 +1347,8 @@ struct RotPlan {
   uint64_t bytes;
 };
 
-RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target) {
+// flevels > 0: the shard layout (F^(2^k) levels instead of the chain ping-pong, carry state).
+RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, uint32_t flevels = 0) {
   RotPlan P{};
   Carve cv{base, off};
   const uint64_t N1 = n_max + 1;
@@ -1169,8 +1360,16 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target) {
   P.r.alcp = cv.take<uint32_t>(N1);
   P.r.J = cv.take<uint32_t>(N1 * L);
   P.r.S = cv.take<uint32_t>(N1 * L);
-  P.r.F0 = cv.take<uint32_t>(N1);
-  P.r.F1 = cv.take<uint32_t>(N1);
+  if (flevels) {
+    P.r.flevels = flevels;
+    P.r.FL = cv.take<uint32_t>(N1 * flevels);
+    P.r.F0 = P.r.FL;
+    P.r.F1 = nullptr;
+    P.r.sstate = cv.take<uint64_t>(kShardWords);
+  } else {
+    P.r.F0 = cv.take<uint32_t>(N1);
+    P.r.F1 = cv.take<uint32_t>(N1);
+  }
   P.r.need = cv.take<uint32_t>(kRotMaxLevels + 2);
   P.r.chain_end = P.r.need + kRotMaxLevels;
   P.r.nsst = P.r.need + kRotMaxLevels + 1;
@@ -1180,15 +1379,23 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target) {
 }
 
 // SST cut points of the stream (keys, key_off, val_off; *dn entries, <= n_max) into starts[]
-int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
-  (void)c;
+// The carry-independent part: adjacency, block chains and their doubling levels, F.
+int rotation_chains(const RotArgs& r, hipStream_t st) {
   if (hipMemsetAsync(r.need, 0, (kRotMaxLevels + 2) * sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
-  if (hipMemsetAsync(r.starts, 0, sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
   hipLaunchKernelGGL(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
   hipLaunchKernelGGL(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
   for (uint32_t k = 1; k < r.levels; ++k) hipLaunchKernelGGL(rot_double_kernel, dim3(g), dim3(256), 0, st, r, k);
   hipLaunchKernelGGL(rot_f_kernel, dim3(g), dim3(256), 0, st, r);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
+  (void)c;
+  if (hipMemsetAsync(r.starts, 0, sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
+  int rc = rotation_chains(r, st);
+  if (rc) return rc;
+  const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
   uint32_t* cur = r.F0;
   uint32_t* nxt = r.F1;
   for (uint32_t k = 0; k < 32 && (1ull << k) < r.sst_cap; ++k) {
@@ -1225,9 +1432,125 @@ int check_merge_args(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* 
   return LSMBLK_OK;
 }
 
+uint32_t shard_flevels(uint32_t sst_cap) {
+  uint32_t k = 1;
+  while (k < 32 && (1ull << k) < uint64_t(sst_cap) + 1) ++k;
+  return k;
+}
+
+// The rotation arguments of the last lsmblk_shard_rotation_prepare on this context.
+RotArgs shard_args(lsmblk_ctx* c, const lsmblk_kv_stream* ext) {
+  const RotPlan P = plan_rot(c->rws, 0, c->shard_n, c->shard_target, shard_flevels(c->shard_sst_cap));
+  RotArgs r = P.r;
+  r.dn = P.dn;
+  r.m = c->shard_m;
+  r.shard_last = c->shard_flags & LSMBLK_SHARD_LAST;
+  r.block_size = c->shard_block_size;
+  if (ext) {
+    r.keys = ext->keys;
+    r.key_off = ext->key_off;
+    r.val_off = ext->val_off;
+  }
+  return r;
+}
+
+__global__ void copy_u64_kernel(uint64_t* dst, const uint64_t* src) {
+  if (threadIdx.x == 0) *dst = *src;
+}
+
 }  // namespace
 
 extern "C" {
+
+uint64_t lsmblk_shard_halo_entries(uint32_t block_size) { return uint64_t(block_size) / 16 + 2; }
+
+int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                               const lsmblk_compact_opts* o, const lsmblk_key_range* range,
+                               const lsmblk_kv_stream* kept, uint64_t* stats, void* stream) {
+  int rc = check_merge_args(c, in, run_start, nrun, kept, stats);
+  if (rc) return rc;
+  if (!o || (o->nprefix && (!o->prefixes || !o->prefix_off))) return LSMBLK_E_INVAL;
+  if (range && ((range->has_lo && range->lo_len && !range->lo) || (range->has_hi && range->hi_len && !range->hi)))
+    return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats + 4, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  MergePlan MP{};
+  if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
+                                o->nprefix, range, kept, stats, st, &MP)))
+    return rc;
+  if (in->n) hipLaunchKernelGGL(copy_u64_kernel, dim3(1), dim3(64), 0, st, stats + 4, MP.m.mstats);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int lsmblk_shard_rotation_prepare(lsmblk_ctx* c, const lsmblk_kv_stream* ext, uint64_t n_own, uint32_t flags,
+                                  uint32_t block_size, uint64_t target_sst_size, uint32_t sst_cap, void* stream) {
+  if (!c || !ext || !ext->key_off || !ext->val_off) return LSMBLK_E_INVAL;
+  if (block_size == 0 || target_sst_size == 0 || sst_cap == 0 || n_own > ext->n || ext->n >= 0xFFFFFFF0ull)
+    return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  c->shard_ready = false;
+  const uint32_t fl = shard_flevels(sst_cap);
+  const RotPlan P0 = plan_rot(nullptr, 0, ext->n, target_sst_size, fl);
+  int rc = grow(&c->rws, &c->rws_cap, P0.bytes, 1);
+  if (rc) return rc;
+  c->shard_n = ext->n;
+  c->shard_m = n_own;
+  c->shard_target = target_sst_size;
+  c->shard_block_size = block_size;
+  c->shard_flags = flags;
+  c->shard_sst_cap = sst_cap;
+  const RotArgs r = shard_args(c, ext);
+  hipLaunchKernelGGL(set_u64_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(r.dn), uint64_t(ext->n));
+  if ((rc = rotation_chains(r, st))) return rc;
+  const uint32_t gr = uint32_t((ext->n + 1 + 255) / 256);
+  for (uint32_t k = 1; k < fl; ++k) hipLaunchKernelGGL(rot_flev_kernel, dim3(gr), dim3(256), 0, st, r, k);
+  if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
+  c->shard_ready = true;
+  return LSMBLK_OK;
+}
+
+int lsmblk_shard_rotation_carry(lsmblk_ctx* c, const uint64_t* carry_in, uint64_t* carry_out, void* stream) {
+  if (!c || !carry_in || !carry_out) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->shard_ready) return LSMBLK_E_INVAL;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  const RotArgs r = shard_args(c, nullptr);
+  hipLaunchKernelGGL(shard_carry_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), r, carry_in,
+                     carry_out);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+int lsmblk_shard_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* ext, uint8_t* out, uint64_t out_cap,
+                              uint64_t* blk_off, uint64_t blk_cap, uint32_t* seg_start, uint32_t* seg_blk,
+                              uint32_t seg_cap, uint64_t* stats, void* stream) {
+  if (!c || !ext || !ext->key_off || !ext->val_off || !out || !blk_off || !seg_start || !seg_blk || !stats)
+    return LSMBLK_E_INVAL;
+  if (seg_cap < 2 || blk_cap == 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->shard_ready || ext->n != c->shard_n) return LSMBLK_E_INVAL;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const RotArgs r = shard_args(c, ext);
+  uint64_t* est = r.sstate + 8;
+  if (hipMemsetAsync(stats, 0, LSMBLK_COMPACT_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  hipLaunchKernelGGL(shard_seg_kernel, dim3((seg_cap + 255) / 256), dim3(256), 0, st, r, seg_start, seg_cap, r.nsst);
+  if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
+  int rc = lsmblk_impl::encode_locked(c, ext, nullptr, seg_start, r.nsst, seg_cap - 1, c->shard_block_size, out,
+                                      out_cap, blk_off, blk_cap, est, st, true);
+  if (rc) return rc;
+  if ((rc = lsmblk_impl::segment_blocks_locked(c, seg_start, seg_cap - 1, est, seg_blk, st))) return rc;
+  hipLaunchKernelGGL(shard_stats_kernel, dim3(1), dim3(64), 0, st, stats, est, r.sstate);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
 
 int lsmblk_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                        const lsmblk_kv_stream* out, uint64_t* stats, void* stream) {
@@ -1236,7 +1559,7 @@ int lsmblk_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
   if (!dg.ok) return LSMBLK_E_HIP;
-  return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, out, stats,
+  return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, nullptr, out, stats,
                              reinterpret_cast<hipStream_t>(stream), nullptr);
 }
 
@@ -1294,7 +1617,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
   MergePlan MP{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
-                                o->nprefix, kept, fst, st, &MP)))
+                                o->nprefix, nullptr, kept, fst, st, &MP)))
     return rc;
   R = plan_rot(c->cws, M.bytes, n, o->target_sst_size);
   hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);

@@ -416,6 +416,13 @@ struct lsmblk_ctx {
   // SST files (lsmblk_sst.hip)
   uint8_t* sws = nullptr;
   uint64_t sws_cap = 0;
+  // key-range shard rotation (lsmblk_shard_*): its own arena, carved from the parameters of the
+  // last lsmblk_shard_rotation_prepare, which the carry and encode calls replay
+  uint8_t* rws = nullptr;
+  uint64_t rws_cap = 0;
+  uint64_t shard_n = 0, shard_m = 0, shard_target = 0;
+  uint32_t shard_block_size = 0, shard_flags = 0, shard_sst_cap = 0;
+  bool shard_ready = false;
 };
 
 namespace {
@@ -467,10 +474,12 @@ struct DeviceGuard {
 // Internal entry points shared between translation units (called with ctx->mu held).
 namespace lsmblk_impl {
 // lsmblk_encode_batch with optional device-side entry count (dn) and segment count (dnseg):
-// in->n and nseg are then upper bounds that size the grids and the workspace.
+// in->n and nseg are then upper bounds that size the grids and the workspace.  span: the
+// segments cover [seg_start[0], seg_start[nseg]) of the stream (a key-range shard's part of a
+// stream that also holds the previous rank's crossing block and the halo), not all of it.
 int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
                   const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
-                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st);
+                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span = false);
 // lsmblk_encode_segment_blocks for the encode that just ran on this context.
 int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
                           uint32_t* seg_blk, hipStream_t st);

@@ -787,6 +787,7 @@ struct PlanArgs {
   uint32_t poll;
   const uint64_t* dn;      // optional: n read from device memory (overrides n)
   const uint32_t* dnseg;   // optional: nseg read from device memory (overrides nseg)
+  uint32_t span;           // segments cover [seg_start[0], seg_start[nseg]) of the stream, not all of it
 };
 
 __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
@@ -875,7 +876,8 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
   if (g >= a.nseg) return;
   uint32_t err = 0;
   uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
-  if ((g == 0 && s0 != 0) || (g == a.nseg - 1 && uint64_t(s1) != a.n) || s0 > s1 || uint64_t(s1) > a.n) {
+  if ((!a.span && g == 0 && s0 != 0) || (!a.span && g == a.nseg - 1 && uint64_t(s1) != a.n) || s0 > s1 ||
+      uint64_t(s1) > a.n) {
     err |= LSMBLK_ERR_SEGMENTS;
     s1 = s0 = (s0 > a.n ? uint32_t(a.n) : s0);
     if (s1 < s0) s1 = s0;
@@ -995,7 +997,7 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
   }
   if (g == a.nseg - 1 && l == 0) {
     const uint64_t Bt = B0 + nb, Ot = O0 + bytes;
-    a.blk_first[Bt] = uint32_t(a.n);
+    a.blk_first[Bt] = a.span ? s1 : uint32_t(a.n);
     if (Bt < a.blk_cap) a.blk_off[Bt] = Ot;
     a.stats[0] = Bt;
     a.stats[1] = Ot;
@@ -2135,6 +2137,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->cws);
   (void)hipFree(c->vcrc);
   (void)hipFree(c->sws);
+  (void)hipFree(c->rws);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2293,7 +2296,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
 namespace lsmblk_impl {
 int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
                   const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
-                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st) {
+                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span) {
   // in->n (and nseg) are upper bounds when dn (dnseg) point at the device-side values
   int rc = reserve_locked(c, 0, in->n, nseg);
   if (rc) return rc;
@@ -2331,6 +2334,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.poll = c->poll;
   p.dn = dn;
   p.dnseg = dnseg;
+  p.span = span ? 1u : 0u;
   c->enc_timed = c->timing;
   if (c->timing) (void)hipEventRecord(c->ev[4], st);
   if (in->n) {

@@ -1,24 +1,38 @@
-"""Multi-GPU sharding for the block path.
+"""Multi-GPU sharding of the block path.
 
 Two shapes:
-  * block-parallel (bench.py): every rank owns a contiguous range of blocks or segments;
-    blocks decode and segments (SSTs) encode independently, so there is no data-path
+  * block-parallel (bench.py configs U / Z / M): every rank owns a contiguous range of blocks or
+    segments; blocks decode and segments (SSTs) encode independently, so there is no data-path
     collective -- only the timing barrier and a max-reduce of the elapsed time.
-  * compaction-shaped (next step): key-range sharding of L0 -> L1 batches.  The only
-    exchange is the splitter keys: each rank samples the first keys of the input blocks
-    it holds (BlockMeta.first_key, reference src/table.rs:22-26, 253-257: host-visible
-    without decoding), the samples are all-gathered (tiny: <= world x samples x key bytes,
-    latency-bound over xGMI), and every rank derives the same world-1 splitters.  Data
-    never moves between GPUs; blocks straddling a splitter are read by both neighbours and
-    filtered on the key range.
+  * compaction-shaped (bench.py config C at N > 1): the L0 -> L1 compaction split by user-key range,
+    one range per rank, with output byte-identical to the single-stream compact_generate_sst
+    (reference src/compact.rs:223-311), SST boundaries included.  Three small exchanges:
+      1. splitters: every rank contributes key samples of the input blocks it holds (BlockMeta first
+         keys, src/table.rs:22-26, host-visible without decoding); one all-gather, and every rank
+         derives the same world-1 splitters.  Blocks straddling a splitter are read by both
+         neighbours; the merge keeps only the rank's own keys (lsmblk_compact_merge_batch's range).
+      2. halo: every rank all-gathers the head of its kept stream -- the first
+         lsmblk_shard_halo_entries(block_size) entries, enough to finish any block that starts
+         before the next range.  A rank appends the heads of the ranks after it to its own stream.
+      3. carry: the SST rotation's state entering each range -- the open SST's next block start and
+         data-section size, 16 bytes -- goes rank to rank (send / recv), each rank turning its
+         carry-in into its carry-out with one tiny kernel (lsmblk_shard_rotation_carry) after the
+         carry-independent rotation work has run everywhere at once.
+    Bulk KV data never moves between GPUs: the halo is a few KiB, the carry 16 bytes.
 
-Works with any torch.distributed backend ("nccl" = RCCL on ROCm, "gloo" on CPU).
+Works with any torch.distributed backend ("nccl" = RCCL on ROCm, "gloo" on CPU).  The device work
+is liblsmblk.so's; RangeShard is its host-side driver, and the exchange drivers (compact_local,
+compact_dist) only move the small messages above.
 """
 import bisect
 import struct
 
+import numpy as np
 import torch
 import torch.distributed as dist
+
+from . import batch
+from ._lib import LsmBlkError, lib
 
 
 def block_ranges(nblk: int, world: int):
@@ -41,6 +55,8 @@ def max_over_ranks(x: float, device=None) -> float:
     return float(t.item())
 
 
+# ---------------------------------------------------------------------------------------------
+# splitters
 def _pack_keys(keys, max_key_bytes):
     buf = bytearray()
     for k in keys:
@@ -78,16 +94,16 @@ def choose_splitters(all_samples, world: int):
 def exchange_splitters(first_keys, samples: int = 64, max_key_bytes: int = 64, device=None):
     """All-gather every rank's key samples (fixed-size records in one tensor) and return
     the common splitters.  Keys longer than max_key_bytes are truncated for the sample,
-    which only moves a splitter, never correctness (straddling blocks go to both ranks)."""
+    which only moves a splitter (any byte string splits the key space)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     mine = sample_first_keys(first_keys, samples)
+    if world == 1:
+        return choose_splitters(mine, 1)
     rec = 2 + max_key_bytes
     payload = bytearray(_pack_keys(mine, max_key_bytes))
     payload += b"\0" * (rec * samples - len(payload))
     count = torch.tensor([len(mine)], dtype=torch.int64, device=device)
     t = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
-    if world == 1:
-        return choose_splitters(mine, 1)
     counts = [torch.zeros_like(count) for _ in range(world)]
     dist.all_gather(counts, count)
     bufs = [torch.zeros_like(t) for _ in range(world)]
@@ -101,3 +117,296 @@ def exchange_splitters(first_keys, samples: int = 64, max_key_bytes: int = 64, d
 def owner_of(key: bytes, splitters) -> int:
     """Rank owning `key` under the splitters (rank i owns [s_{i-1}, s_i))."""
     return bisect.bisect_right(splitters, key)
+
+
+def range_of(rank: int, splitters):
+    """(lo, hi) key bounds of a rank (None: unbounded)."""
+    lo = splitters[rank - 1] if rank > 0 else None
+    hi = splitters[rank] if rank < len(splitters) else None
+    return lo, hi
+
+
+# ---------------------------------------------------------------------------------------------
+# halo: the heads of the kept streams
+def halo_entries(block_size: int) -> int:
+    return int(lib().lsmblk_shard_halo_entries(block_size))
+
+
+class Head:
+    """The first h <= W kept entries of a range (of n in all): relative offsets int64[h+1], ts
+    int64[h], key / value bytes -- tensors on the exchange's device."""
+
+    def __init__(self, n, ko, vo, ts, keys, vals):
+        self.n, self.ko, self.vo, self.ts, self.keys, self.vals = n, ko, vo, ts, keys, vals
+
+    @property
+    def h(self):
+        return self.ts.numel()
+
+
+def assemble_halo(heads, g: int, W: int):
+    """Rank g's halo: the first W entries after its range, from the heads of the ranks after it
+    (a short range contributes all of its entries and the next one continues).  Returns (keys,
+    ko, vals, vo, ts, last): `last` when the halo reaches the end of the whole stream."""
+    need, parts, taken, remaining = W, [], 0, sum(h.n for h in heads[g + 1:])
+    for hd in heads[g + 1:]:
+        if need == 0:
+            break
+        t = min(need, hd.h)
+        if t:
+            parts.append((hd, t))
+        need -= t
+        taken += t
+    dev = heads[g].ts.device
+    kb = [hd.keys[:int(hd.ko[t])] for hd, t in parts]
+    vb = [hd.vals[:int(hd.vo[t])] for hd, t in parts]
+    ko, vo, kbase, vbase = [torch.zeros(1, dtype=torch.int64, device=dev)], [torch.zeros(1, dtype=torch.int64,
+                                                                                         device=dev)], 0, 0
+    for hd, t in parts:
+        ko.append(hd.ko[1:t + 1] + kbase)
+        vo.append(hd.vo[1:t + 1] + vbase)
+        kbase += int(hd.ko[t])
+        vbase += int(hd.vo[t])
+    cat = (lambda xs, dt: torch.cat(xs) if xs else torch.zeros(0, dtype=dt, device=dev))
+    return (cat(kb, torch.uint8), torch.cat(ko), cat(vb, torch.uint8), torch.cat(vo),
+            cat([hd.ts[:t] for hd, t in parts], torch.int64), taken == remaining)
+
+
+def _u32_as_i32(x: torch.Tensor) -> torch.Tensor:
+    """int64 values in [0, 2^32) -> their u32 bit pattern in an int32 tensor."""
+    x = x & 0xFFFFFFFF
+    return torch.where(x >= (1 << 31), x - (1 << 32), x).to(torch.int32)
+
+
+# ---------------------------------------------------------------------------------------------
+class RangeShard:
+    """One key range of a compaction on one device: the decoded input runs (kv, run_start), the
+    compaction options (batch.compact_opts) and the range [lo, hi) (None: unbounded).  Phases:
+    merge() -> head() -> set_halo() -> prepare() -> carry() -> encode() -> result(); buffers are kept
+    for the next call with the same sizes (the bench's timed loop allocates nothing).  Every shard
+    works on its own stream (default: a new one), so its context -- which holds the rotation state
+    between prepare, carry and encode -- is its own; the exchange drivers run under
+    torch.cuda.stream(shard.stream)."""
+
+    def __init__(self, kv: batch.KVStream, run_start, opts: dict, lo: bytes = None, hi: bytes = None, stream=None):
+        self.dev = torch.device("cuda", batch._dev_index(kv.key_off))
+        self.kv, self.opts = kv, opts
+        self.stream = stream if stream is not None else torch.cuda.Stream(self.dev)
+        self.rs = batch._u32_table(run_start, self.dev)
+        self.nrun = self.rs.numel() - 1
+        self.bs, self.target = opts["block_size"], opts["target_sst_size"]
+        self.W = halo_entries(self.bs)
+        self._lo = self._bound(lo)
+        self._hi = self._bound(hi)
+        self.range_c = batch.key_range_c(self._lo, self._hi)
+        self.K_in, self.V_in = kv.byte_sizes()
+        self.kept = None
+        self.mstats = torch.zeros(5, dtype=torch.int64, device=self.dev)
+        self.cout = torch.zeros(2, dtype=torch.int64, device=self.dev)
+        self.estats = torch.zeros(8, dtype=torch.int64, device=self.dev)
+        self.out = None
+        self._grow_kept(kv.n + self.W, self.K_in + 64 * self.W, self.V_in + 256 * self.W)
+
+    def _bound(self, b):
+        if b is None:
+            return None
+        return torch.frombuffer(bytearray(bytes(b) or b"\0"), dtype=torch.uint8)[:len(b)].to(self.dev)
+
+    def _grow_kept(self, n, kb, vb, keep=0):
+        old = self.kept
+        self.kept = batch.KVStream.empty(n, kb, vb, self.dev)
+        if old is not None and keep:  # the first `keep` entries survive a regrow
+            self.kept.keys[:self.Kk].copy_(old.keys[:self.Kk])
+            self.kept.vals[:self.Vk].copy_(old.vals[:self.Vk])
+            self.kept.key_off[:keep + 1].copy_(old.key_off[:keep + 1])
+            self.kept.val_off[:keep + 1].copy_(old.val_off[:keep + 1])
+            self.kept.ts[:keep].copy_(old.ts[:keep])
+
+    # -- phase 1: merge + rules + range
+    def merge(self):
+        with torch.cuda.stream(self.stream):
+            return self._merge()
+
+    def _merge(self):
+        k = self.kept
+        k.n = 0
+        batch.compact_merge_into(self.kv, self.rs, self.nrun, self.opts, self.range_c, k, self.mstats, self.stream)
+        torch.cuda.synchronize(self.dev)
+        s = self.mstats.cpu().tolist()
+        st = lib().lsmblk_stats_status(s[3] & 0xFFFFFFFFFFFFFFFF)
+        if st:
+            raise LsmBlkError(st, "compact_merge")
+        self.m, self.Kk, self.Vk, self.merged = s[0], s[1], s[2], s[4]
+        k.n = self.m
+        return self.m
+
+    # -- phase 2: halo
+    def head(self) -> Head:
+        with torch.cuda.stream(self.stream):
+            return self._head()
+
+    def _head(self) -> Head:
+        h = min(self.W, self.m)
+        ko = self.kept.key_off[:h + 1].to(torch.int64) & 0xFFFFFFFF
+        vo = self.kept.val_off[:h + 1].to(torch.int64) & 0xFFFFFFFF
+        kb, vb = (int(ko[h]), int(vo[h])) if h else (0, 0)
+        return Head(self.m, ko, vo, self.kept.ts[:h].clone(), self.kept.keys[:kb].clone(), self.kept.vals[:vb].clone())
+
+    def set_halo(self, keys, ko, vals, vo, ts, last: bool):
+        with torch.cuda.stream(self.stream):
+            self._set_halo(keys, ko, vals, vo, ts, last)
+
+    def _set_halo(self, keys, ko, vals, vo, ts, last: bool):
+        m, h = self.m, ts.numel()
+        Kh, Vh = keys.numel(), vals.numel()
+        ecap, kcap, vcap = self.kept.caps()
+        if m + h > ecap or self.Kk + Kh + 16 > kcap or self.Vk + Vh + 16 > vcap:
+            self._grow_kept(max(ecap, m + h), max(kcap, self.Kk + Kh + 16), max(vcap, self.Vk + Vh + 16), keep=m)
+        k = self.kept
+        if Kh:
+            k.keys[self.Kk:self.Kk + Kh].copy_(keys.to(self.dev))
+        if Vh:
+            k.vals[self.Vk:self.Vk + Vh].copy_(vals.to(self.dev))
+        if h:
+            k.key_off[m + 1:m + 1 + h].copy_(_u32_as_i32(ko[1:].to(self.dev) + self.Kk))
+            k.val_off[m + 1:m + 1 + h].copy_(_u32_as_i32(vo[1:].to(self.dev) + self.Vk))
+            k.ts[m:m + h].copy_(ts.to(self.dev))
+        self.h, self.Kh, self.Vh, self.last = h, Kh, Vh, bool(last)
+        self.ext = batch.KVStream(k.keys, k.key_off, k.vals, k.val_off, k.ts, m + h)
+
+    # -- phase 3: carry-independent rotation
+    def prepare(self):
+        n = self.m + self.h
+        self.sst_cap = (self.Kk + self.Vk + self.Kh + self.Vh + 22 * n) // self.target + 3
+        batch.shard_prepare(self.ext, self.m, self.last, self.bs, self.target, self.sst_cap, self.stream)
+
+    # -- phase 4: carry
+    def carry(self, carry_in: torch.Tensor) -> torch.Tensor:
+        self.carry_in = carry_in
+        batch.shard_carry(carry_in, self.cout, self.stream)
+        return self.cout
+
+    # -- phase 5: SST cut points + blocks
+    def encode(self):
+        with torch.cuda.stream(self.stream):
+            self._encode()
+
+    def _encode(self):
+        n = self.ext.n
+        out_cap = self.Kk + self.Vk + self.Kh + self.Vh + 18 * n + 16
+        blk_cap, seg_cap = n + 2, self.sst_cap + 3
+        if self.out is None or self.out.numel() < out_cap or self.blk_off.numel() < blk_cap or \
+                self.seg.numel() < seg_cap:
+            self.out = batch._aligned_empty(out_cap, self.dev)
+            self.blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=self.dev)
+            self.seg = torch.zeros(seg_cap, dtype=torch.int32, device=self.dev)
+            self.seg_blk = torch.zeros(seg_cap, dtype=torch.int32, device=self.dev)
+        batch.shard_encode_into(self.ext, self.out, out_cap, self.blk_off, blk_cap, self.seg, self.seg_blk, seg_cap,
+                                self.estats, self.stream)
+
+    def result(self):
+        """Host view of the range's output (synchronizes): blocks, blk_off, seg_start (ext entry
+        indices, nseg+1), seg_blk, and whether the first / last segment continue an SST of the
+        previous / next range."""
+        torch.cuda.synchronize(self.dev)
+        s = self.estats.cpu().tolist()
+        st = lib().lsmblk_stats_status(s[3] & 0xFFFFFFFFFFFFFFFF)
+        if st:
+            raise LsmBlkError(st, "shard_encode")
+        nblk, nbytes, nseg = s[0], s[1], s[2]
+        return dict(blocks=self.out[:nbytes], blk_off=self.blk_off[:nblk + 1],
+                    seg_start=self.seg[:nseg + 1].cpu().numpy().view(np.uint32) if nseg else np.zeros(0, np.uint32),
+                    seg_blk=self.seg_blk[:nseg + 1].cpu().numpy().view(np.uint32) if nseg else np.zeros(0, np.uint32),
+                    nblk=nblk, nbytes=nbytes, nseg=nseg, first_continues=bool(s[4]), last_continues=bool(s[5]),
+                    first=s[6], end=s[7], m=self.m, merged=self.merged,
+                    carry_in=tuple(self.carry_in.cpu().tolist()), carry_out=tuple(self.cout.cpu().tolist()))
+
+
+def sst_starts(results, bases):
+    """Global kept-entry index of every SST start, from the ranges' results in key order (bases =
+    each range's first global kept index)."""
+    starts = []
+    for r, base in zip(results, bases):
+        if r["nseg"] == 0:
+            continue
+        first = 1 if r["first_continues"] else 0
+        starts += [base + int(x) for x in r["seg_start"][first:-1]]
+    return starts
+
+
+# ---------------------------------------------------------------------------------------------
+# exchange drivers
+def compact_local(shards):
+    """Every range of the compaction in this process (in key order), e.g. several ranges on one
+    GPU: the same phases and messages as compact_dist, passed in memory."""
+    for s in shards:
+        s.merge()
+    heads = [s.head() for s in shards]
+    for g, s in enumerate(shards):
+        s.set_halo(*assemble_halo(heads, g, s.W))
+    for s in shards:
+        s.prepare()
+    c = torch.zeros(2, dtype=torch.int64, device=shards[0].dev) if shards else None
+    for s in shards:
+        torch.cuda.synchronize(s.dev)   # the carry-in was made on the previous shard's stream
+        with torch.cuda.stream(s.stream):
+            c = s.carry(c).clone()
+    for s in shards:
+        s.encode()
+    return [s.result() for s in shards]
+
+
+def _allgather_heads(head: Head, group=None):
+    """All-gather every rank's head: one int64 meta all-gather, then one padded byte buffer."""
+    world = dist.get_world_size(group)
+    dev = head.ts.device
+    meta = torch.tensor([head.n, head.h, head.keys.numel(), head.vals.numel()], dtype=torch.int64, device=dev)
+    metas = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    metas = [m.cpu().tolist() for m in metas]
+    H = max(m[1] for m in metas)
+    KB = max(m[2] for m in metas)
+    VB = max(m[3] for m in metas)
+
+    def pad(t, n):
+        out = torch.zeros(n, dtype=t.dtype, device=dev)
+        out[:t.numel()].copy_(t)
+        return out
+    buf = torch.cat([pad(head.ko, H + 1).view(torch.uint8), pad(head.vo, H + 1).view(torch.uint8),
+                     pad(head.ts, max(H, 1)).view(torch.uint8), pad(head.keys, max(KB, 1)),
+                     pad(head.vals, max(VB, 1))])
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
+    heads = []
+    o1 = 8 * (H + 1)
+    o2, o3 = 2 * o1, 2 * o1 + 8 * max(H, 1)
+    o4 = o3 + max(KB, 1)
+    for (n, h, kb, vb), b in zip(metas, bufs):
+        heads.append(Head(n, b[:o1].view(torch.int64)[:h + 1], b[o1:o2].view(torch.int64)[:h + 1],
+                          b[o2:o3].view(torch.int64)[:h], b[o3:o3 + kb], b[o4:o4 + vb]))
+    return heads
+
+
+def compact_dist(shard: RangeShard, group=None):
+    """One range per rank (rank order = key order) over torch.distributed: merge, all-gather the
+    heads, prepare, carry from rank - 1 to rank + 1, encode.  Returns the rank's result."""
+    if shard.dev.type == "cuda":
+        with torch.cuda.stream(shard.stream):
+            return _compact_dist(shard, group)
+    return _compact_dist(shard, group)
+
+
+def _compact_dist(shard, group):
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    shard.merge()
+    heads = _allgather_heads(shard.head(), group)
+    shard.set_halo(*assemble_halo(heads, rank, shard.W))
+    shard.prepare()
+    cin = torch.zeros(2, dtype=torch.int64, device=shard.dev)
+    if rank > 0:
+        dist.recv(cin, src=rank - 1, group=group)
+    cout = shard.carry(cin)
+    if rank + 1 < world:
+        dist.send(cout, dst=rank + 1, group=group)
+    shard.encode()
+    return shard.result()

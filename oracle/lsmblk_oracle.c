@@ -503,6 +503,59 @@ done:
   return rc;
 }
 
+/* compact_generate_sst resumed from a range's carry-in (see the header).  The loop is the one of
+ * orc_compact with the rules already applied (ext holds the entries handed to SsTableBuilder::add;
+ * "same as last key" is then the previous ext entry's key): before adding entry e, a new SST starts
+ * when data_len >= target and key(e) != key(e-1) (:278-289); adding e finishes the open block when
+ * BlockBuilder rejects it (builder.rs:55-64), data_len += block + 4.  Entry p itself was already
+ * checked with the data before its block's predecessor was finished. */
+int orc_shard_rotation(const orc_kv* ext, uint64_t m, int last, uint64_t p, uint64_t d0, size_t block_size,
+                       uint64_t target, uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg, uint64_t* p_out,
+                       uint64_t* d_out) {
+  const uint64_t n = ext->n;
+  uint64_t g = 0, data_len = d0;
+  *nseg = 0;
+  if (p >= m) { *p_out = p - m; *d_out = d0; return ORC_OK; }
+  if (m > n) return ORC_E_INVAL;
+  orc_builder* b = orc_builder_new(block_size);
+  if (seg_cap) seg_start[0] = (uint32_t)p;
+  int rc = ORC_E_INVAL;   /* the halo ran out before the first event at or after m */
+  for (uint64_t e = p; e < n; ++e) {
+    const uint8_t* k = ext->keys + ext->key_off[e];
+    size_t kl = ext->key_off[e + 1] - ext->key_off[e];
+    int same = e > 0 && same_key(ext, e - 1, e);
+    if (e > p && data_len >= target && !same) {              /* a new SST starts at e */
+      if (e >= m) { *p_out = e - m; *d_out = 0; rc = ORC_OK; break; }
+      ++g;
+      if (g < seg_cap) seg_start[g] = (uint32_t)e;
+      data_len = 0;
+      orc_builder_free(b);
+      b = orc_builder_new(block_size);
+    }
+    const uint8_t* v = ext->vals + ext->val_off[e];
+    size_t vl = ext->val_off[e + 1] - ext->val_off[e];
+    int a = orc_builder_add(b, k, kl, ext->ts[e], v, vl);
+    if (a < 0) { rc = a; break; }
+    if (a == 0) {                                             /* finish_block: a block starts at e */
+      data_len += orc_builder_estimated_size(b) + 4;
+      if (e >= m) { *p_out = e - m; *d_out = data_len; rc = ORC_OK; break; }
+      orc_builder_free(b);
+      b = orc_builder_new(block_size);
+      orc_builder_add(b, k, kl, ext->ts[e], v, vl);
+    }
+  }
+  if (rc == ORC_E_INVAL && last) {                            /* the stream ended inside the range's SST */
+    uint64_t end = n;
+    *p_out = end - m; *d_out = 0; rc = ORC_OK;
+  }
+  orc_builder_free(b);
+  if (rc) return rc;
+  ++g;
+  if (g < seg_cap) seg_start[g] = (uint32_t)(m + *p_out);
+  *nseg = g;
+  return g + 1 <= seg_cap ? ORC_OK : ORC_E_CAPACITY;
+}
+
 /* ------------------------------------------------------------------ crc32 */
 uint32_t orc_crc32(const uint8_t* p, size_t n) {
   static uint32_t table[256];

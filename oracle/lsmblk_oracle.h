@@ -105,6 +105,18 @@ int orc_compact(const orc_kv* in, const uint32_t* src, uint64_t n, uint64_t wate
                 uint64_t kept_cap, uint64_t* nblk_out, uint64_t* nbytes_out, uint64_t* nsst_out,
                 uint64_t* nkept_out);
 
+/* compact_generate_sst's SST rotation (src/compact.rs:278-289 with SsTableBuilder::add,
+ * table/builder.rs:48-65,105-123) resumed mid-stream, for one range of a key-range split: the
+ * stream `ext` holds the range's m kept entries, then the next entries of the whole stream (the
+ * halo; `last`: ext ends where the whole stream ends).  The loop's state when it reaches the
+ * range's entry p -- a new block starts at p, the open SST's data section holds d0 bytes (d0 = 0:
+ * an SST starts at p) -- is the carry-in.  The loop runs from there until its first event at or
+ * after entry m: an SST starting there (carry-out {e - m, 0}) or a block starting there (carry-out
+ * {e - m, data section}).  seg_start[0..nseg] = p, the SSTs starting in [p, m), the end entry. */
+int orc_shard_rotation(const orc_kv* ext, uint64_t m, int last, uint64_t p, uint64_t d0, size_t block_size,
+                       uint64_t target, uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg, uint64_t* p_out,
+                       uint64_t* d_out);
+
 /* CRC-32/ISO-HDLC (crc32fast 1.4.0 == zlib crc32), used by SST framing. */
 uint32_t orc_crc32(const uint8_t* p, size_t n);
 

@@ -52,6 +52,8 @@ def lib():
         L.orc_compact.argtypes = [P, P, U64, U64, I, P, P, U32, S, U64, P, U64, P, U64, P, P, U64, P, U64,
                                   ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64),
                                   ctypes.POINTER(U64)]
+        L.orc_shard_rotation.argtypes = [P, U64, I, U64, U64, S, U64, P, U64, ctypes.POINTER(U64),
+                                         ctypes.POINTER(U64), ctypes.POINTER(U64)]
         _lib = L
     return _lib
 
@@ -213,6 +215,26 @@ def compact(kv: KV, src, watermark, bottom, prefixes, block_size, target):
     assert rc == ORC_OK, rc
     return dict(blocks=out[:nbytes.value], blk_off=blk_off[:nb.value + 1], sst_blk=sst_blk[:nsst.value + 1],
                 sst_ent=sst_ent[:nsst.value + 1], kept=kept[:nk.value])
+
+
+def shard_rotation(ext: KV, m: int, last: bool, p: int, d0: int, block_size: int, target: int):
+    """compact_generate_sst's rotation resumed at a range's carry-in (orc_shard_rotation) ->
+    (rc, segments u32[nseg+1], (p_out, d_out))."""
+    seg = np.zeros(ext.n + 3, np.uint32)
+    ns, po, do = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    c = ext._c()
+    rc = lib().orc_shard_rotation(ctypes.byref(c), m, int(bool(last)), p, d0, block_size, target, seg.ctypes.data,
+                                  len(seg), ctypes.byref(ns), ctypes.byref(po), ctypes.byref(do))
+    return rc, seg[:ns.value + 1] if ns.value else seg[:0], (po.value, do.value)
+
+
+def encode_span(kv: KV, seg, block_size: int):
+    """Blocks of the segments seg[0..] of kv, which may start after entry 0 and end before kv.n."""
+    seg = np.asarray(seg, np.int64)
+    if len(seg) < 2:
+        return 0, np.zeros(0, np.uint8), np.zeros(1, np.uint64)
+    sub = gather(kv, np.arange(seg[0], seg[-1]))
+    return encode_segments(sub, (seg - seg[0]).astype(np.uint32), block_size)
 
 
 class Builder:

@@ -1,0 +1,155 @@
+"""Key-range sharded compaction on the device (SURVEY.md §8 e, compaction-shaped): several ranges
+driven through lsmblk_compact_merge_batch / lsmblk_shard_* on one GPU with the in-process exchange
+(shard.compact_local -- the same phases and messages as the RCCL driver).  Bar: the concatenated
+blocks and the SST boundaries equal the single-stream compaction (lsmblk_compact_batch and the C
+oracle's compact_generate_sst), and every range's segments and carry equal the oracle's
+compact_generate_sst resumed at that range's carry-in (orc_shard_rotation)."""
+import numpy as np
+import pytest
+import torch
+
+from lsm_amd import batch, shard, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+def case(seed, versions=1, nkeys=6000, nrun=5, tomb=0.05):
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(nkeys, nrun=nrun, seed=seed, versions=versions, tombstone=tomb)
+    return O.KV(keys, ko, vals, vo, ts), rs
+
+
+def to_dev(kv: O.KV):
+    return batch.KVStream.from_numpy(kv.keys, kv.key_off, kv.vals, kv.val_off, kv.ts)
+
+
+def pick_splitters(kv: O.KV, rng, k, tiny=False):
+    """k sorted distinct splitters: existing keys, and byte strings between keys."""
+    allk = sorted({kv.entry(i)[0] for i in range(kv.n)})
+    out = set()
+    while len(out) < k:
+        i = int(rng.integers(1, len(allk)))
+        out.add(allk[i] if rng.random() < 0.6 else allk[i][:int(rng.integers(1, 16))] + b"\x00")
+        if tiny and len(out) < k:       # a range holding one key
+            out.add(allk[min(i + 1, len(allk) - 1)])
+    return sorted(out)[:k]
+
+
+def run_ranges(kv_dev, rs, opts, splitters, inputs=None):
+    shards = []
+    for r in range(len(splitters) + 1):
+        lo, hi = shard.range_of(r, splitters)
+        kv_r, rs_r = inputs[r] if inputs else (kv_dev, rs)
+        shards.append(shard.RangeShard(kv_r, rs_r, opts, lo, hi))
+    return shard.compact_local(shards), shards
+
+
+def check_against_single_stream(kv, rs, res, wm, bottom, bs, target):
+    src = O.merge_runs(kv, rs)
+    want = O.compact(kv, src, wm, bottom, (), bs, target)
+    blocks = b"".join(r["blocks"].cpu().numpy().tobytes() for r in res)
+    assert blocks == want["blocks"].tobytes()
+    bases = np.concatenate([[0], np.cumsum([r["m"] for r in res])]).tolist()
+    assert bases[-1] == len(want["kept"])
+    assert shard.sst_starts(res, bases) == want["sst_ent"][:-1].tolist()
+    for a, b in zip(res, res[1:]):
+        assert a["carry_out"] == b["carry_in"]
+    return want, O.gather(kv, src[want["kept"]]), bases
+
+
+def check_each_range_against_resumed_oracle(kept, res, bases, bs, target):
+    W = shard.halo_entries(bs)
+    for r, base in zip(res, bases):
+        e = min(base + r["m"] + W, kept.n)
+        ext = O.gather(kept, np.arange(base, e))
+        rc, seg, cout = O.shard_rotation(ext, r["m"], e == kept.n, *r["carry_in"], bs, target)
+        assert rc == 0
+        assert cout == r["carry_out"]
+        assert r["seg_start"].tolist() == seg.tolist()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sharded_compaction_equals_single_stream(seed):
+    rng = np.random.default_rng(seed)
+    kv, rs = case(600 + seed, versions=1 + seed % 3)
+    bs, target = [(4096, 32 << 10), (1024, 8 << 10), (256, 3000), (4096, 1 << 20)][seed]
+    wm, bottom = int(kv.ts.max()) // 2, bool(seed % 2)
+    d = to_dev(kv)
+    opts = batch.compact_opts(wm, bottom, block_size=bs, target_sst_size=target)
+    single = batch.compact_runs(d, rs, wm, bottom, block_size=bs, target_sst_size=target)
+    for k in (1, 3, 7):
+        res, _ = run_ranges(d, rs, opts, pick_splitters(kv, rng, k))
+        want, kept, bases = check_against_single_stream(kv, rs, res, wm, bottom, bs, target)
+        assert b"".join(r["blocks"].cpu().numpy().tobytes() for r in res) == \
+            single["blocks"].cpu().numpy().tobytes()
+        check_each_range_against_resumed_oracle(kept, res, bases, bs, target)
+
+
+def test_tiny_and_empty_ranges():
+    """Ranges of one key (swallowed by a crossing block) and ranges with no keys at all."""
+    rng = np.random.default_rng(11)
+    kv, rs = case(41, versions=2, nkeys=1500)
+    d = to_dev(kv)
+    opts = batch.compact_opts(0, False, block_size=4096, target_sst_size=16 << 10)
+    sp = pick_splitters(kv, rng, 6, tiny=True) + [b"\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff"]
+    sp = [b"\x00"] + sorted(set(sp))             # range 0 empty, the last range empty
+    res, _ = run_ranges(d, rs, opts, sp)
+    assert res[0]["m"] == 0 and res[-1]["m"] == 0
+    want, kept, bases = check_against_single_stream(kv, rs, res, 0, False, 4096, 16 << 10)
+    check_each_range_against_resumed_oracle(kept, res, bases, 4096, 16 << 10)
+
+
+def test_ranges_read_only_their_blocks_decode_merge_encode():
+    """The §8 e pipeline from SST blocks: each range decodes only the blocks of every run that
+    overlap it (straddling blocks read by both neighbours), merges its own keys, and the ranges
+    together give the single-stream compaction."""
+    rng = np.random.default_rng(5)
+    kv, rs = case(900, versions=2, nkeys=8000, nrun=4)
+    bs, target = 4096, 48 << 10
+    runs = []
+    for r in range(len(rs) - 1):
+        sub = O.gather(kv, np.arange(rs[r], rs[r + 1]))
+        seg = synth.segments_by_bytes(sub.key_off, sub.val_off, 64 << 10)
+        blocks, off = batch.encode_kv(to_dev(sub), seg, bs)
+        dec = batch.decode_blocks(blocks, off)
+        keys, ko, _, _, _ = dec.to_numpy()
+        runs.append((blocks, off.cpu().numpy().view(np.uint64), keys, ko))
+    splitters = pick_splitters(kv, rng, 3)
+    inputs = []
+    for g in range(len(splitters) + 1):
+        lo, hi = shard.range_of(g, splitters)
+        parts, rstarts = [], [0]
+        for blocks, off, keys, ko in runs:
+            # block first / last keys from the decoded run (BlockMeta's first_key / last_key)
+            dec = batch.decode_blocks(blocks, torch.from_numpy(off.view(np.int64)).cuda(), with_blk_ent=True)[1]
+            ent = dec.cpu().numpy().view(np.uint64)
+            fk = [bytes(keys[ko[ent[b]]:ko[ent[b] + 1]]) for b in range(len(off) - 1)]
+            lk = [bytes(keys[ko[ent[b + 1] - 1]:ko[ent[b + 1]]]) for b in range(len(off) - 1)]
+            sel = [b for b in range(len(off) - 1) if (lo is None or lk[b] >= lo) and (hi is None or fk[b] < hi)]
+            if sel:
+                a, z = sel[0], sel[-1] + 1
+                seg_blocks = blocks[int(off[a]):int(off[z])]
+                seg_off = torch.from_numpy((off[a:z + 1] - off[a]).view(np.int64)).cuda()
+                parts.append(batch.decode_blocks(seg_blocks.contiguous(), seg_off))
+            rstarts.append(rstarts[-1] + (parts[-1].n if sel else 0))
+        cat = [p.to_numpy() for p in parts]
+        k_all = np.concatenate([c[0] for c in cat]) if cat else np.zeros(0, np.uint8)
+        v_all = np.concatenate([c[2] for c in cat]) if cat else np.zeros(0, np.uint8)
+        ko_all = np.concatenate([[0]] + [c[1][1:].astype(np.int64) + sum(len(x[0]) for x in cat[:i])
+                                         for i, c in enumerate(cat)]).astype(np.uint32)
+        vo_all = np.concatenate([[0]] + [c[3][1:].astype(np.int64) + sum(len(x[2]) for x in cat[:i])
+                                         for i, c in enumerate(cat)]).astype(np.uint32)
+        ts_all = np.concatenate([c[4] for c in cat]) if cat else np.zeros(0, np.uint64)
+        inputs.append((batch.KVStream.from_numpy(k_all, ko_all, v_all, vo_all, ts_all),
+                       np.array(rstarts, np.uint32)))
+    wm = int(kv.ts.max()) // 3
+    opts = batch.compact_opts(wm, True, block_size=bs, target_sst_size=target)
+    res, _ = run_ranges(None, None, opts, splitters, inputs)
+    want, kept, bases = check_against_single_stream(kv, rs, res, wm, True, bs, target)
+    check_each_range_against_resumed_oracle(kept, res, bases, bs, target)

@@ -1,0 +1,148 @@
+"""Key-range sharded compaction over torch.distributed (gloo, CPU, world 2 and 3): the product's
+exchange driver shard.compact_dist -- splitter all-gather, head all-gather + halo assembly, carry
+send/recv -- run with a CPU stand-in for the device stages (OracleShard: the C oracle's merge /
+compact_generate_sst rules / resumed rotation / encode, test infrastructure only).  Bar: the ranks'
+outputs concatenate to the single-stream compaction, SST boundaries included."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lsm_amd import shard, synth
+
+BS, TARGET = 1024, 12 << 10
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def global_input(seed=7):
+    from oracle import oracle as O
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(3000, nrun=4, seed=seed, versions=2, tombstone=0.05)
+    return O.KV(keys, ko, vals, vo, ts), rs
+
+
+class OracleShard:
+    """CPU stand-in for shard.RangeShard (same phase methods) over the C oracle."""
+
+    def __init__(self, kv, rs, wm, bottom, lo, hi):
+        from oracle import oracle as O
+        self.O, self.dev, self.W = O, torch.device("cpu"), BS // 16 + 2
+        src = O.merge_runs(kv, rs)
+        kept = O.gather(kv, src[O.compact(kv, src, wm, bottom, (), BS, 1 << 62)["kept"]])
+        keep = [i for i in range(kept.n) if (lo is None or kept.entry(i)[0] >= lo) and
+                (hi is None or kept.entry(i)[0] < hi)]
+        self.kept = O.gather(kept, np.array(keep, np.int64))
+
+    def merge(self):
+        self.m = self.kept.n
+        return self.m
+
+    def head(self):
+        h = min(self.W, self.m)
+        k = self.kept
+        t = (lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)))
+        return shard.Head(self.m, t(k.key_off[:h + 1], np.int64), t(k.val_off[:h + 1], np.int64),
+                          t(k.ts[:h].view(np.int64), np.int64), t(k.keys[:k.key_off[h]], np.uint8),
+                          t(k.vals[:k.val_off[h]], np.uint8))
+
+    def set_halo(self, keys, ko, vals, vo, ts, last):
+        O, k = self.O, self.kept
+        self.ext = O.KV(np.concatenate([k.keys[:k.key_off[-1]], keys.numpy()]),
+                        np.concatenate([k.key_off, ko.numpy()[1:] + k.key_off[-1]]).astype(np.uint32),
+                        np.concatenate([k.vals[:k.val_off[-1]], vals.numpy()]),
+                        np.concatenate([k.val_off, vo.numpy()[1:] + k.val_off[-1]]).astype(np.uint32),
+                        np.concatenate([k.ts, ts.numpy().view(np.uint64)]))
+        self.last = last
+
+    def prepare(self):
+        pass
+
+    def carry(self, cin):
+        self.cin = tuple(int(x) for x in cin.tolist())
+        rc, self.seg, cout = self.O.shard_rotation(self.ext, self.m, self.last, *self.cin, BS, TARGET)
+        assert rc == 0
+        self.cout = cout
+        return torch.tensor(cout, dtype=torch.int64)
+
+    def encode(self):
+        rc, self.blocks, _ = self.O.encode_span(self.ext, self.seg, BS)
+        assert rc == 0
+
+    def result(self):
+        nseg = max(len(self.seg) - 1, 0)
+        return dict(blocks=self.blocks.tobytes(), seg_start=self.seg, nseg=nseg, m=self.m,
+                    first_continues=nseg > 0 and self.cin[1] > 0, carry_in=self.cin, carry_out=self.cout)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kv, rs = global_input()
+        # every rank "holds" a slice of every run: sample the first keys of its slice's 32-entry blocks
+        n = kv.n
+        mine = [kv.entry(i)[0] for i in range(rank * n // world, (rank + 1) * n // world, 32)]
+        splitters = shard.exchange_splitters(sorted(mine), samples=16)
+        lo, hi = shard.range_of(rank, splitters)
+        s = OracleShard(kv, rs, int(kv.ts.max()) // 2, True, lo, hi)
+        res = shard.compact_dist(s)
+        q.put((rank, res["blocks"], res["seg_start"].tolist(), res["nseg"], res["m"], res["first_continues"],
+               res["carry_in"], res["carry_out"], splitters))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_compaction_equals_single_stream(world):
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=200) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert all(r[8] == res[0][8] and len(r[8]) == world - 1 for r in res)
+    kv, rs = global_input()
+    src = O.merge_runs(kv, rs)
+    want = O.compact(kv, src, int(kv.ts.max()) // 2, True, (), BS, TARGET)
+    assert b"".join(r[1] for r in res) == want["blocks"].tobytes()
+    results = [dict(seg_start=np.array(r[2], np.uint32), nseg=r[3], first_continues=r[5]) for r in res]
+    bases = np.concatenate([[0], np.cumsum([r[4] for r in res])]).tolist()
+    assert shard.sst_starts(results, bases) == want["sst_ent"][:-1].tolist()
+    for a, b in zip(res, res[1:]):
+        assert a[7] == b[6]
+    assert any(r[5] for r in res)  # some SST crosses a rank boundary
+
+
+def test_assemble_halo_spans_short_ranges():
+    """A range shorter than the halo contributes all its entries and the next range continues."""
+    def head(n, h, base):
+        return shard.Head(n, torch.arange(h + 1, dtype=torch.int64) * 2, torch.arange(h + 1, dtype=torch.int64),
+                          torch.arange(base, base + h, dtype=torch.int64),
+                          torch.arange(2 * h, dtype=torch.uint8), torch.arange(h, dtype=torch.uint8))
+    heads = [head(100, 5, 0), head(2, 2, 100), head(0, 0, 200), head(50, 5, 300)]
+    keys, ko, vals, vo, ts, last = shard.assemble_halo(heads, 0, 5)
+    assert ts.tolist() == [100, 101, 300, 301, 302] and not last
+    assert ko.tolist() == [0, 2, 4, 6, 8, 10] and keys.numel() == 10 and vals.numel() == 5
+    keys, ko, vals, vo, ts, last = shard.assemble_halo(heads, 1, 5)
+    assert ts.tolist() == [300, 301, 302, 303, 304] and not last
+    assert shard.assemble_halo(heads, 3, 5)[-1] is True           # the last range
+    heads[3] = head(3, 3, 300)
+    assert shard.assemble_halo(heads, 0, 9)[4].tolist() == [100, 101, 300, 301, 302]
+    assert shard.assemble_halo(heads, 0, 9)[-1] is True           # the halo reached the stream's end
