@@ -292,6 +292,8 @@ def reduce_ranks(elapsed, ok, checked, world, dev):
     if world == 1:
         return elapsed, ok, checked
     import torch.distributed as dist
+    from lsm_amd.shard import comm_device
+    dev = comm_device(dev)
     tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     cc = torch.tensor([checked], dtype=torch.int64, device=dev)
@@ -301,13 +303,14 @@ def reduce_ranks(elapsed, ok, checked, world, dev):
 
 # ---------------------------------------------------------------------------------------------
 # config C: compaction-shaped decode -> merge -> rules -> rotation -> encode
-def build_runs(nblk, nrun, seg_bytes, seed, dev, key_lo=0, key_hi=None):
+def build_runs(nblk, nrun, seg_bytes, seed, dev, key_slice=(0, 1)):
     """nrun overlapping sorted runs (L0 SSTs of seg_bytes each), about nblk 4 KiB blocks in all,
     encoded on the device; returns the concatenated input blocks, their offsets, the per-run
-    entry starts, and the host KV (for the oracle)."""
+    entry starts, and the host KV (for the oracle).  key_slice = (s, w): this rank's storage holds
+    slice s of w of the key space."""
     t = time.time()
     n_keys = int(nblk * 31.0 / 1.1)
-    keys, ko, vals, vo, ts, rs = synth.gen_runs(n_keys, nrun=nrun, seed=seed)
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(n_keys, nrun=nrun, seed=seed, key_slice=key_slice)
     parts, offs, base = [], [], 0
     for r in range(nrun):
         a, b = int(rs[r]), int(rs[r + 1])
@@ -349,7 +352,41 @@ def oracle_check_compaction(host, rs, opts, buf, stats):
     return nblk if ok else 0
 
 
+def oracle_check_range(host, rs, opts, sh, res):
+    """One range of the sharded compaction against the C oracle: the range's kept stream ==
+    orc_merge_runs + compact_generate_sst's rules over the rank's input; its segments, carry-out
+    and blocks == compact_generate_sst resumed at the received carry-in (orc_shard_rotation) over
+    that stream + the received halo.  Chained over the ranks (carry-out r == carry-in r+1, checked
+    by the caller) this is the whole single-stream compaction."""
+    from oracle import oracle as O
+    t = time.time()
+    kv = O.KV(*host)
+    src = O.merge_runs(kv, rs)
+    kept = O.gather(kv, src[O.compact(kv, src, opts["watermark"], opts["bottom_level"], (), opts["block_size"],
+                                      1 << 62)["kept"]])
+    m = sh.m
+    ok = kept.n == m
+    ek, eko, ev, evo, ets = batch.KVStream(sh.ext.keys, sh.ext.key_off, sh.ext.vals, sh.ext.val_off, sh.ext.ts,
+                                           sh.ext.n).to_numpy()
+    ok = ok and np.array_equal(eko[:m + 1], kept.key_off) and np.array_equal(evo[:m + 1], kept.val_off)
+    ok = ok and np.array_equal(ets[:m], kept.ts) and np.array_equal(ek[:kept.key_off[-1]], kept.keys)
+    ok = ok and np.array_equal(ev[:kept.val_off[-1]], kept.vals)
+    if ok:
+        ext = O.KV(ek, eko, ev, evo, ets)
+        rc, seg, cout = O.shard_rotation(ext, m, sh.last, *res["carry_in"], opts["block_size"], opts["target_sst_size"])
+        ok = rc == 0 and cout == res["carry_out"] and seg.tolist() == res["seg_start"].tolist()
+        if ok and len(seg):
+            rc, blk, off = O.encode_span(ext, seg, opts["block_size"])
+            ok = rc == 0 and np.array_equal(blk, res["blocks"].cpu().numpy())
+            ok = ok and np.array_equal(off, res["blk_off"].cpu().numpy().view(np.uint64))
+    log(f"[rank] oracle check of the range ({res['nblk']} output blocks, {res['nseg']} segments, carry "
+        f"{res['carry_in']} -> {res['carry_out']}): {'ok' if ok else 'MISMATCH'} ({time.time() - t:.1f}s)")
+    return res["nblk"] if ok else 0
+
+
 def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
+    if world > 1:
+        return run_compaction_sharded(args, steps, warmup, rank, world, local, dev)
     nblk_in = args.blocks or (1 << 20)
     nrun = 8
     blocks, blk_off, rs, host = build_runs(nblk_in, nrun, args.segment_bytes, 2000 + rank, dev)
@@ -413,6 +450,90 @@ def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
     }
 
 
+def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
+    """Config C over N GPUs, split by key range: rank r's storage holds
+    slice r of the key space in every run (its L0 SSTs' blocks, resident in HBM); the splitters are
+    the ranks' lowest BlockMeta first keys (one all-gather), so no input block belongs to two
+    ranges.  One step = decode + merge / rules (range-restricted) + halo all-gather + rotation +
+    carry send/recv + block packing (shard.compact_dist): together the ranks' outputs are the
+    single-stream compaction of all N slices, byte for byte, SST boundaries included."""
+    import torch.distributed as dist
+    from lsm_amd import shard
+    nblk_in = args.blocks or (1 << 20)
+    nrun = 8
+    blocks, blk_off, rs, host = build_runs(nblk_in, nrun, args.segment_bytes, 2000 + rank, dev,
+                                           key_slice=(rank, world))
+    nblk = blk_off.numel() - 1
+    E = int(blocks.numel())
+    n = int(rs[-1])
+    K, V = len(host[0]), len(host[2])
+    keys, ko = host[0], host[1]
+    first = min(bytes(keys[ko[rs[r]]:ko[rs[r] + 1]]) for r in range(nrun) if rs[r] < rs[r + 1])
+    cdev = shard.comm_device(dev)
+    splitters = shard.exchange_splitters([first], samples=1, device=cdev)
+    lo, hi = shard.range_of(rank, splitters)
+    kv = batch.KVStream.empty(n, K, V, dev)
+    st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
+    # one wm for the whole job (the reference's LsmMvccInner::watermark is global)
+    wm = torch.tensor([int(host[4].max()) // 2], dtype=torch.int64, device=cdev)
+    dist.all_reduce(wm, op=dist.ReduceOp.MAX)
+    opts = batch.compact_opts(watermark=int(wm.item()), bottom_level=True, block_size=4096,
+                              target_sst_size=args.segment_bytes, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = shard.RangeShard(kv, rs, opts, lo, hi, stream=stream)
+    res = {}
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        batch.decode_into(blocks, blk_off, nblk, kv, st_dec, n, K + 16, V + 16)
+        kv.n = n
+        if ev is not None:
+            ev[1].record(stream)
+        res.update(shard.compact_dist(sh))
+        if ev is not None:
+            ev[2].record(stream)
+
+    elapsed, (dec_ms, cmp_ms) = timed(step, steps, warmup, world, dev)
+    sd = st_dec.cpu().tolist()
+    ok = sd[3] == 0 and sd[0] == n
+    checked = 0
+    if ok and not args.no_oracle_check:
+        checked = oracle_check_range(host, rs, opts, sh, res)
+        ok = checked == res["nblk"]
+    # the carries chain: carry-out of rank r == carry-in of rank r + 1
+    cc = torch.tensor(list(res["carry_in"]) + list(res["carry_out"]), dtype=torch.int64, device=cdev)
+    allc = [torch.zeros_like(cc) for _ in range(world)]
+    dist.all_gather(allc, cc)
+    allc = [c.cpu().tolist() for c in allc]
+    chain_ok = allc[0][:2] == [0, 0] and all(allc[r][2:] == allc[r + 1][:2] for r in range(world - 1))
+    tot = torch.tensor([res["nblk"], res["nbytes"], res["nseg"] - int(res["first_continues"]), res["m"],
+                        res["merged"]], dtype=torch.int64, device=cdev)
+    dist.all_reduce(tot)
+    t_max, ok_all, checked_all = reduce_ranks(elapsed, ok and chain_ok, checked, world, dev)
+    if rank != 0:
+        return None
+    ms = t_max / steps * 1e3
+    tot = tot.cpu().tolist()
+    return {
+        "metric": METRIC, "value": round(world * E * steps / t_max / GiB, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"C: compaction-shaped, {nrun} overlapping sorted runs of {args.segment_bytes >> 20} MiB "
+                               f"SSTs ({nblk} x 4 KiB input blocks/GPU, ~10% overwrites, 2% tombstones), split by "
+                               f"key range over {world} GPUs: decode + range merge + compaction rules + halo "
+                               "all-gather + SST rotation with rank-to-rank carry + block packing",
+                   "input_blocks_per_gpu": nblk, "input_entries_per_gpu": n, "encoded_bytes_per_gpu": E,
+                   "merged_entries": tot[4], "kept_entries": tot[3], "output_blocks": tot[0], "output_bytes": tot[1],
+                   "output_ssts": tot[2], "target_sst_size": args.segment_bytes,
+                   "parallelism": f"key-range sharded x{world} ({'RCCL' if dist.get_backend() == 'nccl' else 'gloo'}: "
+                                  "splitter + halo all-gather, carry send/recv)",
+                   "rccl_world": world, "compaction_bit_exact": bool(ok_all), "carry_chain_ok": bool(chain_ok),
+                   "oracle_checked_blocks": int(checked_all)},
+        "stage_ms": {"decode": round(dec_ms, 4), "compact": round(cmp_ms, 4)},
+    }
+
+
 def dry_run(rank, world, local):
     """The launcher's contract without a GPU: every rank joins one gloo group; rank 0 reports the
     world size the collective saw and the ranks it heard from."""
@@ -444,12 +565,20 @@ def main():
         return 2
     if args.dry_run:
         return dry_run(rank, world, local)
+    # diagnostics only: LSMBLK_BENCH_BACKEND=gloo runs the N-rank logic with host-side collectives,
+    # e.g. several ranks sharing the one GPU of a test box
+    backend = os.environ.get("LSMBLK_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         if dist.get_world_size() != args.gpus:
             log(f"refusing to run: RCCL world {dist.get_world_size()} != --gpus {args.gpus}")
             return 2
@@ -467,6 +596,16 @@ def main():
         torch.cuda.empty_cache()
         extras["C"] = run_compaction(args, 3, 1, rank, world, local, dev, extra=True)
         result["extra_configs"] = extras
+    elif world > 1 and args.config == "U" and not args.no_extras and args.blocks is None:
+        # the compaction-shaped config split by key range over the same N GPUs (one extra line)
+        torch.cuda.empty_cache()
+        try:
+            c = run_compaction(args, 3, 1, rank, world, local, dev, extra=True)
+        except Exception as e:  # an extra never takes the headline line down
+            log(f"[rank {rank}] extra config C failed: {e!r}")
+            c = {"error": repr(e)}
+        if result is not None:
+            result["extra_configs"] = {"C": c}
     ok = True
     if world > 1:
         import torch.distributed as dist

@@ -143,6 +143,10 @@ class Head:
     def h(self):
         return self.ts.numel()
 
+    def to(self, device):
+        return Head(self.n, self.ko.to(device), self.vo.to(device), self.ts.to(device), self.keys.to(device),
+                    self.vals.to(device))
+
 
 def assemble_halo(heads, g: int, W: int):
     """Rank g's halo: the first W entries after its range, from the heads of the ranks after it
@@ -199,13 +203,14 @@ class RangeShard:
         self._lo = self._bound(lo)
         self._hi = self._bound(hi)
         self.range_c = batch.key_range_c(self._lo, self._hi)
-        self.K_in, self.V_in = kv.byte_sizes()
+        # the input's capacities bound the kept stream (the input may not be decoded yet)
+        self.n_in, self.K_in, self.V_in = kv.key_off.numel() - 1, kv.keys.numel(), kv.vals.numel()
         self.kept = None
         self.mstats = torch.zeros(5, dtype=torch.int64, device=self.dev)
         self.cout = torch.zeros(2, dtype=torch.int64, device=self.dev)
         self.estats = torch.zeros(8, dtype=torch.int64, device=self.dev)
         self.out = None
-        self._grow_kept(kv.n + self.W, self.K_in + 64 * self.W, self.V_in + 256 * self.W)
+        self._grow_kept(self.n_in + self.W, self.K_in + 64 * self.W, self.V_in + 256 * self.W)
 
     def _bound(self, b):
         if b is None:
@@ -396,17 +401,24 @@ def compact_dist(shard: RangeShard, group=None):
     return _compact_dist(shard, group)
 
 
+def comm_device(device, group=None):
+    """Where a collective's tensors live: the GPU for RCCL, the host for gloo."""
+    return torch.device("cpu") if dist.get_backend(group) == "gloo" else torch.device(device)
+
+
 def _compact_dist(shard, group):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
+    cdev = comm_device(shard.dev, group)
     shard.merge()
-    heads = _allgather_heads(shard.head(), group)
-    shard.set_halo(*assemble_halo(heads, rank, shard.W))
+    heads = _allgather_heads(shard.head().to(cdev), group)
+    halo = assemble_halo(heads, rank, shard.W)
+    shard.set_halo(*[x.to(shard.dev) for x in halo[:5]], halo[5])
     shard.prepare()
-    cin = torch.zeros(2, dtype=torch.int64, device=shard.dev)
+    cin = torch.zeros(2, dtype=torch.int64, device=cdev)
     if rank > 0:
         dist.recv(cin, src=rank - 1, group=group)
-    cout = shard.carry(cin)
+    cout = shard.carry(cin.to(shard.dev))
     if rank + 1 < world:
-        dist.send(cout, dst=rank + 1, group=group)
+        dist.send(cout.to(cdev), dst=rank + 1, group=group)
     shard.encode()
     return shard.result()

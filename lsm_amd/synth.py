@@ -22,10 +22,13 @@ def _random_bytes(rng, n):
     return np.frombuffer(rng.bytes(int(n)), np.uint8).copy() if n else np.zeros(0, np.uint8)
 
 
-def _sorted_keys16(rng, n):
-    """n sorted unique 16-B keys spread uniformly over the 128-bit space."""
-    step = np.uint64((2 ** 64 - 1) // max(n, 1))
-    hi = np.arange(n, dtype=np.uint64) * step + rng.integers(0, int(step), n, dtype=np.uint64)
+def _sorted_keys16(rng, n, key_slice=(0, 1)):
+    """n sorted unique 16-B keys spread uniformly over the 128-bit space, or over slice s of w
+    equal slices of it (key_slice = (s, w): a storage shard of a key-range-partitioned dataset)."""
+    s, w = key_slice
+    width = (2 ** 64 - 1) // w
+    step = np.uint64(width // max(n, 1))
+    hi = np.uint64(s * width) + np.arange(n, dtype=np.uint64) * step + rng.integers(0, int(step), n, dtype=np.uint64)
     lo = rng.integers(0, 2 ** 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
     k = np.empty((n, 16), np.uint8)
     k[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
@@ -78,15 +81,16 @@ def gen_mixed(n, seed=44, vmin=8, vmax=4096):
     return keys, _offsets(np.full(n, 16, np.uint64)), vals, _offsets(vl), _ts(rng, n)
 
 
-def gen_runs(n_keys, nrun=8, overwrite=0.10, tombstone=0.02, seed=45, value_len=100, versions=1):
+def gen_runs(n_keys, nrun=8, overwrite=0.10, tombstone=0.02, seed=45, value_len=100, versions=1, key_slice=(0, 1)):
     """Compaction-shaped input (SURVEY.md section 8(d) config 5 at one-GPU scale): `nrun` sorted
     runs (L0 SSTs, run 0 the newest) over one key space with overlapping ranges.  Every key has
     a home run; a fraction `overwrite` also appears in a second run.  A run holds `versions`
     versions per key it contains (newest first, as SsTableBuilder receives them); ts are larger
     in newer runs; `tombstone` of the values are empty (deletes).  Returns (keys, key_off, vals,
-    val_off, ts, run_start) with the runs concatenated in priority order."""
+    val_off, ts, run_start) with the runs concatenated in priority order.  key_slice: keys from
+    one slice of the key space only (see _sorted_keys16)."""
     rng = np.random.default_rng(seed)
-    base = _sorted_keys16(rng, n_keys).reshape(n_keys, 16)
+    base = _sorted_keys16(rng, n_keys, key_slice).reshape(n_keys, 16)
     home = rng.integers(0, nrun, n_keys)
     extra = rng.random(n_keys) < overwrite
     second = (home + rng.integers(1, max(nrun, 2), n_keys)) % max(nrun, 1)
