@@ -248,7 +248,9 @@ class RangeShard:
     # -- phase 2: halo
     def head(self) -> Head:
         with torch.cuda.stream(self.stream):
-            return self._head()
+            hd = self._head()
+        self.stream.synchronize()  # the head is read on other streams (the exchange)
+        return hd
 
     def _head(self) -> Head:
         h = min(self.W, self.m)
@@ -258,8 +260,10 @@ class RangeShard:
         return Head(self.m, ko, vo, self.kept.ts[:h].clone(), self.kept.keys[:kb].clone(), self.kept.vals[:vb].clone())
 
     def set_halo(self, keys, ko, vals, vo, ts, last: bool):
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))  # the halo was assembled there
         with torch.cuda.stream(self.stream):
             self._set_halo(keys, ko, vals, vo, ts, last)
+        self.stream.synchronize()  # the halo tensors may be freed by the caller right after
 
     def _set_halo(self, keys, ko, vals, vo, ts, last: bool):
         m, h = self.m, ts.numel()
