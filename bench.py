@@ -184,7 +184,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
             ev[2].record(stream)
 
     if args.ablate is not None and not extra:
-        if args.ablate >= 16:  # encode-side masks: per-kernel times with the mask applied
+        if 16 <= args.ablate < 256:  # encode-side masks: per-kernel times with the mask applied
             res = {}
             for mask in (0, 16, 32, 64, 112, 128, 240):
                 check(lib().lsmblk_debug_set(ctx, 1, mask))

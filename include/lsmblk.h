@@ -397,6 +397,16 @@ int lsmblk_sst_files_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_
                            const uint32_t* sst_blk, const uint32_t* sst_ent, uint32_t nsst,
                            const lsmblk_kv_stream* kv, uint8_t* files, uint64_t files_cap, uint64_t* file_off,
                            uint64_t* stats, void* stream);
+/* BlockIterator::create_and_seek_to_key (src/block/iterator.rs:73-94) for a batch of point
+ * lookups (§8 a row 13): lookup q seeks key qkeys[qkey_off[q] .. qkey_off[q+1]) in block q_blk[q]
+ * of (blocks, blk_off, tail as for lsmblk_decode_batch_ex).  idx[q] = the entry index the
+ * iterator lands on -- its binary search with ts-agnostic key order, stopping at the first probe
+ * that compares equal -- or the block's entry count when the iterator ends invalid.  All device
+ * pointers (qkey_off: u32[nq+1], q_blk, idx: u32[nq]).  stats[3]: MALFORMED for a block that does
+ * not parse (idx = its entry count), SEGMENTS for a block index out of range.  Asynchronous. */
+int lsmblk_seek_batch(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+                      const uint8_t* qkeys, const uint32_t* qkey_off, const uint32_t* q_blk, uint64_t nq,
+                      uint32_t* idx, uint64_t* stats, void* stream);
 /* farmhash::fingerprint32 (the key hash of SsTableBuilder::add, src/table/builder.rs:53), host. */
 uint32_t lsmblk_fingerprint32(const uint8_t* key, size_t klen);
 /* Bloom::may_contain (src/table/bloom.rs:104-120) over a decoded filter, host. */

@@ -107,6 +107,7 @@ SIGNATURES = [
     ("lsmblk_memtable_flush", I, [P, P, P, P, P, P, U64, U64, U64, ctypes.POINTER(U64), ctypes.POINTER(U64),
                                   ctypes.POINTER(U64)]),
     ("lsmblk_sst_files_batch", I, [P, P, P, U64, P, P, U32, ctypes.POINTER(KVStreamC), P, U64, P, P, P]),
+    ("lsmblk_seek_batch", I, [P, P, P, U64, U32, P, P, P, U64, P, P, P]),
     ("lsmblk_fingerprint32", U32, [P, S]),
     ("lsmblk_bloom_may_contain", I, [P, S, U32, U32]),
 ]

@@ -607,3 +607,27 @@ def shard_encode_into(ext: KVStream, out, out_cap, blk_off, blk_cap, seg_start, 
                                           blk_off.data_ptr(), blk_cap, seg_start.data_ptr(), seg_blk.data_ptr(),
                                           seg_cap, stats.data_ptr(), _stream_ptr(stream, dev)),
           "lsmblk_shard_encode_batch")
+
+
+def seek_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, q_blk, qkeys, tail: int = 0, stream=None):
+    """BlockIterator::create_and_seek_to_key (reference src/block/iterator.rs:73-94) for a batch of
+    (block index, key) lookups -> int64 numpy array of the entry indices the iterators land on
+    (a block's entry count = ended invalid)."""
+    dev = torch.device("cuda", _dev_index(blk_off))
+    nblk = blk_off.numel() - 1
+    _need(blk_off, torch.int64, "blk_off", dev.index, nblk + 1)
+    kb = b"".join(bytes(k) for k in qkeys)
+    ko = np.zeros(len(qkeys) + 1, np.uint32)
+    ko[1:] = np.cumsum([len(k) for k in qkeys]) if qkeys else []
+    qk = torch.frombuffer(bytearray(kb or b"\0"), dtype=torch.uint8).to(dev)
+    qo, qb = _u32_table(ko, dev), _u32_table(np.asarray(q_blk, np.uint32), dev)
+    idx = torch.zeros(max(len(qkeys), 1), dtype=torch.int32, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    check(lib().lsmblk_seek_batch(_ctx(dev.index, stream), _ptr(blocks), blk_off.data_ptr(), nblk, tail,
+                                  qk.data_ptr(), qo.data_ptr(), qb.data_ptr(), len(qkeys), idx.data_ptr(),
+                                  stats.data_ptr(), _stream_ptr(stream, dev.index)), "lsmblk_seek_batch")
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "seek_blocks")
+    return idx[:len(qkeys)].cpu().numpy().view(np.uint32).astype(np.int64)

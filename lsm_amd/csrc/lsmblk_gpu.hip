@@ -45,7 +45,7 @@ struct DecodeArgs {
   uint32_t tail;              // bytes after each block inside its range (4: the framing CRC)
   uint64_t* blk_ent;          // optional: first entry index of every block
   uint32_t skip;  // ablation mask (lsmblk_debug_set, timing experiments only): 2 keys,
-                  // 4 values, 8 per-entry metadata, 16 value pass 2, 32 value pass 1
+                  // 4 values, 8 per-entry metadata, 256 stop after staging, 512 after the tables
 };
 
 constexpr uint32_t kTile = 64;  // blocks per count tile
@@ -486,6 +486,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   } else {
     h = parse_hdr(GlbImg{R, lead}, len);
   }
+  if (a.skip & 256) return;  // ablation: staging only
   if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
   const bool fast = fits && h.n <= kDecMaxE;
   const bool big = !fits && h.n <= kDecMaxE;  // large block: tables in LDS, bytes from HBM
@@ -536,6 +537,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
       V += wave_sum<uint64_t>(vl);
     }
   }
+  if (a.skip & 512) return;  // ablation: staging + entry tables only
   if (__ballot(bad)) err |= LSMBLK_ERR_MALFORMED;
   uint64_t agg[3] = {h.n, K, V};
   if (err) agg[0] = agg[1] = agg[2] = 0;

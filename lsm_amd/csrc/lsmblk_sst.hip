@@ -17,6 +17,8 @@
 //   sst_bloom_kernel    one workgroup per SST: the key fingerprints set k bits each in an LDS
 //                       bitmap (LDS atomics), CRC of filter | k by the lane-parallel CRC, the
 //                       filter, k, CRC and bloom_offset written into the file.
+// and the read side's point lookup inside a block:
+//   lsmblk_seek_batch   BlockIterator::seek_to_key for a batch of (block, key) lookups
 #include "lsmblk_dev.hpp"
 
 namespace {
@@ -385,9 +387,122 @@ __global__ __launch_bounds__(256) void sst_bloom_kernel(SstArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- batched seek_to_key
+// BlockIterator::seek_to_key (src/block/iterator.rs:80-94), one lane per point lookup: the same
+// binary search (mid = low + (high - low) / 2, returning at the first probe whose key compares
+// equal -- with several versions of a user key in the block that is not necessarily the first of
+// them), keys reconstructed as first_key[..prefix] || suffix (seek_to_offset :125-132) and compared
+// ts-agnostically (src/key.rs:77-81).  A block or probed entry that breaks the decode rules
+//  reports LSMBLK_ERR_MALFORMED and the block's entry count.
+struct SeekArgs {
+  const uint8_t* blocks;
+  const uint64_t* blk_off;
+  uint64_t nblk;
+  uint32_t tail;
+  const uint8_t* qkeys;
+  const uint32_t* qkey_off;
+  const uint32_t* q_blk;
+  uint64_t nq;
+  uint32_t* idx;
+  uint64_t* stats;
+};
+
+__device__ __forceinline__ uint32_t be16_at(const uint8_t* p, uint32_t i) { return (uint32_t(p[i]) << 8) | p[i + 1]; }
+
+__global__ __launch_bounds__(256) void seek_kernel(SeekArgs a) {
+  const uint64_t q = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (q >= a.nq) return;
+  uint32_t err = 0, res = 0;
+  const uint32_t b = a.q_blk[q];
+  const uint8_t* key = a.qkeys + a.qkey_off[q];
+  const uint32_t klen = a.qkey_off[q + 1] - a.qkey_off[q];
+  do {
+    if (b >= a.nblk) {
+      err = LSMBLK_ERR_SEGMENTS;
+      break;
+    }
+    const uint64_t start = a.blk_off[b], end = a.blk_off[b + 1];
+    if (end < start + a.tail || end - start > 0x7FFFFFF0ull || end - start - a.tail < 2) {
+      err = LSMBLK_ERR_MALFORMED;
+      break;
+    }
+    const uint32_t len = uint32_t(end - start) - a.tail;
+    const uint8_t* p = a.blocks + start;
+    const uint32_t n = be16_at(p, len - 2);
+    res = n;
+    if (2 + 2 * n > len) {
+      err = LSMBLK_ERR_MALFORMED;
+      break;
+    }
+    const uint32_t data_end = len - 2 - 2 * n;
+    uint32_t fks = 0;
+    if (n) {
+      if (data_end < 4 || 4 + (fks = be16_at(p, 2)) + 8 > data_end) {
+        err = LSMBLK_ERR_MALFORMED;
+        break;
+      }
+    }
+    uint32_t lo = 0, hi = n;
+    bool found = false;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      const uint32_t off = be16_at(p, data_end + 2 * mid);
+      if (off + 4 > data_end) {
+        err = LSMBLK_ERR_MALFORMED;
+        break;
+      }
+      const uint32_t pf = be16_at(p, off), sf = be16_at(p, off + 2);
+      if (!(off + 4 + sf + 10 <= data_end && pf <= fks && pf + sf > 0) ||
+          off + 14 + sf + be16_at(p, off + 12 + sf) > data_end) {
+        err = LSMBLK_ERR_MALFORMED;
+        break;
+      }
+      // key order of first_key[..pf] || suffix against the target
+      const uint32_t kl = pf + sf, m = kl < klen ? kl : klen;
+      int c = 0;
+      for (uint32_t i = 0; i < m && !c; ++i) {
+        const uint32_t x = i < pf ? p[4 + i] : p[off + 4 + i - pf];
+        if (x != key[i]) c = x < key[i] ? -1 : 1;
+      }
+      if (!c) c = kl < klen ? -1 : (kl > klen ? 1 : 0);
+      if (c < 0) {
+        lo = mid + 1;
+      } else if (c > 0) {
+        hi = mid;
+      } else {
+        res = mid;
+        found = true;
+        break;
+      }
+    }
+    if (err) {
+      res = n;
+      break;
+    }
+    if (!found) res = lo;
+  } while (false);
+  a.idx[q] = res;
+  if (err) atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)err);
+}
+
 }  // namespace
 
 extern "C" {
+
+int lsmblk_seek_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
+                      const uint8_t* qkeys, const uint32_t* qkey_off, const uint32_t* q_blk, uint64_t nq, uint32_t* idx,
+                      uint64_t* stats, void* stream) {
+  if (!c || !blk_off || !stats || (nq && (!qkey_off || !q_blk || !idx)) || tail > 16) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  if (nq == 0) return LSMBLK_OK;
+  SeekArgs a{blocks, blk_off, nblk, tail, qkeys, qkey_off, q_blk, nq, idx, stats};
+  hipLaunchKernelGGL(seek_kernel, dim3(uint32_t((nq + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
 
 uint32_t lsmblk_fingerprint32(const uint8_t* key, size_t klen) {
   return fingerprint32(HostKey{key}, uint32_t(klen));
