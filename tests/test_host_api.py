@@ -30,6 +30,13 @@ def test_library_exports_every_header_symbol():
     assert len(header_functions()) >= 30
 
 
+def test_integration_doc_binds_every_header_symbol():
+    """INTEGRATION.md's Rust extern block (tools/gen_rust_ffi.py) names every header function."""
+    doc = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "INTEGRATION.md")).read()
+    missing = [f for f in header_functions() if f"pub fn {f}(" not in doc]
+    assert not missing, missing
+
+
 def test_python_binding_covers_header():
     bound = {n for n, _, _ in SIGNATURES}
     assert set(header_functions()) <= bound
