@@ -56,6 +56,21 @@ def _ctx(device: int, stream=None):
     return _ctx_for(device, _stream_ptr(stream, device)).h
 
 
+class OwnCtx:
+    """A context owned by one object (e.g. a shard.RangeShard, whose rotation state lives on its
+    context between calls), independent of the stream it is used on."""
+
+    def __init__(self, device: int):
+        h = ctypes.c_void_p()
+        check(lib().lsmblk_ctx_create(device, ctypes.byref(h)), "lsmblk_ctx_create")
+        self.h = h.value
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().lsmblk_ctx_destroy(self.h)
+            self.h = None
+
+
 def _stream_ptr(stream, device):
     s = stream if stream is not None else torch.cuda.current_stream(device)
     return s.cuda_stream
@@ -559,7 +574,7 @@ def key_range_c(lo, hi):
 
 
 def compact_merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, key_range, kept: KVStream,
-                       stats, stream=None):
+                       stats, stream=None, ctx=None):
     """Asynchronous lsmblk_compact_merge_batch: merge + rules restricted to key_range (a KeyRangeC
     or None) into preallocated `kept`.  stats: int64[5] device."""
     dev = _dev_index(run_start)
@@ -569,32 +584,32 @@ def compact_merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: d
     _need(stats, torch.int64, "stats", dev, 5)
     o = _opts_c(opts)
     ci, ck = kv._c(), kept._c(*kept.caps())
-    check(lib().lsmblk_compact_merge_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun,
+    check(lib().lsmblk_compact_merge_batch(ctx.h if ctx is not None else _ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun,
                                            ctypes.byref(o), ctypes.byref(key_range) if key_range is not None else None,
                                            ctypes.byref(ck), stats.data_ptr(), _stream_ptr(stream, dev)),
           "lsmblk_compact_merge_batch")
 
 
 def shard_prepare(ext: KVStream, n_own: int, last: bool, block_size: int, target_sst_size: int, sst_cap: int,
-                  stream=None):
+                  stream=None, ctx=None):
     dev = _dev_index(ext.key_off)
     ext.check(dev, "ext")
     c = ext._c()
-    check(lib().lsmblk_shard_rotation_prepare(_ctx(dev, stream), ctypes.byref(c), n_own,
+    check(lib().lsmblk_shard_rotation_prepare(ctx.h if ctx is not None else _ctx(dev, stream), ctypes.byref(c), n_own,
                                               LSMBLK_SHARD_LAST if last else 0, block_size, target_sst_size, sst_cap,
                                               _stream_ptr(stream, dev)), "lsmblk_shard_rotation_prepare")
 
 
-def shard_carry(carry_in: torch.Tensor, carry_out: torch.Tensor, stream=None):
+def shard_carry(carry_in: torch.Tensor, carry_out: torch.Tensor, stream=None, ctx=None):
     dev = _dev_index(carry_in)
     _need(carry_in, torch.int64, "carry_in", dev, 2)
     _need(carry_out, torch.int64, "carry_out", dev, 2)
-    check(lib().lsmblk_shard_rotation_carry(_ctx(dev, stream), carry_in.data_ptr(), carry_out.data_ptr(),
+    check(lib().lsmblk_shard_rotation_carry(ctx.h if ctx is not None else _ctx(dev, stream), carry_in.data_ptr(), carry_out.data_ptr(),
                                             _stream_ptr(stream, dev)), "lsmblk_shard_rotation_carry")
 
 
 def shard_encode_into(ext: KVStream, out, out_cap, blk_off, blk_cap, seg_start, seg_blk, seg_cap, stats,
-                      stream=None):
+                      stream=None, ctx=None):
     dev = _dev_index(ext.key_off)
     ext.check(dev, "ext")
     _need(out, torch.uint8, "out", dev, out_cap)
@@ -603,7 +618,7 @@ def shard_encode_into(ext: KVStream, out, out_cap, blk_off, blk_cap, seg_start, 
     _need(seg_blk, torch.int32, "seg_blk", dev, seg_cap)
     _need(stats, torch.int64, "stats", dev, 8)
     c = ext._c()
-    check(lib().lsmblk_shard_encode_batch(_ctx(dev, stream), ctypes.byref(c), out.data_ptr(), out_cap,
+    check(lib().lsmblk_shard_encode_batch(ctx.h if ctx is not None else _ctx(dev, stream), ctypes.byref(c), out.data_ptr(), out_cap,
                                           blk_off.data_ptr(), blk_cap, seg_start.data_ptr(), seg_blk.data_ptr(),
                                           seg_cap, stats.data_ptr(), _stream_ptr(stream, dev)),
           "lsmblk_shard_encode_batch")

@@ -59,7 +59,7 @@ struct alignas(16) DecLds {
   uint8_t img[kDecImg];
   uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE], vsrc[kDecMaxE];
   uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
-  uint8_t out[kDecOut];  // decoded key run, then (16-B aligned) value run
+  alignas(16) uint8_t out[kDecOut];  // decoded key run, then (16-B aligned) value run
 };
 
 // 16 bytes at LDS byte offset x (any alignment) via three 8-B reads: ds_read_b64 at a 16-B

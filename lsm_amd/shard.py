@@ -188,14 +188,14 @@ class RangeShard:
     compaction options (batch.compact_opts) and the range [lo, hi) (None: unbounded).  Phases:
     merge() -> head() -> set_halo() -> prepare() -> carry() -> encode() -> result(); buffers are kept
     for the next call with the same sizes (the bench's timed loop allocates nothing).  Every shard
-    works on its own stream (default: a new one), so its context -- which holds the rotation state
-    between prepare, carry and encode -- is its own; the exchange drivers run under
-    torch.cuda.stream(shard.stream)."""
+    owns its library context (which holds the rotation state between prepare, carry and encode),
+    so several shards can share one stream; `stream` defaults to the device's current stream."""
 
     def __init__(self, kv: batch.KVStream, run_start, opts: dict, lo: bytes = None, hi: bytes = None, stream=None):
         self.dev = torch.device("cuda", batch._dev_index(kv.key_off))
         self.kv, self.opts = kv, opts
-        self.stream = stream if stream is not None else torch.cuda.Stream(self.dev)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        self.ctx = batch.OwnCtx(self.dev.index)
         self.rs = batch._u32_table(run_start, self.dev)
         self.nrun = self.rs.numel() - 1
         self.bs, self.target = opts["block_size"], opts["target_sst_size"]
@@ -235,7 +235,8 @@ class RangeShard:
     def _merge(self):
         k = self.kept
         k.n = 0
-        batch.compact_merge_into(self.kv, self.rs, self.nrun, self.opts, self.range_c, k, self.mstats, self.stream)
+        batch.compact_merge_into(self.kv, self.rs, self.nrun, self.opts, self.range_c, k, self.mstats, self.stream,
+                                 ctx=self.ctx)
         torch.cuda.synchronize(self.dev)
         s = self.mstats.cpu().tolist()
         st = lib().lsmblk_stats_status(s[3] & 0xFFFFFFFFFFFFFFFF)
@@ -287,12 +288,12 @@ class RangeShard:
     def prepare(self):
         n = self.m + self.h
         self.sst_cap = (self.Kk + self.Vk + self.Kh + self.Vh + 22 * n) // self.target + 3
-        batch.shard_prepare(self.ext, self.m, self.last, self.bs, self.target, self.sst_cap, self.stream)
+        batch.shard_prepare(self.ext, self.m, self.last, self.bs, self.target, self.sst_cap, self.stream, ctx=self.ctx)
 
     # -- phase 4: carry
     def carry(self, carry_in: torch.Tensor) -> torch.Tensor:
         self.carry_in = carry_in
-        batch.shard_carry(carry_in, self.cout, self.stream)
+        batch.shard_carry(carry_in, self.cout, self.stream, ctx=self.ctx)
         return self.cout
 
     # -- phase 5: SST cut points + blocks
@@ -311,7 +312,7 @@ class RangeShard:
             self.seg = torch.zeros(seg_cap, dtype=torch.int32, device=self.dev)
             self.seg_blk = torch.zeros(seg_cap, dtype=torch.int32, device=self.dev)
         batch.shard_encode_into(self.ext, self.out, out_cap, self.blk_off, blk_cap, self.seg, self.seg_blk, seg_cap,
-                                self.estats, self.stream)
+                                self.estats, self.stream, ctx=self.ctx)
 
     def result(self):
         """Host view of the range's output (synchronizes): blocks, blk_off, seg_start (ext entry
@@ -357,7 +358,7 @@ def compact_local(shards):
         s.prepare()
     c = torch.zeros(2, dtype=torch.int64, device=shards[0].dev) if shards else None
     for s in shards:
-        torch.cuda.synchronize(s.dev)   # the carry-in was made on the previous shard's stream
+        torch.cuda.synchronize(s.dev)   # the carry-in may come from another shard's stream
         with torch.cuda.stream(s.stream):
             c = s.carry(c).clone()
     for s in shards:
