@@ -305,8 +305,8 @@ __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, 
 }
 
 // ---------------------------------------------------------------- large blocks
-// Blocks over the LDS image (config M: 64 KiB blocks, values up to 4 KiB) with <= kDecMaxE
-// entries keep their entry tables in LDS and move bytes HBM -> HBM: every entry lane copies
+// Blocks over the LDS image (config M: 64 KiB blocks, values up to 4 KiB) keep their entry
+// tables in LDS, kDecMaxE entries at a time, and move bytes HBM -> HBM: every entry lane copies
 // its key and value as 16-B unaligned buffer loads/stores (last piece overlapping), with
 // kBigB pieces' loads issued before their stores (one memory round trip per kBigB pieces).
 constexpr uint32_t kBigB = 8;
@@ -425,19 +425,21 @@ __device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecLds&
   }
 }
 
+// Outputs of the n entries whose tables are in L (block entries Eb - E0 .. + n), large block.
 __device__ void dec_big_outputs(const DecodeArgs& a, const DecLds& L, const rsrc_t& R, uint32_t lead,
-                                const BlockHdr& h, uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V) {
+                                const BlockHdr& h, uint32_t n, uint64_t Eb, uint64_t K0, uint64_t V0, uint32_t K,
+                                uint32_t V) {
   const uint32_t l = lane_id();
   const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
   const rsrc_t RK = make_rsrc_exact(a.keys + (K0 - kb), kb + K), RV = make_rsrc_exact(a.vals + (V0 - vb), vb + V);
   const GlbImg im{R, lead};
   const uint32_t lim = lead + h.len;  // descriptor byte of the block end
-  for (uint32_t c = 0; c < h.n; c += 64) {  // uniform trip count: the wave copies long values
+  for (uint32_t c = 0; c < n; c += 64) {  // uniform trip count: the wave copies long values
     const uint32_t k = c + l;
-    const bool live = k < h.n;
+    const bool live = k < n;
     uint32_t vsrc = 0, vdst = 0, vl = 0;
     if (live) {
-      dec_big_entry(a, L, im, k, lim, RK, kb, E0, K0, V0);
+      dec_big_entry(a, L, im, k, lim, RK, kb, Eb, K0, V0);
       vsrc = lead + L.epos[k] + 14 + L.sfx[k];
       vdst = vb + L.vout[k];
       vl = L.vout[k + 1] - L.vout[k];
@@ -489,40 +491,44 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   if (a.skip & 256) return;  // ablation: staging only
   if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
   const bool fast = fits && h.n <= kDecMaxE;
-  const bool big = !fits && h.n <= kDecMaxE;  // large block: tables in LDS, bytes from HBM
+  // large block: entry tables in LDS, bytes HBM -> HBM; more than kDecMaxE entries are taken
+  // kDecMaxE at a time (the tables of each chunk are built just before its outputs)
+  const bool big = !fits;
 
   // phase 1: parse entries, block aggregates (entries, key bytes, value bytes)
   uint64_t K = 0, V = 0;
   bool bad = false;
-  auto parse_tables = [&](const auto& im) {
-    for (uint32_t c = 0; c < h.n; c += 64) {
+  // tables of entries [c0, c0 + cn) (cn <= kDecMaxE) at table rows 0 .. cn, output offsets
+  // from the block's key / value bytes before c0 (kr, vr)
+  auto parse_tables = [&](const auto& im, uint32_t c0, uint32_t cn, uint64_t& kr, uint64_t& vr) {
+    for (uint32_t c = 0; c < cn; c += 64) {
       const uint32_t k = c + l;
       uint32_t off = 0, p = 0, s = 0, vl = 0;
       bool ok = true;
-      if (k < h.n) ok = parse_entry(im, h, k, off, p, s, vl);
+      if (k < cn) ok = parse_entry(im, h, c0 + k, off, p, s, vl);
       bad = bad || !ok;
       const uint32_t kl = p + s;
       const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
-      if (k < h.n) {
+      if (k < cn) {
         L.epos[k] = uint16_t(off);
         L.pfx[k] = uint16_t(p);
         L.sfx[k] = uint16_t(s);
         L.vsrc[k] = uint16_t(off + 14 + s);
-        L.kout[k] = uint32_t(K) + ki - kl;
-        L.vout[k] = uint32_t(V) + vi - vl;
+        L.kout[k] = uint32_t(kr) + ki - kl;
+        L.vout[k] = uint32_t(vr) + vi - vl;
       }
-      K += __shfl(ki, 63, 64);
-      V += __shfl(vi, 63, 64);
+      kr += __shfl(ki, 63, 64);
+      vr += __shfl(vi, 63, 64);
     }
     if (l == 0) {
-      L.kout[h.n] = uint32_t(K);
-      L.vout[h.n] = uint32_t(V);
+      L.kout[cn] = uint32_t(kr);
+      L.vout[cn] = uint32_t(vr);
     }
   };
   if (fast) {
-    parse_tables(LdsImg{L.img, lead});
-  } else if (big) {
-    parse_tables(GlbImg{R, lead});
+    parse_tables(LdsImg{L.img, lead}, 0, h.n, K, V);
+  } else if (big && h.n <= kDecMaxE) {
+    parse_tables(GlbImg{R, lead}, 0, h.n, K, V);
   } else {
     for (uint32_t c = 0; c < h.n; c += 64) {
       const uint32_t k = c + l;
@@ -557,8 +563,17 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
     if (fast) {
       dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
+    } else if (big && h.n <= kDecMaxE) {
+      dec_big_outputs(a, L, R, lead, h, h.n, E0, K0, V0, uint32_t(K), uint32_t(V));
     } else if (big) {
-      dec_big_outputs(a, L, R, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V));
+      uint64_t kr = 0, vr = 0;
+      for (uint32_t c0 = 0; c0 < h.n; c0 += kDecMaxE) {
+        const uint32_t cn = min(kDecMaxE, h.n - c0);
+        wave_sync();  // the previous chunk's table reads are done
+        parse_tables(GlbImg{R, lead}, c0, cn, kr, vr);
+        wave_sync();
+        dec_big_outputs(a, L, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V));
+      }
     } else if (fits) {
       dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
     } else {
