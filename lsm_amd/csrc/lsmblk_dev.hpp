@@ -285,44 +285,87 @@ __device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4]
 // ---------------------------------------------------------------- CRC-32 (crc32fast) tables
 namespace {
 constexpr uint32_t kCrcChunk = 4096;
-constexpr uint32_t kCrcMats = 7;  // Z(., 64 << j), j = 0..5, and j = 6: a whole chunk
-constexpr uint32_t kCrcStage = 5 * 1024;  // five 1-KiB load pieces (lead + chunk <= 4111 B)
+// A chunk is cut into lane segments of kCrcSeg = 68 B (17 dwords, odd): lane l's dword i is
+// then LDS bank (17 l + i) mod 32, so the 32 lanes of a ds_read_b32 group hit 32 distinct
+// banks.  64-B segments put every lane of a group on 2 banks (a 16-way conflict per read).
+constexpr uint32_t kCrcSeg = 68;
+constexpr uint32_t kCrcMats = 7;  // Z(., kCrcSeg << j), j = 0..5, and j = 6: Z(., kCrcChunk)
+#ifndef LSMBLK_CRC_ABL
+#define LSMBLK_CRC_ABL 0  // timing experiments only (tools/crc_time.py)
+#endif
+// crc_chunk reads up to kCrcPad bytes before a chunk, which must hold zeros
+constexpr uint32_t kCrcPad = 80;
+constexpr uint32_t kCrcStage = kCrcPad + 5 * 1024 + 16;  // zero pad, five 1-KiB load pieces (+3 shift)
 struct alignas(16) CrcTabs {
   uint32_t fold[8][16];              // R_0 after xoring a dword into the register: by nibble
-  uint32_t shift[kCrcMats][8][16];   // Z(., 64 << j) by nibble of the register
-  uint32_t nib[16];                  // one 4-bit step (leading odd bytes of a segment)
+  uint32_t shift[kCrcMats][8][16];   // Z(., kCrcSeg << j), j < 6, Z(., kCrcChunk): by nibble
+  uint32_t zinv[kCrcSeg];            // zinv[j]: the register that j zero bytes take to the init
 };
 
+// 4 * (byte B of v & 15 << 2 ...): (byte B of v) & 0x3C as one SDWA instruction
+template <int B>
+__device__ __forceinline__ uint32_t sdwa_and(uint32_t v, uint32_t m) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "=v"(r) : "v"(v), "v"(m));
+  else if constexpr (B == 1)
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(r) : "v"(v), "v"(m));
+  else if constexpr (B == 2)
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(r) : "v"(v), "v"(m));
+  else
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(r) : "v"(v), "v"(m));
+  return r;
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// m applied to x: the XOR of m[k][nibble k of x].  The LDS byte offsets 4 * nibble come from
+// y = x << 2 (even nibbles: byte k/2 of y, bits 2..5) and z = x >> 2 (odd nibbles: byte
+// (k-1)/2 of z), one SDWA AND with 0x3C each, so a map costs 2 + 8 + 4 VALU (xor3 tree).
 __device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[8][16], uint32_t x) {
-  return (m[0][x & 15] ^ m[1][(x >> 4) & 15]) ^ (m[2][(x >> 8) & 15] ^ m[3][(x >> 12) & 15]) ^
-         (m[4][(x >> 16) & 15] ^ m[5][(x >> 20) & 15]) ^ (m[6][(x >> 24) & 15] ^ m[7][x >> 28]);
+  const uint32_t y = x << 2, z = x >> 2, k3c = 0x3C;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(&m[0][0]);
+  auto at = [&](uint32_t k, uint32_t off) { return *reinterpret_cast<const uint32_t*>(b + 64 * k + off); };
+  const uint32_t a0 = at(0, sdwa_and<0>(y, k3c)), a1 = at(1, sdwa_and<0>(z, k3c));
+  const uint32_t a2 = at(2, sdwa_and<1>(y, k3c)), a3 = at(3, sdwa_and<1>(z, k3c));
+  const uint32_t a4 = at(4, sdwa_and<2>(y, k3c)), a5 = at(5, sdwa_and<2>(z, k3c));
+  const uint32_t a6 = at(6, sdwa_and<3>(y, k3c)), a7 = at(7, sdwa_and<3>(z, k3c));
+  return xor3(xor3(xor3(a0, a1, a2), a3, a4), a5, a6) ^ a7;
 }
 
-// R over the chunk bytes p[0, sz) (LDS), 0 < sz <= kCrcChunk; the block's first chunk
+// R over the chunk bytes p[0, sz) (LDS), 0 < sz <= 64 * kCrcSeg; the block's first chunk
 // starts from the CRC init.  Every lane returns the chunk's register.
+//
+// Lane l >= l0 = 64 - ceil(sz / 68) folds the 68-B window that ends 68 (63 - l) bytes before
+// the chunk end: 17 dword steps, fully unrolled, every load issued first.  Lane l0's window
+// starts up to 67 bytes before p: the caller keeps p[-kCrcPad, 0) zero, and zero bytes leave a
+// zero register unchanged, so the window's CRC is the chunk head's.  On a block's first chunk
+// lane l0 starts from zinv[68 - r] instead, the register that the 68 - r leading zeros carry
+// to the init 0xFFFFFFFF.  Windows are 4-aligned in LDS when p + sz is.
 __device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p, uint32_t sz, bool first) {
   const uint32_t l = lane_id();
-  const uint32_t nseg = (sz + 63) >> 6, l0 = 64 - nseg, r = sz - 64 * (nseg - 1);
-  uint32_t crc = 0;
-  if (l >= l0) {
-    const uint32_t so = l == l0 ? 0u : r + 64 * (l - l0 - 1), sn = l == l0 ? r : 64u;
-    crc = first && l == l0 ? 0xFFFFFFFFu : 0u;
-    const uint8_t* q = p + so;
-    const uint32_t nb = sn & 3;
-    for (uint32_t i = 0; i < nb; ++i) {
-      crc ^= q[i];
-      crc = T.nib[crc & 15] ^ (crc >> 4);
-      crc = T.nib[crc & 15] ^ (crc >> 4);
-    }
-#pragma unroll 4
-    for (uint32_t i = nb; i < sn; i += 4) crc = crc_apply(T.fold, crc ^ *reinterpret_cast<const uint32_t*>(q + i));
-    const uint32_t m = 63 - l;  // full segments after this one
+  const uint32_t nseg = (sz + kCrcSeg - 1) / kCrcSeg, l0 = 64 - nseg, r = sz - kCrcSeg * (nseg - 1);
+  const bool live = l >= l0;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(live ? p + sz - kCrcSeg * (64 - l) : p - kCrcSeg);
+  uint32_t d[kCrcSeg / 4];
 #pragma unroll
-    for (uint32_t j = 0; j < 6; ++j)
-      if ((m >> j) & 1) crc = crc_apply(T.shift[j], crc);
-  }
+  for (uint32_t i = 0; i < kCrcSeg / 4; ++i) d[i] = q[i];
+  uint32_t crc = first && l == l0 ? T.zinv[kCrcSeg - r] : 0u;
+#if LSMBLK_CRC_ABL == 3  // timing experiment: data reads, no table lookups
 #pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) crc ^= __shfl_xor(crc, d, 64);
+  for (uint32_t i = 0; i < kCrcSeg / 4; ++i) crc = __builtin_amdgcn_alignbit(crc, crc, 1) ^ d[i];
+#else
+#pragma unroll
+  for (uint32_t i = 0; i < kCrcSeg / 4; ++i) crc = crc_apply(T.fold, crc ^ d[i]);
+#endif
+  const uint32_t m = 63 - l;  // full windows after this one
+#if LSMBLK_CRC_ABL != 2 && LSMBLK_CRC_ABL != 3
+#pragma unroll
+  for (uint32_t j = 0; j < 6; ++j)
+    if ((m >> j) & 1) crc = crc_apply(T.shift[j], crc);
+#endif
+  crc = live ? crc : 0u;
+#pragma unroll
+  for (uint32_t dd = 32; dd >= 1; dd >>= 1) crc ^= __shfl_xor(crc, dd, 64);
   return crc;
 }
 
@@ -343,11 +386,13 @@ inline void crc_nibble_tables(const uint32_t (&col)[32], uint32_t (&m)[8][16]) {
       m[k][v] = y;
     }
 }
+// inverse of one bit step: the top bit of c' says whether the polynomial was folded in
+inline uint32_t crc_bit_unstep(uint32_t c) { return (c & 0x80000000u) ? ((c ^ 0xEDB88320u) << 1) | 1u : c << 1; }
 inline void crc_host_tables(CrcTabs& T) {
-  for (uint32_t v = 0; v < 16; ++v) {
-    uint32_t c = v;
-    for (int s = 0; s < 4; ++s) c = crc_bit_step(c);
-    T.nib[v] = c;
+  uint32_t z = 0xFFFFFFFFu;
+  for (uint32_t j = 0; j < kCrcSeg; ++j) {
+    T.zinv[j] = z;
+    for (int s = 0; s < 8; ++s) z = crc_bit_unstep(z);
   }
   uint32_t col[32];
   for (uint32_t bit = 0; bit < 32; ++bit) {  // fold: 32 bit steps (4 zero bytes after the xor)
@@ -356,8 +401,8 @@ inline void crc_host_tables(CrcTabs& T) {
     col[bit] = x;
   }
   crc_nibble_tables(col, T.fold);
-  for (uint32_t j = 0; j < kCrcMats; ++j) {  // Z(., 64 << j): 8 (64 << j) bit steps
-    const uint32_t steps = 8u * (64u << j);
+  for (uint32_t j = 0; j < kCrcMats; ++j) {  // Z(., n) = 8 n bit steps
+    const uint32_t steps = 8u * (j < 6 ? kCrcSeg << j : kCrcChunk);
     for (uint32_t bit = 0; bit < 32; ++bit) {
       uint32_t x = 1u << bit;
       for (uint32_t s = 0; s < steps; ++s) x = crc_bit_step(x);
@@ -385,7 +430,7 @@ struct lsmblk_ctx {
   uint32_t* rec_first = nullptr; // n+1
   uint32_t* blk_first = nullptr;
   uint32_t* ent = nullptr;       // 3 per entry: rec, alcp, block sizes (plan passes)
-  uint32_t* big_list = nullptr;  // n+1: blocks for emit_big_kernel
+  uint32_t* big_list = nullptr;  // n+1 u32: emit_big_kernel's per-block flags (bytes)
   uint64_t rec_cap = 0;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)

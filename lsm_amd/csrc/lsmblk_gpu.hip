@@ -1036,8 +1036,9 @@ struct EmitArgs {
   uint64_t out_cap, blk_cap;
   uint64_t n;  // entries; arena sizes are key_off[n], val_off[n]
   uint64_t* stats;
-  uint32_t* big_list;  // blocks beyond the LDS image, appended by emit_kernel for emit_big_kernel
-  uint32_t* big_cnt;
+  // per block: 1 = beyond the LDS image, left by emit_kernel for emit_big_kernel (a flag per
+  // block, not a list: appending through one shared counter cost 0.6 ms on 64 Ki big blocks)
+  uint8_t* big_flag;
   uint32_t skip;  // ablation mask (timing experiments only): 16 entry-lane byte writes,
                   // 32 bulk value copy, 64 flush, 128 LCP
   const uint64_t* dn;  // optional: n read from device memory (overrides n)
@@ -1242,7 +1243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint32_t olead = uint32_t(O & 15);
     bool nxt_fast = false;
     if (!cur_fast) {  // handed to emit_big_kernel (its registers stay out of this loop)
-      if (l == 0) a.big_list[atomicAdd(a.big_cnt, 1u)] = uint32_t(cur.bi);
+      if (l == 0) a.big_flag[cur.bi] = 1;
       if (!has_next) break;
       meta2(nxt);
       nxt_fast = is_fast(nxt);
@@ -1442,17 +1443,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   raise_err(a.stats, err);
 }
 
-// The blocks emit_kernel listed as beyond its LDS image, one wave per block.
+// The blocks emit_kernel flagged as beyond its LDS image, one wave per block: wave j checks
+// blocks j, j + nw, j + 2 nw, ... 64 at a time (a flag per lane, then a ballot).
 __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   const EmitArgs a = resolve(a0);
-  const uint32_t cnt = uni(*a.big_cnt);
-  const uint32_t nw = gridDim.x * 4;
+  const uint64_t nblk = uni64(a.stats[0]);
+  const uint64_t lim = nblk < a.blk_cap ? nblk : (a.blk_cap ? a.blk_cap - 1 : 0);
+  const uint64_t nw = uint64_t(gridDim.x) * 4;
+  const uint32_t l = lane_id();
   uint32_t err = 0;
-  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < cnt; i += nw) {
-    const uint64_t bi = uni(a.big_list[i]);
-    const uint32_t s = uni(a.blk_first[bi]), e = uni(a.blk_first[bi + 1]);
-    const uint64_t O = uni64(a.blk_off[bi]), size = uni64(a.blk_off[bi + 1]) - O;
-    emit_big(a, s, e - s, O, size, err);
+  for (uint64_t base = blockIdx.x * 4 + (threadIdx.x >> 6); base < lim; base += nw * 64) {
+    const uint64_t mine = base + nw * l;
+    uint64_t big = __ballot(mine < lim && a.big_flag[mine]);
+    while (big) {
+      const uint32_t i = uint32_t(__builtin_ctzll(big));
+      big &= big - 1;
+      const uint64_t bi = base + nw * i;
+      const uint32_t s = uni(a.blk_first[bi]), e = uni(a.blk_first[bi + 1]);
+      const uint64_t O = uni64(a.blk_off[bi]), size = uni64(a.blk_off[bi + 1]) - O;
+      emit_big(a, s, e - s, O, size, err);
+    }
   }
   raise_err(a.stats, err);
 }
@@ -1488,14 +1498,16 @@ __global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64
 // (src/table/builder.rs:120-122) and SsTable::read_block verifies (src/table.rs:226-230).
 // CRC-32/ISO-HDLC: reflected polynomial 0xEDB88320, init and xorout 0xFFFFFFFF.
 //
-// CRC is a serial recurrence per block, so a wave splits each 4-KiB chunk into 64 segments
-// of 64 B, one per lane, and recombines them by linearity.  With R_x(M) the CRC register
-// after feeding M from state x and Z(x, n) = R_x(n zero bytes) (linear in x):
+// CRC is a serial recurrence per block, so a wave splits each 4-KiB chunk into (at most 61)
+// segments of kCrcSeg = 68 B, one per lane, and recombines them by linearity.  With R_x(M)
+// the CRC register after feeding M from state x and Z(x, n) = R_x(n zero bytes) (linear in x):
 //   R_x(A || B) = Z(R_x(A), |B|) ^ R_0(B).
-// The chunk is right-aligned on the lanes -- its one short segment (sz mod 64) is the
+// The chunk is right-aligned on the lanes -- its one short segment (sz mod 68) is the
 // first -- so the segment of lane l is followed by exactly 63 - l full segments and
-// contributes Z(R(seg_l), 64 (63 - l)): the binary digits of 63 - l select up to six of the
-// precomputed maps Z(., 64 << j).  The block's init 0xFFFFFFFF rides in its first segment;
+// contributes Z(R(seg_l), 68 (63 - l)): the binary digits of 63 - l select up to six of the
+// precomputed maps Z(., 68 << j).  (68 = 17 dwords keeps the 32 lanes of an LDS read group on
+// 32 distinct banks; 64-B segments measured 2.5 ms per 4.2 GB, 16-way conflicted.)  The
+// block's init 0xFFFFFFFF rides in its first segment;
 // chunk after chunk, acc = Z(acc, 4096) ^ R_0(chunk).
 //
 // Every linear map (the 4-byte fold step and each Z) is applied as eight 16-entry NIBBLE
@@ -1519,12 +1531,14 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   const uint32_t t = threadIdx.x, w = t >> 6, l = lane_id();
   for (uint32_t i = t; i < sizeof(CrcTabs) / 16; i += 256)
     reinterpret_cast<u32x4*>(&T)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
+  if (t < 4 * kCrcPad / 16)  // the zero pad before each wave's chunk image (crc_chunk reads it)
+    *reinterpret_cast<u32x4*>(stage[t / (kCrcPad / 16)] + 16 * (t % (kCrcPad / 16))) = u32x4{0, 0, 0, 0};
   if (blockIdx.x == 0 && t == 0) {
     a.stats[0] = a.nblk;
     a.stats[1] = a.blk_off[a.nblk] - a.blk_off[0];
   }
   __syncthreads();
-  uint8_t* S = stage[w];
+  uint8_t* S = stage[w] + kCrcPad;
   const uint64_t stride = uint64_t(gridDim.x) * 4;
   uint64_t b = uint64_t(blockIdx.x) * 4 + w;
   if (b >= a.nblk) return;
@@ -1543,7 +1557,9 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   uint32_t qlead = 0;
   auto issue = [&](uint64_t cs, uint32_t sz) {  // loads of block bytes [cs, cs + sz)
     const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(a.blocks + cs) & 15));
-    const rsrc_t R = make_rsrc(a.blocks + cs - lead, lead + sz);
+    // (uniform base and size, so the descriptor lives in SGPRs: no waterfall loop per load)
+    const rsrc_t R = make_rsrc(reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uintptr_t>(a.blocks + cs - lead))),
+                               uni(lead + sz));
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i) q[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
     qlead = lead;
@@ -1566,13 +1582,29 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
     uint32_t acc = 0;
     for (uint32_t c = 0; c == 0 || c < nch; ++c) {  // an empty block still lands its (zero) loads
       const uint32_t sz = c == 0 ? h : kCrcChunk, lead = qlead;
+      // land the chunk at S + sh, sh making its end 4-aligned (aligned window reads in
+      // crc_chunk), with the lead bytes before it zeroed (they are in lane l0's window)
+      const uint32_t sh = LSMBLK_CRC_ABL == 4 ? 0u : (0u - (lead + sz)) & 3u;
+      if (l == 0) {
+        *reinterpret_cast<uint32_t*>(S) = 0;  // [S, S + sh): older chunks' bytes
+        uint32_t* v = reinterpret_cast<uint32_t*>(&q[0]);
 #pragma unroll
-      for (uint32_t i = 0; i < 5; ++i) *reinterpret_cast<u32x4*>(S + 16 * (l + 64 * i)) = q[i];
+        for (uint32_t d = 0; d < 4; ++d) {
+          const int32_t z = int32_t(lead) - int32_t(4 * d);  // lead bytes in this dword
+          v[d] &= z <= 0 ? ~0u : z >= 4 ? 0u : ~0u << (8 * z);
+        }
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i) *reinterpret_cast<u32x4*>(S + sh + 16 * (l + 64 * i)) = q[i];
       wave_sync();
-      if (c + 1 < nch) issue(st + h + uint64_t(kCrcChunk) * c, kCrcChunk);
-      else if (has_next) issue(stn, nchn ? lenn - kCrcChunk * (nchn - 1) : 0u);
-      if (nch) {
-        const uint32_t part = crc_chunk(T, S + lead, sz, c == 0);
+      {  // one issue site with uniform operands (two sites get merged into a divergent phi)
+        const bool more = c + 1 < nch;
+        const uint64_t ncs = more ? st + h + uint64_t(kCrcChunk) * c : stn;
+        const uint32_t nsz = more ? kCrcChunk : nchn ? lenn - kCrcChunk * (nchn - 1) : 0u;
+        if (more || has_next) issue(uni64(ncs), uni(nsz));
+      }
+      if (nch && LSMBLK_CRC_ABL != 1) {
+        const uint32_t part = crc_chunk(T, S + sh + lead, sz, c == 0);
         acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
       }
       wave_sync();  // the next landing overwrites S
@@ -2374,19 +2406,20 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   e.blk_cap = blk_cap;
   e.n = in->n;
   e.stats = stats;
-  e.big_list = c->big_list;
-  e.big_cnt = c->counters + 2;
+  e.big_flag = reinterpret_cast<uint8_t*>(c->big_list);
   e.skip = c->skip;
   e.dn = dn;
-  if (hipMemsetAsync(e.big_cnt, 0, sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
+  // blocks <= entries (every block holds one), and <= blk_cap
+  const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;
+  if (nblk_max && hipMemsetAsync(e.big_flag, 0, nblk_max, st) != hipSuccess) return LSMBLK_E_HIP;
   hipLaunchKernelGGL(emit_kernel, dim3(grid), dim3(256), 0, st, e);
-  hipLaunchKernelGGL(emit_big_kernel, dim3(uint32_t(cus) * 4), dim3(256), 0, st, e);
+  hipLaunchKernelGGL(emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), 0, st, e);
   if (c->timing) (void)hipEventRecord(c->ev[6], st);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }

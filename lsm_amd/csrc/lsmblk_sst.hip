@@ -294,13 +294,16 @@ __global__ __launch_bounds__(256) void sst_meta_kernel(SstArgs a) {
 
 constexpr uint32_t kBloomLds = 32768;  // filters up to 32 KiB (~26 K keys) are built in LDS
 
-// crc32fast of LDS bytes p[0, len): chunks of 4 KiB (the first holds the remainder), combined
-// with Z(., 4096) as in crc_kernel.  Every lane of the wave returns the CRC.
+// crc32fast of LDS bytes p[0, len), p[-kCrcPad, 0) zero: chunks of 64 whole 68-B windows
+// (the first holds the remainder), so only the first chunk's windows reach before its start;
+// combined with Z(., 4352) = Z(., 68 << 5) twice.  Every lane of the wave returns the CRC.
 __device__ uint32_t crc_lds(const CrcTabs& T, const uint8_t* p, uint32_t len) {
+  constexpr uint32_t kW = 64 * kCrcSeg;
   if (len == 0) return 0;
-  const uint32_t nch = (len + kCrcChunk - 1) / kCrcChunk, h = len - kCrcChunk * (nch - 1);
+  const uint32_t nch = (len + kW - 1) / kW, h = len - kW * (nch - 1);
   uint32_t acc = crc_chunk(T, p, h, true);
-  for (uint32_t c = 1; c < nch; ++c) acc = crc_apply(T.shift[6], acc) ^ crc_chunk(T, p + h + kCrcChunk * (c - 1), kCrcChunk, false);
+  for (uint32_t c = 1; c < nch; ++c)
+    acc = crc_apply(T.shift[5], crc_apply(T.shift[5], acc)) ^ crc_chunk(T, p + h + kW * (c - 1), kW, false);
   return ~acc;
 }
 
@@ -308,7 +311,8 @@ __device__ uint32_t crc_lds(const CrcTabs& T, const uint8_t* p, uint32_t len) {
 // bloom.rs:80-101), encoded as filter | k | crc (:63-69), then bloom_offset (builder.rs:83-85).
 __global__ __launch_bounds__(256) void sst_bloom_kernel(SstArgs a) {
   __shared__ CrcTabs T;
-  __shared__ __attribute__((aligned(16))) uint32_t bits[kBloomLds / 4 + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t bitbuf[kCrcPad / 4 + kBloomLds / 4 + 4];
+  uint32_t* const bits = bitbuf + kCrcPad / 4;  // after the zeros crc_chunk reads before a chunk
   if (a.stats[3]) return;
   const uint32_t s = blockIdx.x;
   if (s >= a.nsst) return;
@@ -320,6 +324,7 @@ __global__ __launch_bounds__(256) void sst_bloom_kernel(SstArgs a) {
   for (uint32_t i = threadIdx.x; i < sizeof(CrcTabs) / 16; i += 256)
     reinterpret_cast<u32x4*>(&T)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
   const uint32_t nw = (G.nbytes + 1 + 3) / 4;
+  if (threadIdx.x < kCrcPad / 4) bitbuf[threadIdx.x] = 0;
   if (lds) {
     for (uint32_t i = threadIdx.x; i < nw; i += 256) bits[i] = 0;
   } else {
