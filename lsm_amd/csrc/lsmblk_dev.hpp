@@ -290,9 +290,6 @@ constexpr uint32_t kCrcChunk = 4096;
 // banks.  64-B segments put every lane of a group on 2 banks (a 16-way conflict per read).
 constexpr uint32_t kCrcSeg = 68;
 constexpr uint32_t kCrcMats = 7;  // Z(., kCrcSeg << j), j = 0..5, and j = 6: Z(., kCrcChunk)
-#ifndef LSMBLK_CRC_ABL
-#define LSMBLK_CRC_ABL 0  // timing experiments only (tools/crc_time.py)
-#endif
 // crc_chunk reads up to kCrcPad bytes before a chunk, which must hold zeros
 constexpr uint32_t kCrcPad = 80;
 constexpr uint32_t kCrcStage = kCrcPad + 5 * 1024 + 16;  // zero pad, five 1-KiB load pieces (+3 shift)
@@ -300,6 +297,7 @@ struct alignas(16) CrcTabs {
   uint32_t fold[8][16];              // R_0 after xoring a dword into the register: by nibble
   uint32_t shift[kCrcMats][8][16];   // Z(., kCrcSeg << j), j < 6, Z(., kCrcChunk): by nibble
   uint32_t zinv[kCrcSeg];            // zinv[j]: the register that j zero bytes take to the init
+  uint32_t unz[3][8][16];            // Z(., t)^-1, t = 1..3: undoes t appended zero bytes
 };
 
 // 4 * (byte B of v & 15 << 2 ...): (byte B of v) & 0x3C as one SDWA instruction
@@ -332,40 +330,37 @@ __device__ __forceinline__ uint32_t crc_apply(const uint32_t (&m)[8][16], uint32
   return xor3(xor3(xor3(a0, a1, a2), a3, a4), a5, a6) ^ a7;
 }
 
-// R over the chunk bytes p[0, sz) (LDS), 0 < sz <= 64 * kCrcSeg; the block's first chunk
+// R over the chunk bytes p[0, sz) (LDS), 0 < sz + t <= 64 * kCrcSeg; the block's first chunk
 // starts from the CRC init.  Every lane returns the chunk's register.
 //
-// Lane l >= l0 = 64 - ceil(sz / 68) folds the 68-B window that ends 68 (63 - l) bytes before
-// the chunk end: 17 dword steps, fully unrolled, every load issued first.  Lane l0's window
-// starts up to 67 bytes before p: the caller keeps p[-kCrcPad, 0) zero, and zero bytes leave a
-// zero register unchanged, so the window's CRC is the chunk head's.  On a block's first chunk
-// lane l0 starts from zinv[68 - r] instead, the register that the 68 - r leading zeros carry
-// to the init 0xFFFFFFFF.  Windows are 4-aligned in LDS when p + sz is.
-__device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p, uint32_t sz, bool first) {
-  const uint32_t l = lane_id();
-  const uint32_t nseg = (sz + kCrcSeg - 1) / kCrcSeg, l0 = 64 - nseg, r = sz - kCrcSeg * (nseg - 1);
+// The chunk is read as M || 0^t, t < 4 zero bytes the caller placed after it (so that p + sz + t
+// is 4-aligned and every window read is an aligned dword); the register of M || 0^t is
+// Z(R(M), t), undone by the map unz[t - 1] at the end.  Lane l >= l0 = 64 - ceil((sz + t) / 68)
+// folds the 68-B window that ends 68 (63 - l) bytes before the end: 17 dword steps, fully
+// unrolled, every load issued first.  Lane l0's window starts up to 67 bytes before p: the
+// caller keeps p[-kCrcPad, 0) zero, and zero bytes leave a zero register unchanged, so the
+// window's CRC is the chunk head's.  On a block's first chunk lane l0 starts from zinv[68 - r]
+// instead, the register that the 68 - r leading zeros carry to the init 0xFFFFFFFF.
+__device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p, uint32_t sz, bool first,
+                                              uint32_t t = 0) {
+  const uint32_t l = lane_id(), sx = sz + t;
+  const uint32_t nseg = (sx + kCrcSeg - 1) / kCrcSeg, l0 = 64 - nseg, r = sx - kCrcSeg * (nseg - 1);
   const bool live = l >= l0;
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(live ? p + sz - kCrcSeg * (64 - l) : p - kCrcSeg);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(live ? p + sx - kCrcSeg * (64 - l) : p - kCrcSeg);
   uint32_t d[kCrcSeg / 4];
 #pragma unroll
   for (uint32_t i = 0; i < kCrcSeg / 4; ++i) d[i] = q[i];
   uint32_t crc = first && l == l0 ? T.zinv[kCrcSeg - r] : 0u;
-#if LSMBLK_CRC_ABL == 3  // timing experiment: data reads, no table lookups
-#pragma unroll
-  for (uint32_t i = 0; i < kCrcSeg / 4; ++i) crc = __builtin_amdgcn_alignbit(crc, crc, 1) ^ d[i];
-#else
 #pragma unroll
   for (uint32_t i = 0; i < kCrcSeg / 4; ++i) crc = crc_apply(T.fold, crc ^ d[i]);
-#endif
   const uint32_t m = 63 - l;  // full windows after this one
-#if LSMBLK_CRC_ABL != 2 && LSMBLK_CRC_ABL != 3
 #pragma unroll
   for (uint32_t j = 0; j < 6; ++j)
     if ((m >> j) & 1) crc = crc_apply(T.shift[j], crc);
-#endif
   crc = live ? crc : 0u;
 #pragma unroll
   for (uint32_t dd = 32; dd >= 1; dd >>= 1) crc ^= __shfl_xor(crc, dd, 64);
+  if (t) crc = crc_apply(T.unz[t - 1], crc);
   return crc;
 }
 
@@ -393,6 +388,15 @@ inline void crc_host_tables(CrcTabs& T) {
   for (uint32_t j = 0; j < kCrcSeg; ++j) {
     T.zinv[j] = z;
     for (int s = 0; s < 8; ++s) z = crc_bit_unstep(z);
+  }
+  for (uint32_t t = 1; t <= 3; ++t) {  // Z(., t)^-1: 8 t inverse bit steps
+    uint32_t col[32];
+    for (uint32_t bit = 0; bit < 32; ++bit) {
+      uint32_t x = 1u << bit;
+      for (uint32_t s = 0; s < 8 * t; ++s) x = crc_bit_unstep(x);
+      col[bit] = x;
+    }
+    crc_nibble_tables(col, T.unz[t - 1]);
   }
   uint32_t col[32];
   for (uint32_t bit = 0; bit < 32; ++bit) {  // fold: 32 bit steps (4 zero bytes after the xor)

@@ -1582,11 +1582,11 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
     uint32_t acc = 0;
     for (uint32_t c = 0; c == 0 || c < nch; ++c) {  // an empty block still lands its (zero) loads
       const uint32_t sz = c == 0 ? h : kCrcChunk, lead = qlead;
-      // land the chunk at S + sh, sh making its end 4-aligned (aligned window reads in
-      // crc_chunk), with the lead bytes before it zeroed (they are in lane l0's window)
-      const uint32_t sh = LSMBLK_CRC_ABL == 4 ? 0u : (0u - (lead + sz)) & 3u;
+      // land the chunk at S + lead; the lead bytes before it (lane l0's window reaches them) and
+      // the t < 4 bytes after it (up to the next 4-aligned byte: crc_chunk's aligned windows)
+      // are zeroed in registers first
+      const uint32_t P = lead + sz, t = (0u - P) & 3u;
       if (l == 0) {
-        *reinterpret_cast<uint32_t*>(S) = 0;  // [S, S + sh): older chunks' bytes
         uint32_t* v = reinterpret_cast<uint32_t*>(&q[0]);
 #pragma unroll
         for (uint32_t d = 0; d < 4; ++d) {
@@ -1594,8 +1594,20 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
           v[d] &= z <= 0 ? ~0u : z >= 4 ? 0u : ~0u << (8 * z);
         }
       }
+      if (t && l == ((P >> 4) & 63)) {
 #pragma unroll
-      for (uint32_t i = 0; i < 5; ++i) *reinterpret_cast<u32x4*>(S + sh + 16 * (l + 64 * i)) = q[i];
+        for (uint32_t i = 0; i < 5; ++i) {
+          if (i != (P >> 10)) continue;
+          uint32_t* v = reinterpret_cast<uint32_t*>(&q[i]);
+#pragma unroll
+          for (uint32_t d = 0; d < 4; ++d) {
+            const int32_t z = int32_t(P & 15) - int32_t(4 * d);  // chunk bytes in this dword
+            v[d] &= z <= 0 ? 0u : z >= 4 ? ~0u : ~(~0u << (8 * z));
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i) *reinterpret_cast<u32x4*>(S + 16 * (l + 64 * i)) = q[i];
       wave_sync();
       {  // one issue site with uniform operands (two sites get merged into a divergent phi)
         const bool more = c + 1 < nch;
@@ -1603,8 +1615,8 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
         const uint32_t nsz = more ? kCrcChunk : nchn ? lenn - kCrcChunk * (nchn - 1) : 0u;
         if (more || has_next) issue(uni64(ncs), uni(nsz));
       }
-      if (nch && LSMBLK_CRC_ABL != 1) {
-        const uint32_t part = crc_chunk(T, S + sh + lead, sz, c == 0);
+      if (nch) {
+        const uint32_t part = crc_chunk(T, S + lead, sz, c == 0, t);
         acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
       }
       wave_sync();  // the next landing overwrites S
