@@ -253,6 +253,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     if extra:
         return result
     result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
+    result["read_path_verify"] = read_path_verify(blocks, blk_off, nblk, out_kv, n, K, V, st_dec, dev, stream)
     result["framing_meta"] = framing_meta(out_blocks, out_off, nblk, seg_t, st_enc, dev, stream)
     result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
     if world == 1 and not args.no_cpu_baseline:
@@ -647,6 +648,54 @@ def framing_crc32(blocks, blk_off, nblk, E, dev, stream, reps=5):
     return {"kernel": "crc_kernel", "ms": round(ms, 4), "gib_s": round(E / (ms * 1e-3) / GiB, 2),
             "achieved_gbs": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
             "bytes_per_launch": E, "checked_vs_zlib": int(len(idx)) if ok else 0, "ok": bool(ok)}
+
+
+def read_path_verify(blocks, blk_off, nblk, out_kv, n, K, V, st_dec, dev, stream, reps=5):
+    """read_block over a framed SST data section (src/table.rs:213-233): every
+    block followed by its BE crc32fast, decoded with verify=True -- one CRC pass over E that also
+    counts every block (in place of dec_count_kernel), the checksum test, scan and decode.  Timed
+    beside the plain decode of the same blocks; the KV stream must be identical.  Not part of
+    `value`."""
+    E = int(blk_off[nblk].item())
+    if E >= (1 << 33):
+        return None
+    crc = torch.zeros(nblk, dtype=torch.int32, device=dev)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+    batch.crc32_into(blocks, blk_off, nblk, crc, st)
+    off = blk_off.cpu().numpy()
+    be = crc.cpu().numpy().view(np.uint32).byteswap().view(np.uint8)
+    framed_h = np.insert(blocks.cpu().numpy(), np.repeat(off[1:], 4), be)
+    framed = torch.from_numpy(framed_h).to(dev)
+    del framed_h
+    foff = blk_off + 4 * torch.arange(nblk + 1, dtype=torch.int64, device=dev)
+    vkv = batch.KVStream(batch._aligned_empty(K + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
+                         batch._aligned_empty(V + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
+                         torch.empty(n, dtype=torch.int64, device=dev), n)
+    sv = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def run(verify):
+        if verify:
+            batch.decode_ex_into(framed, foff, nblk, vkv, sv, n, K, V, tail=4, verify=True)
+        else:
+            batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K, V)
+
+    ms = {}
+    for verify in (True, False, True):
+        run(verify)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            run(verify)
+        ev[1].record(stream)
+        torch.cuda.synchronize(dev)
+        ms["verify" if verify else "plain"] = ev[0].elapsed_time(ev[1]) / reps
+    ok = sv[3].item() == 0 and st_dec[3].item() == 0
+    ok = ok and all(torch.equal(a, b) for a, b in ((vkv.keys[:K], out_kv.keys[:K]), (vkv.vals[:V], out_kv.vals[:V]),
+                                                   (vkv.key_off, out_kv.key_off[:n + 1]),
+                                                   (vkv.val_off, out_kv.val_off[:n + 1]), (vkv.ts, out_kv.ts[:n])))
+    return {"kernels": "crc_kernel<count> + crc_verify + agg_tile + dec_scan + decode",
+            "framed_bytes": E + 4 * nblk, "verify_ms": round(ms["verify"], 4), "plain_decode_ms": round(ms["plain"], 4),
+            "verify_gib_s": round(E / (ms["verify"] * 1e-3) / GiB, 2), "kv_equal_to_plain_decode": bool(ok)}
 
 
 def framing_meta(blocks, blk_off, nblk, seg_t, st_enc, dev, stream, reps=5):

@@ -1473,7 +1473,7 @@ __global__ __launch_bounds__(256) void crc_verify_kernel(const uint8_t* blocks, 
                                                          const uint32_t* crc, const uint64_t* cstats, uint64_t* stats) {
   const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   uint32_t err = 0;
-  if (b == 0 && cstats[3]) err |= LSMBLK_ERR_MALFORMED;
+  if (b == 0) err |= uint32_t(cstats[3]);  // MALFORMED ranges, and the fused count's flags
   if (b < nblk) {
     const uint64_t e = blk_off[b + 1];
     if (e >= blk_off[b] + 4) {
@@ -1484,6 +1484,23 @@ __global__ __launch_bounds__(256) void crc_verify_kernel(const uint8_t* blocks, 
   }
   for (uint32_t d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
   raise_err(stats, err);
+}
+
+// Per-64-block tile sums of agg (what dec_count_kernel writes beside agg), one wave per tile.
+__global__ __launch_bounds__(256) void agg_tile_kernel(const uint32_t* agg, uint64_t nblk, uint64_t* tile_sum) {
+  const uint64_t tile = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6), b = tile * kTile + lane_id();
+  if (tile * kTile >= nblk) return;
+  uint64_t x[3] = {0, 0, 0};
+  if (b < nblk) {
+    x[0] = agg[3 * b];
+    x[1] = agg[3 * b + 1];
+    x[2] = agg[3 * b + 2];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint64_t t = wave_sum(x[i]);
+    if (lane_id() == 0) tile_sum[3 * tile + i] = t;
+  }
 }
 
 __global__ void finish_empty_decode(uint32_t* key_off, uint32_t* val_off, uint64_t cap) {
@@ -1523,8 +1540,40 @@ struct CrcArgs {
   uint32_t* crc;
   const CrcTabs* tabs;
   uint64_t* stats;
+  // optional (the verifying decode): per-block (entries, key bytes, value bytes) exactly as
+  // dec_count_kernel computes them, parsed from the staged block -- one read of E for both
+  uint32_t* agg;
 };
 
+// (entries, key bytes, value bytes) of one block with decode_block's parse rules; 0s and
+// MALFORMED for a block that breaks them, OVERFLOW past u32.  Written by lane 0.
+template <class Img>
+__device__ void count_block(const Img& im, uint32_t len, bool len_ok, uint32_t* agg, uint32_t& err) {
+  const uint32_t l = lane_id();
+  BlockHdr h = parse_hdr(im, len);
+  bool bad = !len_ok || !h.ok;
+  uint64_t K = 0, V = 0;
+  const uint32_t n = bad ? 0u : h.n;
+  for (uint32_t c = 0; c < n; c += 64) {
+    const uint32_t k = c + l;
+    uint32_t off = 0, p = 0, s = 0, vl = 0;
+    if (k < n) bad = bad || !parse_entry(im, h, k, off, p, s, vl);
+    K += wave_sum<uint64_t>(p + s);
+    V += wave_sum<uint64_t>(vl);
+  }
+  bad = __ballot(bad) != 0;
+  if (bad) err |= LSMBLK_ERR_MALFORMED;
+  if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+  if (l == 0) {
+    agg[0] = bad ? 0u : n;
+    agg[1] = bad ? 0u : uint32_t(K > 0xFFFFFFFFull ? 0xFFFFFFFFull : K);
+    agg[2] = bad ? 0u : uint32_t(V > 0xFFFFFFFFull ? 0xFFFFFFFFull : V);
+  }
+}
+
+// COUNT: also the per-block counts into a.agg (the verifying decode); a separate instantiation
+// so the plain CRC keeps its registers (and occupancy)
+template <bool COUNT>
 __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   __shared__ CrcTabs T;
   __shared__ __attribute__((aligned(16))) uint8_t stage[4][kCrcStage];
@@ -1543,12 +1592,14 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   uint64_t b = uint64_t(blockIdx.x) * 4 + w;
   if (b >= a.nblk) return;
   uint32_t err = 0;
-  auto meta = [&](uint64_t bi, uint64_t& st, uint32_t& len) {
+  bool len_ok = true, len_okn = true;
+  auto meta = [&](uint64_t bi, uint64_t& st, uint32_t& len, bool& lok) {
     const uint64_t s0 = uni64(a.blk_off[bi]), e0 = uni64(a.blk_off[bi + 1]);
     const bool ok = e0 >= s0 + a.tail && e0 - s0 <= 0x7FFFFFF0ull;
     if (!ok) err |= LSMBLK_ERR_MALFORMED;
     st = s0;
     len = ok ? uint32_t(e0 - s0) - a.tail : 0u;
+    lok = ok;
   };
   // Always five 16-B loads per lane (bytes past the chunk come back 0 from the descriptor's
   // bound) and five LDS stores: no predicated loads, so the compiler counts the waits
@@ -1567,8 +1618,8 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   // block metadata runs two blocks ahead of the folding, chunk loads one chunk ahead
   uint64_t st, stn = 0;
   uint32_t len, lenn = 0;
-  meta(b, st, len);
-  if (b + stride < a.nblk) meta(b + stride, stn, lenn);
+  meta(b, st, len, len_ok);
+  if (b + stride < a.nblk) meta(b + stride, stn, lenn, len_okn);
   uint32_t nch = (len + kCrcChunk - 1) / kCrcChunk;
   issue(st, nch ? len - kCrcChunk * (nch - 1) : 0u);
   for (;;) {
@@ -1576,7 +1627,8 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
     const bool has_next = bn < a.nblk;
     uint64_t st2 = 0;
     uint32_t len2 = 0;
-    if (b2 < a.nblk) meta(b2, st2, len2);
+    bool len_ok2 = true;
+    if (b2 < a.nblk) meta(b2, st2, len2, len_ok2);
     const uint32_t nchn = (lenn + kCrcChunk - 1) / kCrcChunk;
     const uint32_t h = len - kCrcChunk * (nch ? nch - 1 : 0u);  // first chunk's size
     uint32_t acc = 0;
@@ -1619,16 +1671,25 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
         const uint32_t part = crc_chunk(T, S + lead, sz, c == 0, t);
         acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
       }
+      if (COUNT && nch <= 1) count_block(LdsImg{S, lead}, len, len_ok, a.agg + 3 * b, err);
       wave_sync();  // the next landing overwrites S
+    }
+    if (COUNT && nch > 1) {  // a block over one chunk: its headers from global memory
+      const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(a.blocks + st) & 15));
+      const rsrc_t R = make_rsrc(reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uintptr_t>(a.blocks + st - lead))),
+                                 uni(lead + len));
+      count_block(GlbImg{R, lead}, len, len_ok, a.agg + 3 * b, err);
     }
     if (l == 0) a.crc[b] = nch ? ~acc : 0u;
     if (!has_next) break;
     b = bn;
     st = stn;
     len = lenn;
+    len_ok = len_okn;
     nch = nchn;
     stn = st2;
     lenn = len2;
+    len_okn = len_ok2;
   }
   raise_err(a.stats, err);
 }
@@ -2285,22 +2346,29 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
       return LSMBLK_E_NOMEM;
     }
     if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-    if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st))) return rc;
-    hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
-                       c->vcrc, c->meta_cstats, stats);
   }
   const uint64_t ntiles = (nblk + kTile - 1) / kTile;
-  CountArgs ca;
-  ca.blocks = blocks;
-  ca.blk_off = blk_off;
-  ca.nblk = nblk;
-  ca.agg = c->dec_agg;
-  ca.tile_sum = c->tile_sum;
-  ca.stats = stats;
-  ca.tail = tail;
   c->dec_timed = c->timing;
   if (c->timing) (void)hipEventRecord(c->ev[0], st);
-  hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
+  if (flags & LSMBLK_DECODE_VERIFY_CRC) {
+    // one pass over E: the CRC of every block and its (entries, key bytes, value bytes), in
+    // place of dec_count_kernel's second read of the headers
+    if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st, c->dec_agg)))
+      return rc;
+    hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
+                       c->vcrc, c->meta_cstats, stats);
+    hipLaunchKernelGGL(agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), 0, st, c->dec_agg, nblk, c->tile_sum);
+  } else {
+    CountArgs ca;
+    ca.blocks = blocks;
+    ca.blk_off = blk_off;
+    ca.nblk = nblk;
+    ca.agg = c->dec_agg;
+    ca.tile_sum = c->tile_sum;
+    ca.stats = stats;
+    ca.tail = tail;
+    hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
+  }
   if (c->timing) (void)hipEventRecord(c->ev[1], st);
   ScanArgs sa;
   sa.tile_sum = c->tile_sum;
@@ -2601,8 +2669,9 @@ int ensure_crc_tabs(lsmblk_ctx* c) {
 }
 
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
-               uint32_t* crc, uint64_t* stats, hipStream_t st) {
+               uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg) {
   CrcArgs a;
+  a.agg = agg;
   a.blocks = blocks;
   a.blk_off = blk_off;
   a.nblk = nblk;
@@ -2613,10 +2682,14 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
   // persistent: as many workgroups as are resident at once (4 KiB tables + 4 x 4 KiB staging)
   int cus = 256, per_cu = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, crc_kernel, 256, 0) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, agg ? crc_kernel<true> : crc_kernel<false>, 256, 0) !=
+          hipSuccess ||
+      per_cu < 1)
     per_cu = 3;
   const uint64_t want = (nblk + 3) / 4, cap = uint64_t(cus > 0 ? cus : 256) * uint64_t(per_cu);
-  hipLaunchKernelGGL(crc_kernel, dim3(uint32_t(want < cap ? want : cap)), dim3(256), 0, st, a);
+  const dim3 grid(uint32_t(want < cap ? want : cap));
+  if (agg) hipLaunchKernelGGL(crc_kernel<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(crc_kernel<false>, grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 }  // namespace lsmblk_impl lsmblk_impl

@@ -524,3 +524,46 @@ def test_decode_framed_section_verify_crc_and_block_entries():
     with pytest.raises(LsmBlkError) as e:
         batch.decode_blocks(db, do, tail=4, verify=True)
     assert e.value.status == LSMBLK_E_CHECKSUM
+
+
+def _framed(ref_blocks, ref_off, corrupt=None):
+    """Framed data section (block || BE crc32fast); corrupt(i, bytearray) may edit block i first
+    (its CRC is computed after the edit, so only the decode rules can catch it)."""
+    parts, off = [], [0]
+    for i in range(len(ref_off) - 1):
+        blk = bytearray(ref_blocks[int(ref_off[i]):int(ref_off[i + 1])].tobytes())
+        if corrupt:
+            corrupt(i, blk)
+        parts.append(bytes(blk) + zlib.crc32(blk).to_bytes(4, "big"))
+        off.append(off[-1] + len(parts[-1]))
+    return np.frombuffer(b"".join(parts), np.uint8).copy(), np.array(off, np.uint64)
+
+
+@pytest.mark.parametrize("gen,n,bs", [("mixed", 6000, 65536), ("uniform", 20000, 256), ("mixed", 3000, 4096)])
+def test_verifying_decode_counts_in_the_crc_pass(gen, n, bs):
+    """verify=True replaces dec_count_kernel by the CRC pass's fused count (blocks over one 4-KiB
+    CRC chunk count from global memory): same KV stream, block entry index, and MALFORMED for a
+    block that breaks the decode rules under a correct checksum."""
+    from lsm_amd._lib import LSMBLK_E_MALFORMED
+    g = {"mixed": synth.gen_mixed, "uniform": synth.gen_uniform}[gen]
+    kv = O.KV(*g(n, seed=23))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 1 << 20)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, bs)
+    assert rc == 0
+    framed, off = _framed(ref_blocks, ref_off)
+    db, do = dev_blocks(framed, off, 3)
+    got, ent = batch.decode_blocks(db, do, tail=4, verify=True, with_blk_ent=True)
+    assert_kv_equal(got, kv)
+    counts = [int.from_bytes(ref_blocks[int(ref_off[i + 1]) - 2:int(ref_off[i + 1])].tobytes(), "big")
+              for i in range(len(ref_off) - 1)]
+    np.testing.assert_array_equal(ent.cpu().numpy(), np.concatenate([[0], np.cumsum(counts)]))
+    nb = len(ref_off) - 1
+    for victim in {0, nb // 2, nb - 1}:
+        def corrupt(i, blk, victim=victim):
+            if i == victim:
+                blk[-2:] = b"\xff\xff"  # entry count beyond the block
+        bad, boff = _framed(ref_blocks, ref_off, corrupt)
+        db, do = dev_blocks(bad, boff)
+        with pytest.raises(LsmBlkError) as e:
+            batch.decode_blocks(db, do, tail=4, verify=True)
+        assert e.value.status == LSMBLK_E_MALFORMED
