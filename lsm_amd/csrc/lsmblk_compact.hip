@@ -829,8 +829,8 @@ struct RotArgs {
   uint64_t target;
   uint32_t* rec;            // n_max + 1
   uint32_t* alcp;           // n_max + 1
-  uint32_t* J;              // levels x (n_max + 1)
-  uint32_t* S;              // levels x (n_max + 1)
+  u32x2* JS;                // levels x (n_max + 1): {J_k[s], S_k[s]} side by side, so a doubling
+                            // step gathers both with one 8-B load (two 4-B gathers cost two sectors)
   uint32_t levels;          // levels allocated for J / S
   uint32_t* F0;             // n_max + 1: F, then the doubling ping-pong
   uint32_t* F1;
@@ -931,12 +931,10 @@ __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
       before += uint64_t(r) + 16 - p;
     }
     const uint64_t sz = before + 4;
-    a.J[s] = uint32_t(e);
-    a.S[s] = sz > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(sz);
+    a.JS[s] = u32x2{uint32_t(e), sz > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(sz)};
     short_chain = e < n && sz < a.target;
   } else if (s == n) {
-    a.J[s] = uint32_t(n);
-    a.S[s] = 0;
+    a.JS[s] = u32x2{uint32_t(n), 0u};
   }
   or_need(a.need + 0, short_chain);
 }
@@ -948,14 +946,12 @@ __global__ __launch_bounds__(256) void rot_double_kernel(RotArgs a, uint32_t k) 
   const uint64_t N1 = a.n_max + 1;
   bool short_chain = false;
   if (s <= n) {
-    const uint32_t* J0 = a.J + (k - 1) * N1;
-    const uint32_t* S0 = a.S + (k - 1) * N1;
-    const uint32_t j = J0[s];
-    const uint32_t jj = J0[j];
-    const uint64_t ss = uint64_t(S0[s]) + S0[j];
-    a.J[k * N1 + s] = jj;
-    a.S[k * N1 + s] = ss > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(ss);
-    short_chain = jj < n && ss < a.target;
+    const u32x2* L0 = a.JS + (k - 1) * N1;
+    const u32x2 v = L0[s];
+    const u32x2 w = L0[v.x];
+    const uint64_t ss = uint64_t(v.y) + w.y;
+    a.JS[k * N1 + s] = u32x2{w.x, ss > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(ss)};
+    short_chain = w.x < n && ss < a.target;
   }
   or_need(a.need + k, short_chain);
 }
@@ -972,14 +968,19 @@ __device__ __forceinline__ uint32_t rot_top(const RotArgs& a) {
 __device__ __forceinline__ uint64_t lift_target(const RotArgs& a, uint64_t pos, uint64_t& acc, uint64_t n,
                                                 uint32_t top) {
   const uint64_t N1 = a.n_max + 1;
-  while (pos < n && acc + a.S[top * N1 + pos] < a.target) {
-    acc += a.S[top * N1 + pos];
-    pos = a.J[top * N1 + pos];
+  while (pos < n) {
+    const u32x2 v = a.JS[top * N1 + pos];
+    if (acc + v.y >= a.target) break;
+    acc += v.y;
+    pos = v.x;
   }
   for (int k = int(top) - 1; k >= 0; --k) {
-    if (pos < n && acc + a.S[uint64_t(k) * N1 + pos] < a.target) {
-      acc += a.S[uint64_t(k) * N1 + pos];
-      pos = a.J[uint64_t(k) * N1 + pos];
+    if (pos < n) {
+      const u32x2 v = a.JS[uint64_t(k) * N1 + pos];
+      if (acc + v.y < a.target) {
+        acc += v.y;
+        pos = v.x;
+      }
     }
   }
   return pos;
@@ -990,14 +991,17 @@ __device__ __forceinline__ uint64_t lift_target(const RotArgs& a, uint64_t pos, 
 __device__ __forceinline__ uint64_t lift_before(const RotArgs& a, uint64_t pos, uint64_t& acc, uint64_t bound,
                                                 uint32_t top) {
   const uint64_t N1 = a.n_max + 1;
-  while (a.J[top * N1 + pos] < bound) {
-    acc += a.S[top * N1 + pos];
-    pos = a.J[top * N1 + pos];
+  for (;;) {
+    const u32x2 v = a.JS[top * N1 + pos];
+    if (v.x >= bound) break;
+    acc += v.y;
+    pos = v.x;
   }
   for (int k = int(top) - 1; k >= 0; --k) {
-    if (a.J[uint64_t(k) * N1 + pos] < bound) {
-      acc += a.S[uint64_t(k) * N1 + pos];
-      pos = a.J[uint64_t(k) * N1 + pos];
+    const u32x2 v = a.JS[uint64_t(k) * N1 + pos];
+    if (v.x < bound) {
+      acc += v.y;
+      pos = v.x;
     }
   }
   return pos;
@@ -1024,7 +1028,7 @@ __global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
   // lifting: the longest chain prefix from g whose data stays below the target
   const uint64_t pos = lift_target(a, g, acc, n, rot_top(a));
   // s_{j*}: the first block start whose entries see D >= target
-  a.F0[g] = uint32_t(pos < n ? key_change_after(a, a.J[pos], n) : n);
+  a.F0[g] = uint32_t(pos < n ? key_change_after(a, a.JS[pos].x, n) : n);
 }
 
 // ---------------------------------------------------------------- key-range shard rotation
@@ -1068,7 +1072,7 @@ __global__ void shard_carry_kernel(RotArgs a, const uint64_t* cin, uint64_t* cou
     if (D0 < a.target) {
       uint64_t acc = D0;
       const uint64_t pos = lift_target(a, p, acc, n, top);
-      sj = pos < n ? a.J[pos] : n;
+      sj = pos < n ? a.JS[pos].x : n;
     }
     E1 = key_change_after(a, sj, n);
     uint64_t x = p, accx = D0, fl = E1;
@@ -1091,11 +1095,12 @@ __global__ void shard_carry_kernel(RotArgs a, const uint64_t* cin, uint64_t* cou
       end = m;
     } else {        // it continues: its block chain crosses m
       const uint64_t pos = lift_before(a, x, accx, m, top);
-      const uint64_t b = a.J[pos];
+      const u32x2 v = a.JS[pos];
+      const uint64_t b = v.x;
       if (b >= n && !a.shard_last) err |= LSMBLK_ERR_SEGMENTS;  // the halo is too short
       end = b;
       pout = b - m;
-      Dout = b >= n ? 0 : accx + a.S[pos];  // the whole stream ends inside this SST: nothing continues
+      Dout = b >= n ? 0 : accx + v.y;  // the whole stream ends inside this SST: nothing continues
     }
   }
   uint64_t* w = a.sstate;
@@ -1358,8 +1363,7 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, u
   P.r.levels = L;
   P.r.rec = cv.take<uint32_t>(N1);
   P.r.alcp = cv.take<uint32_t>(N1);
-  P.r.J = cv.take<uint32_t>(N1 * L);
-  P.r.S = cv.take<uint32_t>(N1 * L);
+  P.r.JS = cv.take<u32x2>(N1 * L);
   if (flevels) {
     P.r.flevels = flevels;
     P.r.FL = cv.take<uint32_t>(N1 * flevels);
