@@ -899,9 +899,22 @@ __device__ __forceinline__ void or_need(uint32_t* flag, bool v) {
     atomicOr(flag, 1u);
 }
 
+// The workgroup's starts [s0, s0 + 256) walk at most a block's worth of entries past them
+// (each entry after the first grows the block by >= 16 bytes): (rec, alcp) of [s0, s0 + 256 +
+// kRotWin) are staged in LDS once, coalesced, instead of every lane re-reading its ~30 successors
+// from L2; a walk past the window (blocks over 8 KiB) reads global memory.
+constexpr uint32_t kRotWin = 512;
+
 __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
+  __shared__ uint32_t srec[256 + kRotWin], salcp[256 + kRotWin];
   const uint64_t n = rot_n(a);
-  const uint64_t s = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t s0 = uint64_t(blockIdx.x) * 256, s = s0 + threadIdx.x;
+  for (uint32_t i = threadIdx.x; i < 256 + kRotWin; i += 256) {
+    const uint64_t e = s0 + i;
+    srec[i] = e < n ? a.rec[e] : 0u;
+    salcp[i] = e < n ? a.alcp[e] : 0u;
+  }
+  __syncthreads();
   bool short_chain = false;
   if (s < n) {
     const uint64_t bs = a.block_size;
@@ -912,7 +925,9 @@ __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
     GKeys K;
     uint64_t e = s + 1;
     for (; e < n; ++e) {
-      const uint32_t r = a.rec[e], al = a.alcp[e];
+      const uint64_t x = e - s0;
+      const bool in = x < 256 + kRotWin;
+      const uint32_t r = in ? srec[x] : a.rec[e], al = in ? salcp[x] : a.alcp[e];
       if (before + r + 14 > bs) break;  // BlockBuilder::add rejects (builder.rs:56-60)
       uint32_t p;
       if (!direct && (al & kRotUnsorted)) {  // LCP vs the first key directly from here on
