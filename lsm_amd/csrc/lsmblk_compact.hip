@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
     }
   }
   __shared__ uint64_t ws[4][3];
-  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t w = wave_id();
   const uint32_t sc = wave_sum32(c);
   const uint64_t sk = wave_sum<uint64_t>(kb), sv = wave_sum<uint64_t>(vb);
   if (lane_id() == 0) ws[w][0] = sc, ws[w][1] = sk, ws[w][2] = sv;
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
   const uint64_t N = *a.nm;
   __shared__ uint64_t ws[4][3];
   __shared__ __attribute__((aligned(16))) uint8_t kimg[kGKImg + 32], vimg[kGVImg + 32];
-  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t w = wave_id();
   uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)], a.tile_pre[3 * uint64_t(blockIdx.x) + 1],
                        a.tile_pre[3 * uint64_t(blockIdx.x) + 2]};
   for (uint32_t sub = 0; sub < kGTile / 256; ++sub) {

@@ -31,6 +31,9 @@ __device__ __forceinline__ uint64_t lane64(uint64_t x, uint32_t j) {
   return (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), j))) << 32) |
          uint32_t(__builtin_amdgcn_readlane(uint32_t(x), j));
 }
+// threadIdx.x / 64 through readfirstlane: the compiler does not know it is wave-uniform, and a
+// loop bound or block index derived from it would compile to an exec-masked (divergent) loop
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

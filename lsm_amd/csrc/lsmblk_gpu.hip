@@ -613,7 +613,7 @@ __device__ __forceinline__ uint32_t gb16(const uint8_t* p, uint32_t i) {
 
 __global__ __launch_bounds__(256) void dec_count_kernel(CountArgs a) {
   __shared__ uint64_t red[4][3];
-  const uint32_t l = lane_id(), w = threadIdx.x >> 6, grp = l >> 4, sl = l & 15;
+  const uint32_t l = lane_id(), w = wave_id(), grp = l >> 4, sl = l & 15;
   const uint64_t tile = blockIdx.x;
   uint64_t tn = 0, tk = 0, tv = 0;
   uint32_t err = 0;
@@ -886,8 +886,8 @@ constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
 __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
   __shared__ uint32_t crec[4][kWalk], calcp[4][kWalk];
-  uint32_t* CR = crec[threadIdx.x >> 6];
-  uint32_t* CA = calcp[threadIdx.x >> 6];
+  uint32_t* CR = crec[wave_id()];
+  uint32_t* CA = calcp[wave_id()];
   const uint32_t l = lane_id();
   const uint32_t g = take_ticket(a.ticket);
   if (g >= a.nseg) return;
@@ -1169,7 +1169,7 @@ struct EmitMeta {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void emit_kernel(EmitArgs a0) {
   const EmitArgs a = resolve(a0);
   __shared__ EmitLds lds[kEmitWaves];
-  EmitLds& L = lds[threadIdx.x >> 6];
+  EmitLds& L = lds[threadIdx.x >> 6];  // (a VGPR LDS base: readfirstlane here costs the kernel 4 spilled VGPRs)
   const uint32_t l = lane_id();
   const uint64_t nblk = uni64(a.stats[0]);
   const uint64_t nwaves = uint64_t(gridDim.x) * kEmitWaves;
@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     }
   };
 
-  uint64_t bi0 = uint64_t(blockIdx.x) * kEmitWaves + (threadIdx.x >> 6);
+  uint64_t bi0 = uint64_t(blockIdx.x) * kEmitWaves + wave_id();
   if (bi0 >= lim) {
     raise_err(a.stats, err);
     return;
@@ -1452,7 +1452,7 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   const uint64_t nw = uint64_t(gridDim.x) * 4;
   const uint32_t l = lane_id();
   uint32_t err = 0;
-  for (uint64_t base = blockIdx.x * 4 + (threadIdx.x >> 6); base < lim; base += nw * 64) {
+  for (uint64_t base = blockIdx.x * 4 + wave_id(); base < lim; base += nw * 64) {
     const uint64_t mine = base + nw * l;
     uint64_t big = __ballot(mine < lim && a.big_flag[mine]);
     while (big) {
@@ -1488,7 +1488,7 @@ __global__ __launch_bounds__(256) void crc_verify_kernel(const uint8_t* blocks, 
 
 // Per-64-block tile sums of agg (what dec_count_kernel writes beside agg), one wave per tile.
 __global__ __launch_bounds__(256) void agg_tile_kernel(const uint32_t* agg, uint64_t nblk, uint64_t* tile_sum) {
-  const uint64_t tile = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6), b = tile * kTile + lane_id();
+  const uint64_t tile = uint64_t(blockIdx.x) * 4 + wave_id(), b = tile * kTile + lane_id();
   if (tile * kTile >= nblk) return;
   uint64_t x[3] = {0, 0, 0};
   if (b < nblk) {
@@ -1589,17 +1589,21 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   __syncthreads();
   uint8_t* S = stage[w] + kCrcPad;
   const uint64_t stride = uint64_t(gridDim.x) * 4;
-  uint64_t b = uint64_t(blockIdx.x) * 4 + w;
+  // (readfirstlane: the compiler does not know threadIdx.x >> 6 is wave-uniform, and a block
+  // index it thinks divergent makes the whole block loop an exec-masked one)
+  uint64_t b = uni64(uint64_t(blockIdx.x) * 4 + w);
   if (b >= a.nblk) return;
   uint32_t err = 0;
   bool len_ok = true, len_okn = true;
-  auto meta = [&](uint64_t bi, uint64_t& st, uint32_t& len, bool& lok) {
-    const uint64_t s0 = uni64(a.blk_off[bi]), e0 = uni64(a.blk_off[bi + 1]);
+  auto meta_of = [&](uint64_t s0, uint64_t e0, uint64_t& st, uint32_t& len, bool& lok) {
     const bool ok = e0 >= s0 + a.tail && e0 - s0 <= 0x7FFFFFF0ull;
     if (!ok) err |= LSMBLK_ERR_MALFORMED;
     st = s0;
     len = ok ? uint32_t(e0 - s0) - a.tail : 0u;
     lok = ok;
+  };
+  auto meta = [&](uint64_t bi, uint64_t& st, uint32_t& len, bool& lok) {
+    meta_of(uni64(a.blk_off[bi]), uni64(a.blk_off[bi + 1]), st, len, lok);
   };
   // Always five 16-B loads per lane (bytes past the chunk come back 0 from the descriptor's
   // bound) and five LDS stores: no predicated loads, so the compiler counts the waits
@@ -1625,10 +1629,10 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   for (;;) {
     const uint64_t bn = b + stride, b2 = bn + stride;
     const bool has_next = bn < a.nblk;
-    uint64_t st2 = 0;
-    uint32_t len2 = 0;
-    bool len_ok2 = true;
-    if (b2 < a.nblk) meta(b2, st2, len2, len_ok2);
+    // block b2's offsets: loaded after the first landing (so the landing never waits for them)
+    // into VGPRs, made uniform only at the end of this block -- a readfirstlane right away would
+    // wait (vmcnt counts in order) for a full memory round trip
+    uint64_t r0 = 0, r1 = 0;
     const uint32_t nchn = (lenn + kCrcChunk - 1) / kCrcChunk;
     const uint32_t h = len - kCrcChunk * (nch ? nch - 1 : 0u);  // first chunk's size
     uint32_t acc = 0;
@@ -1660,6 +1664,10 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
       }
 #pragma unroll
       for (uint32_t i = 0; i < 5; ++i) *reinterpret_cast<u32x4*>(S + 16 * (l + 64 * i)) = q[i];
+      if (c == 0 && b2 < a.nblk) {
+        r0 = a.blk_off[b2];
+        r1 = a.blk_off[b2 + 1];
+      }
       wave_sync();
       {  // one issue site with uniform operands (two sites get merged into a divergent phi)
         const bool more = c + 1 < nch;
@@ -1682,6 +1690,10 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
     }
     if (l == 0) a.crc[b] = nch ? ~acc : 0u;
     if (!has_next) break;
+    uint64_t st2 = 0;
+    uint32_t len2 = 0;
+    bool len_ok2 = true;
+    if (b2 < a.nblk) meta_of(uni64(r0), uni64(r1), st2, len2, len_ok2);
     b = bn;
     st = stn;
     len = lenn;
@@ -1776,7 +1788,7 @@ __global__ __launch_bounds__(256) void meta_size_kernel(MetaArgs a) {
   }
   __shared__ uint32_t ws[4];
   const uint32_t t = wave_sum32(r);
-  if (lane_id() == 0) ws[threadIdx.x >> 6] = t;
+  if (lane_id() == 0) ws[wave_id()] = t;
   __syncthreads();
   if (threadIdx.x == 0) a.tile_sum[blockIdx.x] = uint64_t(ws[0]) + ws[1] + ws[2] + ws[3];
 }
@@ -1866,7 +1878,7 @@ __global__ __launch_bounds__(256) void meta_write_kernel(MetaArgs a) {
   const bool live = b < a.nblk;
   const uint32_t r = live ? a.rec[b] : 0u;
   const uint32_t inc = wave_incl_scan32(r);
-  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t w = wave_id();
   if (lane_id() == 63) ws[w] = inc;
   __syncthreads();
   uint64_t pos = a.tile_pre[blockIdx.x] + inc - r;
@@ -2048,7 +2060,7 @@ __global__ __launch_bounds__(256) void filt_flag_kernel(FiltArgs a) {
     }
   }
   __shared__ uint64_t ws[4][3];
-  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t w = wave_id();
   const uint32_t sc = wave_sum32(c);
   const uint64_t sk = wave_sum<uint64_t>(kb), sv = wave_sum<uint64_t>(vb);
   if (lane_id() == 0) ws[w][0] = sc, ws[w][1] = sk, ws[w][2] = sv;
@@ -2121,7 +2133,7 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
 __global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
   if (a.stats[3]) return;
   __shared__ uint64_t ws[4][3];
-  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t w = wave_id();
   uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)], a.tile_pre[3 * uint64_t(blockIdx.x) + 1],
                        a.tile_pre[3 * uint64_t(blockIdx.x) + 2]};
   for (uint32_t sub = 0; sub < kFiltTile / 256; ++sub) {  // 256 entries per round, running carry

@@ -271,7 +271,7 @@ __device__ __forceinline__ uint32_t sst_of_block(const SstArgs& a, uint64_t b) {
 // One wave per block: block bytes, then its BE crc32fast (finish_block, builder.rs:118-122).
 __global__ __launch_bounds__(256) void sst_data_kernel(SstArgs a) {
   if (a.stats[3]) return;
-  const uint64_t b = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const uint64_t b = uint64_t(blockIdx.x) * 4 + wave_id();
   if (b >= a.nblk) return;
   const uint32_t s = sst_of_block(a, b);
   const uint32_t b0 = a.sst_blk[s];
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void sst_data_kernel(SstArgs a) {
 // One wave per SST: the BlockMeta section and the u32 meta_offset (builder.rs:76-78).
 __global__ __launch_bounds__(256) void sst_meta_kernel(SstArgs a) {
   if (a.stats[3]) return;
-  const uint64_t s = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const uint64_t s = uint64_t(blockIdx.x) * 4 + wave_id();
   if (s >= a.nsst) return;
   const uint64_t dl = a.data_len[s], m0 = a.meta_off[s], ml = a.meta_off[s + 1] - m0;
   uint8_t* d = a.files + a.file_off[s] + dl;
