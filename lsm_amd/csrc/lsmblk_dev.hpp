@@ -31,6 +31,13 @@ __device__ __forceinline__ uint64_t lane64(uint64_t x, uint32_t j) {
   return (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), j))) << 32) |
          uint32_t(__builtin_amdgcn_readlane(uint32_t(x), j));
 }
+// Read-only views in the constant address space: a uniform-address load through one is a scalar
+// load (s_load: SGPR result, waited by lgkmcnt, so it never queues behind the vector loads that
+// vmcnt counts in order).  Only for data no kernel of the same launch writes.
+typedef const __attribute__((address_space(4))) uint32_t cu32_t;
+typedef const __attribute__((address_space(4))) uint64_t cu64_t;
+__device__ __forceinline__ cu32_t* kconst(const uint32_t* p) { return (cu32_t*)p; }
+__device__ __forceinline__ cu64_t* kconst(const uint64_t* p) { return (cu64_t*)p; }
 // threadIdx.x / 64 through readfirstlane: the compiler does not know it is wave-uniform, and a
 // loop bound or block index derived from it would compile to an exec-masked (divergent) loop
 __device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }

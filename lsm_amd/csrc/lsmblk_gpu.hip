@@ -1177,13 +1177,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
   const uint64_t lim = nblk < a.blk_cap ? nblk : (a.blk_cap ? a.blk_cap - 1 : 0);  // blk_off[bi+1] must exist
 
+  // block metadata by scalar loads (written by the plan kernels / the caller, read-only here):
+  // they wait on lgkmcnt, not behind the staging loads in flight
+  cu32_t* const kfirst = kconst(a.blk_first);
+  cu64_t* const koff = kconst(a.blk_off);
   auto meta1 = [&](uint64_t bi, EmitMeta& m) {
     m.bi = bi;
-    m.s = uni(a.blk_first[bi]);
-    m.e = uni(a.blk_first[bi + 1]);
+    m.s = kfirst[bi];
+    m.e = kfirst[bi + 1];
     m.n = m.e - m.s;
-    m.O = uni64(a.blk_off[bi]);
-    m.size = uni64(a.blk_off[bi + 1]) - m.O;
+    m.O = koff[bi];
+    m.size = koff[bi + 1] - m.O;
   };
   auto meta2 = [&](EmitMeta& m) {
     m.kb0 = uni(a.key_off[m.s]);
@@ -1235,7 +1239,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint64_t bn = cur.bi + nwaves;
     const bool has_next = bn < lim;
     EmitMeta nxt;
-    if (has_next) meta1(uni64(bn), nxt);  // level-1 of the next block, in flight now
+    if (has_next) meta1(bn, nxt);  // level-1 of the next block (scalar loads)
     const uint32_t s = cur.s, n = cur.n;
     const uint64_t O = cur.O, size = cur.size;
     const uint32_t kb0 = cur.kb0, kb1 = cur.kb1, vb0 = cur.vb0, vb1 = cur.vb1;
@@ -1262,7 +1266,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       for (uint32_t i = 0; i < 5; ++i)
         if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = vq[i];
     }
-    if (has_next) meta2(nxt);  // level-2 of the next block
+    // level-2 of the next block: loaded now into VGPRs, made uniform after phase 1 (a
+    // readfirstlane here would stall on the loads' round trip)
+    uint32_t r_kb0 = 0, r_kb1 = 0, r_vb0 = 0, r_vb1 = 0;
+    __builtin_amdgcn_sched_barrier(0);  // (not hoisted into the landing: its waits would cover them)
+    if (has_next) {
+      r_kb0 = a.key_off[nxt.s];
+      r_kb1 = a.key_off[nxt.e];
+      r_vb0 = a.val_off[nxt.s];
+      r_vb1 = a.val_off[nxt.e];
+    }
     wave_sync();
     // Phase 1, entry lanes: LCP against the first key, record positions (wave scan), tables,
     // and the value bytes of each value's two partial edge chunks (captured in registers: the
@@ -1345,6 +1358,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint32_t data_len = dc;
     if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
     if (has_next) {  // next block's staging loads overlap the rest of this block
+      nxt.kb0 = uni(r_kb0);
+      nxt.kb1 = uni(r_kb1);
+      nxt.vb0 = uni(r_vb0);
+      nxt.vb1 = uni(r_vb1);
       nxt_fast = is_fast(nxt);
       if (nxt_fast) issue(nxt);
     }
