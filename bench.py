@@ -60,6 +60,9 @@ def parse(argv=None):
     p.add_argument("--config", default="U", choices=["U", "Z", "M", "C"])
     p.add_argument("--blocks", type=int, default=None, help="blocks per GPU (default 1 Mi for U/Z/C, 64 Ki for M)")
     p.add_argument("--segment-bytes", type=int, default=2 << 20)
+    p.add_argument("--ranges-per-gpu", type=int, default=1,
+                   help="config C: key ranges per GPU (each under one call's 4 GiB KV arenas); e.g. "
+                        "--blocks 3145728 --ranges-per-gpu 3 is 12.5 GiB of input per GPU (100 GiB on 8)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip the Z / M / C extra configs at N=1")
@@ -386,7 +389,7 @@ def oracle_check_range(host, rs, opts, sh, res):
 
 
 def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
-    if world > 1:
+    if world > 1 or args.ranges_per_gpu > 1:
         return run_compaction_sharded(args, steps, warmup, rank, world, local, dev)
     nblk_in = args.blocks or (1 << 20)
     nrun = 8
@@ -453,82 +456,108 @@ def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
 
 def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
     """Config C over N GPUs, split by key range: rank r's storage holds
-    slice r of the key space in every run (its L0 SSTs' blocks, resident in HBM); the splitters are
-    the ranks' lowest BlockMeta first keys (one all-gather), so no input block belongs to two
-    ranges.  One step = decode + merge / rules (range-restricted) + halo all-gather + rotation +
-    carry send/recv + block packing (shard.compact_dist): together the ranks' outputs are the
-    single-stream compaction of all N slices, byte for byte, SST boundaries included."""
+    slice r of the key space in every run (its L0 SSTs' blocks, resident in HBM) -- R slices with
+    --ranges-per-gpu R, one key range each; the splitters are the ranges' lowest BlockMeta first
+    keys (one all-gather), so no input block belongs to two ranges.  One step = decode + merge /
+    rules (range-restricted) + halo all-gather + rotation + carry (through the rank's ranges, then
+    send/recv to the next rank) + block packing (shard.compact_dist, or shard.compact_local on one
+    GPU): together the outputs are the single-stream compaction of all N x R slices, byte for byte,
+    SST boundaries included."""
     import torch.distributed as dist
     from lsm_amd import shard
+    R = max(1, args.ranges_per_gpu)
     nblk_in = args.blocks or (1 << 20)
     nrun = 8
-    blocks, blk_off, rs, host = build_runs(nblk_in, nrun, args.segment_bytes, 2000 + rank, dev,
-                                           key_slice=(rank, world))
-    nblk = blk_off.numel() - 1
-    E = int(blocks.numel())
-    n = int(rs[-1])
-    K, V = len(host[0]), len(host[2])
-    keys, ko = host[0], host[1]
-    first = min(bytes(keys[ko[rs[r]]:ko[rs[r] + 1]]) for r in range(nrun) if rs[r] < rs[r + 1])
-    cdev = shard.comm_device(dev)
-    splitters = shard.exchange_splitters([first], samples=1, device=cdev)
-    lo, hi = shard.range_of(rank, splitters)
-    kv = batch.KVStream.empty(n, K, V, dev)
-    st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
-    # one wm for the whole job (the reference's LsmMvccInner::watermark is global)
-    wm = torch.tensor([int(host[4].max()) // 2], dtype=torch.int64, device=cdev)
-    dist.all_reduce(wm, op=dist.ReduceOp.MAX)
-    opts = batch.compact_opts(watermark=int(wm.item()), bottom_level=True, block_size=4096,
+    parts = [build_runs(nblk_in // R, nrun, args.segment_bytes, 2000 + rank * R + i, dev,
+                        key_slice=(rank * R + i, world * R)) for i in range(R)]
+    E = sum(int(p[0].numel()) for p in parts)
+    nblk = sum(p[1].numel() - 1 for p in parts)
+    n_all = sum(int(p[2][-1]) for p in parts)
+    firsts = []
+    for blocks_i, off_i, rs, host in parts:
+        keys, ko = host[0], host[1]
+        firsts.append(min(bytes(keys[ko[rs[r]]:ko[rs[r] + 1]]) for r in range(nrun) if rs[r] < rs[r + 1]))
+    if world > 1:
+        cdev = shard.comm_device(dev)
+        splitters = shard.exchange_splitters(firsts, samples=R, device=cdev, ranges=world * R)
+        # one wm for the whole job (the reference's LsmMvccInner::watermark is global)
+        wm = torch.tensor([max(int(p[3][4].max()) for p in parts) // 2], dtype=torch.int64, device=cdev)
+        dist.all_reduce(wm, op=dist.ReduceOp.MAX)
+        wm = int(wm.item())
+    else:
+        cdev = torch.device("cpu")
+        splitters = shard.choose_splitters(firsts, R)
+        wm = max(int(p[3][4].max()) for p in parts) // 2
+    opts = batch.compact_opts(watermark=wm, bottom_level=True, block_size=4096,
                               target_sst_size=args.segment_bytes, device=dev)
     stream = torch.cuda.current_stream(dev)
-    sh = shard.RangeShard(kv, rs, opts, lo, hi, stream=stream)
-    res = {}
+    kvs, decs, shards = [], [], []
+    for i, (blocks_i, off_i, rs, host) in enumerate(parts):
+        n, K, V = int(rs[-1]), len(host[0]), len(host[2])
+        kvs.append(batch.KVStream.empty(n, K, V, dev))
+        decs.append(torch.zeros(4, dtype=torch.int64, device=dev))
+        lo, hi = shard.range_of(rank * R + i, splitters)
+        shards.append(shard.RangeShard(kvs[-1], rs, opts, lo, hi, stream=stream))
+    res = []
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        batch.decode_into(blocks, blk_off, nblk, kv, st_dec, n, K + 16, V + 16)
-        kv.n = n
+        for (blocks_i, off_i, rs, host), kv, sd in zip(parts, kvs, decs):
+            n, K, V = int(rs[-1]), len(host[0]), len(host[2])
+            batch.decode_into(blocks_i, off_i, off_i.numel() - 1, kv, sd, n, K + 16, V + 16)
+            kv.n = n
         if ev is not None:
             ev[1].record(stream)
-        res.update(shard.compact_dist(sh))
+        res[:] = shard.compact_dist(shards) if world > 1 else shard.compact_local(shards)
         if ev is not None:
             ev[2].record(stream)
 
     elapsed, (dec_ms, cmp_ms) = timed(step, steps, warmup, world, dev)
-    sd = st_dec.cpu().tolist()
-    ok = sd[3] == 0 and sd[0] == n
+    ok = all(sd.cpu().tolist()[3] == 0 and sd.cpu().tolist()[0] == int(p[2][-1]) for sd, p in zip(decs, parts))
     checked = 0
     if ok and not args.no_oracle_check:
-        checked = oracle_check_range(host, rs, opts, sh, res)
-        ok = checked == res["nblk"]
-    # the carries chain: carry-out of rank r == carry-in of rank r + 1
-    cc = torch.tensor(list(res["carry_in"]) + list(res["carry_out"]), dtype=torch.int64, device=cdev)
-    allc = [torch.zeros_like(cc) for _ in range(world)]
-    dist.all_gather(allc, cc)
-    allc = [c.cpu().tolist() for c in allc]
-    chain_ok = allc[0][:2] == [0, 0] and all(allc[r][2:] == allc[r + 1][:2] for r in range(world - 1))
-    tot = torch.tensor([res["nblk"], res["nbytes"], res["nseg"] - int(res["first_continues"]), res["m"],
-                        res["merged"]], dtype=torch.int64, device=cdev)
-    dist.all_reduce(tot)
+        for (blocks_i, off_i, rs, host), sh, r in zip(parts, shards, res):
+            c = oracle_check_range(host, rs, opts, sh, r)
+            ok = ok and c == r["nblk"]
+            checked += c
+    # the carries chain through every range: carry-out of range g == carry-in of range g + 1
+    cc = torch.tensor([x for r in res for x in list(r["carry_in"]) + list(r["carry_out"])], dtype=torch.int64,
+                      device=cdev)
+    if world > 1:
+        allc = [torch.zeros_like(cc) for _ in range(world)]
+        dist.all_gather(allc, cc)
+        flat = [x for c in allc for x in c.cpu().tolist()]
+    else:
+        flat = cc.cpu().tolist()
+    chain = [flat[4 * g:4 * g + 4] for g in range(world * R)]
+    chain_ok = chain[0][:2] == [0, 0] and all(chain[g][2:] == chain[g + 1][:2] for g in range(world * R - 1))
+    tot = torch.tensor([sum(r["nblk"] for r in res), sum(r["nbytes"] for r in res),
+                        sum(r["nseg"] - int(r["first_continues"]) for r in res), sum(r["m"] for r in res),
+                        sum(r["merged"] for r in res)], dtype=torch.int64, device=cdev)
+    if world > 1:
+        dist.all_reduce(tot)
     t_max, ok_all, checked_all = reduce_ranks(elapsed, ok and chain_ok, checked, world, dev)
     if rank != 0:
         return None
     ms = t_max / steps * 1e3
     tot = tot.cpu().tolist()
+    backend = ("RCCL" if dist.get_backend() == "nccl" else "gloo") if world > 1 else "in-process"
     return {
         "metric": METRIC, "value": round(world * E * steps / t_max / GiB, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"C: compaction-shaped, {nrun} overlapping sorted runs of {args.segment_bytes >> 20} MiB "
-                               f"SSTs ({nblk} x 4 KiB input blocks/GPU, ~10% overwrites, 2% tombstones), split by "
-                               f"key range over {world} GPUs: decode + range merge + compaction rules + halo "
-                               "all-gather + SST rotation with rank-to-rank carry + block packing",
-                   "input_blocks_per_gpu": nblk, "input_entries_per_gpu": n, "encoded_bytes_per_gpu": E,
+                               f"SSTs ({nblk} x 4 KiB input blocks/GPU, {E / GiB:.2f} GiB/GPU, ~10% overwrites, 2% "
+                               f"tombstones), split by key range into {world} GPUs x {R} ranges: decode + range merge "
+                               "+ compaction rules + halo all-gather + SST rotation with range-to-range carry + block "
+                               "packing",
+                   "input_blocks_per_gpu": nblk, "input_entries_per_gpu": n_all, "encoded_bytes_per_gpu": E,
+                   "ranges_per_gpu": R, "total_input_gib": round(world * E / GiB, 2),
                    "merged_entries": tot[4], "kept_entries": tot[3], "output_blocks": tot[0], "output_bytes": tot[1],
                    "output_ssts": tot[2], "target_sst_size": args.segment_bytes,
-                   "parallelism": f"key-range sharded x{world} ({'RCCL' if dist.get_backend() == 'nccl' else 'gloo'}: "
-                                  "splitter + halo all-gather, carry send/recv)",
+                   "parallelism": f"key-range sharded x{world}x{R} ({backend}: splitter + halo all-gather, "
+                                  "carry send/recv)",
                    "rccl_world": world, "compaction_bit_exact": bool(ok_all), "carry_chain_ok": bool(chain_ok),
                    "oracle_checked_blocks": int(checked_all)},
         "stage_ms": {"decode": round(dec_ms, 4), "compact": round(cmp_ms, 4)},

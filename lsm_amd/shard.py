@@ -91,14 +91,16 @@ def choose_splitters(all_samples, world: int):
     return [keys[(i * len(keys)) // world] for i in range(1, world)]
 
 
-def exchange_splitters(first_keys, samples: int = 64, max_key_bytes: int = 64, device=None):
+def exchange_splitters(first_keys, samples: int = 64, max_key_bytes: int = 64, device=None, ranges: int = None):
     """All-gather every rank's key samples (fixed-size records in one tensor) and return
-    the common splitters.  Keys longer than max_key_bytes are truncated for the sample,
-    which only moves a splitter (any byte string splits the key space)."""
+    the common splitters: ranges - 1 of them (default: one range per rank).  Keys longer than
+    max_key_bytes are truncated for the sample, which only moves a splitter (any byte string
+    splits the key space)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
+    nr = ranges or world
     mine = sample_first_keys(first_keys, samples)
     if world == 1:
-        return choose_splitters(mine, 1)
+        return choose_splitters(mine, nr)
     rec = 2 + max_key_bytes
     payload = bytearray(_pack_keys(mine, max_key_bytes))
     payload += b"\0" * (rec * samples - len(payload))
@@ -111,7 +113,7 @@ def exchange_splitters(first_keys, samples: int = 64, max_key_bytes: int = 64, d
     allk = []
     for c, b in zip(counts, bufs):
         allk += _unpack_keys(bytes(b.cpu().numpy()[:int(c.item()) * rec]), max_key_bytes)
-    return choose_splitters(allk, world)
+    return choose_splitters(allk, nr)
 
 
 def owner_of(key: bytes, splitters) -> int:
@@ -397,13 +399,20 @@ def _allgather_heads(head: Head, group=None):
     return heads
 
 
-def compact_dist(shard: RangeShard, group=None):
-    """One range per rank (rank order = key order) over torch.distributed: merge, all-gather the
-    heads, prepare, carry from rank - 1 to rank + 1, encode.  Returns the rank's result."""
-    if shard.dev.type == "cuda":
-        with torch.cuda.stream(shard.stream):
-            return _compact_dist(shard, group)
-    return _compact_dist(shard, group)
+def compact_dist(shard, group=None):
+    """Key ranges over torch.distributed, rank order = key order: one RangeShard per rank, or a list
+    of R shards per rank (the same R on every rank; rank r holds ranges r*R .. r*R + R - 1 -- a
+    compaction larger than one call's 4 GiB KV arenas).  Merge, all-gather the heads, prepare,
+    carry through the rank's ranges from rank - 1 to rank + 1, encode.  Returns the result (or the
+    list of results)."""
+    shards = shard if isinstance(shard, (list, tuple)) else [shard]
+    s0 = shards[0]
+    if s0.dev.type == "cuda":
+        with torch.cuda.stream(s0.stream):
+            res = _compact_dist(shards, group)
+    else:
+        res = _compact_dist(shards, group)
+    return res if isinstance(shard, (list, tuple)) else res[0]
 
 
 def comm_device(device, group=None):
@@ -411,19 +420,29 @@ def comm_device(device, group=None):
     return torch.device("cpu") if dist.get_backend(group) == "gloo" else torch.device(device)
 
 
-def _compact_dist(shard, group):
+def _compact_dist(shards, group):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    cdev = comm_device(shard.dev, group)
-    shard.merge()
-    heads = _allgather_heads(shard.head().to(cdev), group)
-    halo = assemble_halo(heads, rank, shard.W)
-    shard.set_halo(*[x.to(shard.dev) for x in halo[:5]], halo[5])
-    shard.prepare()
+    R = len(shards)
+    cdev = comm_device(shards[0].dev, group)
+    for s in shards:
+        s.merge()
+    # one all-gather per local range index: heads[r * R + i] = rank r's range i
+    per = [_allgather_heads(s.head().to(cdev), group) for s in shards]
+    heads = [per[i][r] for r in range(world) for i in range(R)]
+    for i, s in enumerate(shards):
+        halo = assemble_halo(heads, rank * R + i, s.W)
+        s.set_halo(*[x.to(s.dev) for x in halo[:5]], halo[5])
+        s.prepare()
     cin = torch.zeros(2, dtype=torch.int64, device=cdev)
     if rank > 0:
         dist.recv(cin, src=rank - 1, group=group)
-    cout = shard.carry(cin.to(shard.dev))
+    c = cin.to(shards[0].dev)
+    for s in shards:
+        if s.dev.type == "cuda":
+            torch.cuda.synchronize(s.dev)   # the carry-in may come from another range's stream
+        c = s.carry(c.to(s.dev)).clone()
     if rank + 1 < world:
-        dist.send(cout.to(cdev), dst=rank + 1, group=group)
-    shard.encode()
-    return shard.result()
+        dist.send(c.to(cdev), dst=rank + 1, group=group)
+    for s in shards:
+        s.encode()
+    return [s.result() for s in shards]

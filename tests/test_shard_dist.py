@@ -84,7 +84,7 @@ class OracleShard:
                     first_continues=nseg > 0 and self.cin[1] > 0, carry_in=self.cin, carry_out=self.cout)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, R=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -93,31 +93,36 @@ def _worker(rank, world, port, q):
         # every rank "holds" a slice of every run: sample the first keys of its slice's 32-entry blocks
         n = kv.n
         mine = [kv.entry(i)[0] for i in range(rank * n // world, (rank + 1) * n // world, 32)]
-        splitters = shard.exchange_splitters(sorted(mine), samples=16)
-        lo, hi = shard.range_of(rank, splitters)
-        s = OracleShard(kv, rs, int(kv.ts.max()) // 2, True, lo, hi)
-        res = shard.compact_dist(s)
-        q.put((rank, res["blocks"], res["seg_start"].tolist(), res["nseg"], res["m"], res["first_continues"],
-               res["carry_in"], res["carry_out"], splitters))
+        splitters = shard.exchange_splitters(sorted(mine), samples=16, ranges=world * R)
+        wm = int(kv.ts.max()) // 2
+        if R == 1:
+            lo, hi = shard.range_of(rank, splitters)
+            outs = [shard.compact_dist(OracleShard(kv, rs, wm, True, lo, hi))]
+        else:  # R ranges per rank: one list through compact_dist
+            shards = [OracleShard(kv, rs, wm, True, *shard.range_of(rank * R + i, splitters)) for i in range(R)]
+            outs = shard.compact_dist(shards)
+        for i, res in enumerate(outs):
+            q.put((rank * R + i, res["blocks"], res["seg_start"].tolist(), res["nseg"], res["m"],
+                   res["first_continues"], res["carry_in"], res["carry_out"], splitters))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sharded_compaction_equals_single_stream(world):
+@pytest.mark.parametrize("world,R", [(2, 1), (3, 1), (2, 3)])
+def test_gloo_sharded_compaction_equals_single_stream(world, R):
     from oracle import oracle as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, R)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted((q.get(timeout=200) for _ in range(world)), key=lambda x: x[0])
+    res = sorted((q.get(timeout=200) for _ in range(world * R)), key=lambda x: x[0])
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    assert all(r[8] == res[0][8] and len(r[8]) == world - 1 for r in res)
+    assert all(r[8] == res[0][8] and len(r[8]) == world * R - 1 for r in res)
     kv, rs = global_input()
     src = O.merge_runs(kv, rs)
     want = O.compact(kv, src, int(kv.ts.max()) // 2, True, (), BS, TARGET)
