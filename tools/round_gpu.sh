@@ -10,7 +10,11 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -2 gpurun_out/tests_$TAG.log
 timeout -k 10 300 python3 bench.py --pcie > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -f csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || { echo "rocprof failed"; exit 1; }
+# the headline workload alone (the extras' kernels would mix into the per-kernel averages)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -f csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || { echo "rocprof failed"; exit 1; }
+for cfg in M C; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$cfg -o run -f csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/benchprof_${TAG}_$cfg.json 2> gpurun_out/benchprof_${TAG}_$cfg.err || { echo "rocprof $cfg failed"; exit 1; }
+done
 head -6 gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -d, -f1-4
 if [ "$1" != "--no-pmc" ]; then
   bash tools/traffic.sh gpurun_out/traffic_$TAG.json || exit 1
