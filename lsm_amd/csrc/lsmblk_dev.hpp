@@ -302,12 +302,13 @@ constexpr uint32_t kCrcSeg = 68;
 constexpr uint32_t kCrcMats = 7;  // Z(., kCrcSeg << j), j = 0..5, and j = 6: Z(., kCrcChunk)
 // crc_chunk reads up to kCrcPad bytes before a chunk, which must hold zeros
 constexpr uint32_t kCrcPad = 80;
-constexpr uint32_t kCrcStage = kCrcPad + 5 * 1024 + 16;  // zero pad, five 1-KiB load pieces (+3 shift)
+constexpr uint32_t kCrcStage = kCrcPad + 5 * 1024;  // zero pad, five 1-KiB load pieces
 struct alignas(16) CrcTabs {
   uint32_t fold[8][16];              // R_0 after xoring a dword into the register: by nibble
   uint32_t shift[kCrcMats][8][16];   // Z(., kCrcSeg << j), j < 6, Z(., kCrcChunk): by nibble
   uint32_t zinv[kCrcSeg];            // zinv[j]: the register that j zero bytes take to the init
   uint32_t unz[3][8][16];            // Z(., t)^-1, t = 1..3: undoes t appended zero bytes
+  uint32_t z32[8][16];               // Z(., 32): joins a window's two fold chains
 };
 
 // 4 * (byte B of v & 15 << 2 ...): (byte B of v) & 0x3C as one SDWA instruction
@@ -360,9 +361,16 @@ __device__ __forceinline__ uint32_t crc_chunk(const CrcTabs& T, const uint8_t* p
   uint32_t d[kCrcSeg / 4];
 #pragma unroll
   for (uint32_t i = 0; i < kCrcSeg / 4; ++i) d[i] = q[i];
-  uint32_t crc = first && l == l0 ? T.zinv[kCrcSeg - r] : 0u;
+  // two independent fold chains per lane (dwords 0..8 and 9..16, joined by Z(., 32)): the
+  // dependent LDS round trips per window drop from 17 to 10
+  uint32_t ca = first && l == l0 ? T.zinv[kCrcSeg - r] : 0u, cb = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < kCrcSeg / 4; ++i) crc = crc_apply(T.fold, crc ^ d[i]);
+  for (uint32_t i = 0; i < 8; ++i) {
+    ca = crc_apply(T.fold, ca ^ d[i]);
+    cb = crc_apply(T.fold, cb ^ d[9 + i]);
+  }
+  ca = crc_apply(T.fold, ca ^ d[8]);
+  uint32_t crc = crc_apply(T.z32, ca) ^ cb;
   const uint32_t m = 63 - l;  // full windows after this one
 #pragma unroll
   for (uint32_t j = 0; j < 6; ++j)
@@ -415,6 +423,12 @@ inline void crc_host_tables(CrcTabs& T) {
     col[bit] = x;
   }
   crc_nibble_tables(col, T.fold);
+  for (uint32_t bit = 0; bit < 32; ++bit) {  // Z(., 32): 256 bit steps
+    uint32_t x = 1u << bit;
+    for (uint32_t s = 0; s < 256; ++s) x = crc_bit_step(x);
+    col[bit] = x;
+  }
+  crc_nibble_tables(col, T.z32);
   for (uint32_t j = 0; j < kCrcMats; ++j) {  // Z(., n) = 8 n bit steps
     const uint32_t steps = 8u * (j < 6 ? kCrcSeg << j : kCrcChunk);
     for (uint32_t bit = 0; bit < 32; ++bit) {
