@@ -35,7 +35,8 @@ namespace {
 
 constexpr uint32_t kMS = 128;       // every kMS-th entry of a run is a merge candidate
 constexpr uint32_t kMaxRuns = 64;   // runs per merge (one lane per run in the tile kernels)
-constexpr uint32_t kMTE = 1024;     // tile entries with LDS tables (larger tiles: global path)
+constexpr uint32_t kMTE = 256;      // tile entries with LDS tables (larger tiles: global path); tiles
+                                   // average kMS entries, and 256 keeps 8 waves/SIMD resident (1024: 3)
 constexpr uint32_t kMTT = 128;      // threads per tile workgroup
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -954,19 +955,36 @@ __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
   or_need(a.need + 0, short_chain);
 }
 
+// kRotPer entries per thread (a block-stride apart, so each round stays coalesced): all their
+// loads are in flight together -- one entry per thread left the kernel latency-bound.
+constexpr uint32_t kRotPer = 4;
+
 __global__ __launch_bounds__(256) void rot_double_kernel(RotArgs a, uint32_t k) {
   if (!*(volatile uint32_t*)(a.need + k - 1)) return;  // every chain done one level down
   const uint64_t n = rot_n(a);
-  const uint64_t s = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t s0 = uint64_t(blockIdx.x) * 256 * kRotPer + threadIdx.x;
   const uint64_t N1 = a.n_max + 1;
+  const u32x2* L0 = a.JS + (k - 1) * N1;
   bool short_chain = false;
-  if (s <= n) {
-    const u32x2* L0 = a.JS + (k - 1) * N1;
-    const u32x2 v = L0[s];
-    const u32x2 w = L0[v.x];
-    const uint64_t ss = uint64_t(v.y) + w.y;
-    a.JS[k * N1 + s] = u32x2{w.x, ss > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(ss)};
-    short_chain = w.x < n && ss < a.target;
+  u32x2 v[kRotPer], w[kRotPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) {
+    const uint64_t s = s0 + 256 * i;
+    v[i] = s <= n ? L0[s] : u32x2{0u, 0u};
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) {
+    const uint64_t s = s0 + 256 * i;
+    w[i] = s <= n ? L0[v[i].x] : u32x2{0u, 0u};
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) {
+    const uint64_t s = s0 + 256 * i;
+    if (s <= n) {
+      const uint64_t ss = uint64_t(v[i].y) + w[i].y;
+      a.JS[k * N1 + s] = u32x2{w[i].x, ss > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(ss)};
+      short_chain = short_chain || (w[i].x < n && ss < a.target);
+    }
   }
   or_need(a.need + k, short_chain);
 }
@@ -1404,7 +1422,8 @@ int rotation_chains(const RotArgs& r, hipStream_t st) {
   const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
   hipLaunchKernelGGL(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
   hipLaunchKernelGGL(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
-  for (uint32_t k = 1; k < r.levels; ++k) hipLaunchKernelGGL(rot_double_kernel, dim3(g), dim3(256), 0, st, r, k);
+  const uint32_t gd = uint32_t((r.n_max + 1 + 256 * kRotPer - 1) / (256 * kRotPer));
+  for (uint32_t k = 1; k < r.levels; ++k) hipLaunchKernelGGL(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
   hipLaunchKernelGGL(rot_f_kernel, dim3(g), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
