@@ -686,28 +686,43 @@ __global__ __launch_bounds__(1024) void mscan_kernel(GatherArgs a) {
   }
 }
 
+// Pieces of a lane's 16-B copy loop whose loads are all issued before their stores: a
+// load -> store per piece waits out a full memory round trip every 16 bytes.
+constexpr uint32_t kCopyB = 8;
+
+// len (>= 16) bytes src -> dst by one lane as 16-B pieces (the last overlapping the one before),
+// kCopyB loads in flight at a time.  Dst is global or LDS (generic pointer).
+__device__ __forceinline__ void copy16_batched(uint8_t* dst, const uint8_t* src, uint32_t len) {
+  const uint32_t np = (len + 15) >> 4;
+  for (uint32_t b = 0; b < np; b += kCopyB) {
+    u32x4 v[kCopyB];
+#pragma unroll
+    for (uint32_t i = 0; i < kCopyB; ++i) {
+      const uint32_t p = min(16 * (b + i), len - 16);
+      if (b + i < np) v[i] = *reinterpret_cast<const u32x4*>(src + p);
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kCopyB; ++i) {
+      const uint32_t p = min(16 * (b + i), len - 16);
+      if (b + i < np) *reinterpret_cast<u32x4*>(dst + p) = v[i];
+    }
+  }
+}
+
 // len bytes src -> dst by one lane, any alignment: 16-B unaligned pieces, the last overlapping.
 __device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, uint32_t len) {
   if (len < 16) {
     for (uint32_t x = 0; x < len; ++x) dst[x] = src[x];
     return;
   }
-  for (uint32_t o = 0;; o += 16) {
-    const uint32_t p = o + 16 <= len ? o : len - 16;
-    *reinterpret_cast<u32x4*>(dst + p) = *reinterpret_cast<const u32x4*>(src + p);
-    if (p == len - 16) break;
-  }
+  copy16_batched(dst, src, len);
 }
 
 // len bytes from global src into the LDS image at dst (any alignment): 16-B pieces, the last
 // overlapping the one before; shorter runs by overlapping 8/4-byte or single-byte stores.
 __device__ __forceinline__ void lds_put(uint8_t* dst, const uint8_t* src, uint32_t len) {
   if (len >= 16) {
-    for (uint32_t o = 0;; o += 16) {
-      const uint32_t p = o + 16 <= len ? o : len - 16;
-      *reinterpret_cast<u32x4*>(dst + p) = *reinterpret_cast<const u32x4*>(src + p);
-      if (p == len - 16) break;
-    }
+    copy16_batched(dst, src, len);
   } else if (len >= 8) {
     *reinterpret_cast<u32x2*>(dst) = *reinterpret_cast<const u32x2*>(src);
     *reinterpret_cast<u32x2*>(dst + len - 8) = *reinterpret_cast<const u32x2*>(src + len - 8);
