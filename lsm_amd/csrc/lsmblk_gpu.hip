@@ -350,7 +350,10 @@ __device__ __forceinline__ void copy_run(const rsrc_t& RS, uint32_t so, uint32_t
 // The same copy by the whole wave (len >= 16, wave-uniform arguments): lane j moves pieces
 // j, j + 64, ... so a wave instruction moves 1 KiB of contiguous bytes.  Values of
 // kCoop bytes or more go this way: one long value no longer keeps 63 lanes idle.
-constexpr uint32_t kCoop = 256;
+#ifndef LSMBLK_COOP
+#define LSMBLK_COOP 16  // M: 799 / 830-846 / 840 GiB/s at 256 / 32 / 16 (every run of 16 B or more packed)
+#endif
+constexpr uint32_t kCoop = LSMBLK_COOP;
 __device__ __forceinline__ void copy_run_wave(const rsrc_t& RS, uint32_t so, const rsrc_t& RD, uint32_t dof,
                                               uint32_t len) {
   const uint32_t l = lane_id();
@@ -373,13 +376,51 @@ __device__ __forceinline__ void copy_run_wave(const rsrc_t& RS, uint32_t so, con
   }
 }
 
-// Copies of every lane's run of kCoop bytes or more, one after another by the whole wave.
+// Copies of every lane's run of kCoop bytes or more by the whole wave, packed: the runs' 16-B
+// pieces are numbered consecutively over the lanes (wave scan of the piece counts) and each
+// lane moves pieces lane, lane + 64, ... of that numbering, kBigB loads in flight per lane --
+// so a wave round trip moves 8 KiB whatever the run lengths.  (One run after another cost a
+// round trip per run: ~46 per 64 KiB block of config M.)  A piece finds its run by a binary
+// search over the lanes' first-piece numbers (ds_bpermute); a run's last piece overlaps the one
+// before, so any length >= 16 is covered exactly.
 __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, uint32_t so, const rsrc_t& RD,
                                                uint32_t dof, uint32_t len) {
-  for (uint64_t m = __ballot(longrun); m; m &= m - 1) {
-    const uint32_t j = uint32_t(__builtin_ctzll(m));
-    copy_run_wave(RS, __builtin_amdgcn_readlane(so, j), RD, __builtin_amdgcn_readlane(dof, j),
-                  __builtin_amdgcn_readlane(len, j));
+  const uint32_t l = lane_id();
+  const uint32_t np = longrun ? (len + 15) >> 4 : 0u;
+  const uint32_t incl = wave_incl_scan32(np);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  const uint32_t first = incl - np;  // this lane's first piece number
+  for (uint32_t g0 = 0; g0 < total; g0 += 64 * kBigB) {
+    u32x4 q[kBigB];
+    uint32_t dst[kBigB];
+#pragma unroll
+    for (uint32_t j = 0; j < kBigB; ++j) {
+      const uint32_t g = g0 + 64 * j + l, gg = min(g, total - 1);
+      // owner: the last lane whose first piece number is <= g (a lane after the owner starts
+      // past g; lanes before it without pieces share its number but are not the last).  The
+      // search and the owner reads run on every lane: ds_bpermute reads nothing from a lane
+      // that is masked off, and the owner may be one whose own piece slot is past the end.
+      uint32_t lo = 0;
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1) {
+        const uint32_t f = uint32_t(__shfl(first, int((lo + step) & 63), 64));
+        if (lo + step < 64 && f <= gg) lo += step;
+      }
+      const uint32_t o_so = uint32_t(__shfl(so, int(lo), 64)), o_dof = uint32_t(__shfl(dof, int(lo), 64));
+      const uint32_t o_len = uint32_t(__shfl(len, int(lo), 64)), o_first = uint32_t(__shfl(first, int(lo), 64));
+      const uint32_t off = min(16 * (gg - o_first), o_len - 16);
+      dst[j] = ~0u;
+      if (g < total) {
+        q[j] = gload16(RS, o_so + off);
+        dst[j] = o_dof + off;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kBigB; ++j)
+      if (dst[j] != ~0u) {
+        const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+        st16(RD, dst[j], v);
+      }
   }
 }
 
