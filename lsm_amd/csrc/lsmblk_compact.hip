@@ -709,6 +709,44 @@ __device__ __forceinline__ void copy16_batched(uint8_t* dst, const uint8_t* src,
   }
 }
 
+// Every lane's run [so, so + len) of sbase -> [dof, dof + len) of dbase (len >= 16 where
+// `mine`; any alignment; dbase global or LDS) by the whole wave, packed: the runs' 16-B pieces
+// are numbered over the lanes and lane l moves pieces l, l + 64, ..., kCopyB loads in flight,
+// so neighbouring lanes read neighbouring pieces of one run.  Called by every lane of the wave.
+__device__ __forceinline__ void wave_copy_packed(bool mine, const uint8_t* sbase, uint32_t so, uint8_t* dbase,
+                                                 uint32_t dof, uint32_t len) {
+  const uint32_t l = lane_id();
+  const uint32_t np = mine ? (len + 15) >> 4 : 0u;
+  const uint32_t incl = wave_incl_scan32(np);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  const uint32_t first = incl - np;
+  for (uint32_t g0 = 0; g0 < total; g0 += 64 * kCopyB) {
+    u32x4 v[kCopyB];
+    uint32_t d[kCopyB];
+#pragma unroll
+    for (uint32_t j = 0; j < kCopyB; ++j) {
+      const uint32_t g = g0 + 64 * j + l, gg = min(g, total - 1);
+      uint32_t lo = 0;  // owner: the last lane whose first piece number is <= gg
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1) {
+        const uint32_t f = uint32_t(__shfl(first, int((lo + step) & 63), 64));
+        if (lo + step < 64 && f <= gg) lo += step;
+      }
+      const uint32_t o_so = uint32_t(__shfl(so, int(lo), 64)), o_dof = uint32_t(__shfl(dof, int(lo), 64));
+      const uint32_t o_len = uint32_t(__shfl(len, int(lo), 64)), o_first = uint32_t(__shfl(first, int(lo), 64));
+      const uint32_t off = min(16 * (gg - o_first), o_len - 16);
+      d[j] = ~0u;
+      if (g < total) {
+        v[j] = *reinterpret_cast<const u32x4*>(sbase + o_so + off);
+        d[j] = o_dof + off;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kCopyB; ++j)
+      if (d[j] != ~0u) *reinterpret_cast<u32x4*>(dbase + d[j]) = v[j];
+  }
+}
+
 // len bytes src -> dst by one lane, any alignment: 16-B unaligned pieces, the last overlapping.
 __device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, uint32_t len) {
   if (len < 16) {
@@ -788,10 +826,13 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
     const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
     const bool staged = K1 - K0 + kb <= kGKImg && V1 - V0 + vb <= kGVImg;
     if (staged) {
-      if (k) {
-        lds_put(kimg + kb + (ko - K0), a.keys + a.key_off[i], kl);
-        lds_put(vimg + vb + (vo - V0), a.vals + a.val_off[i], vl);
-      }
+      // runs of 16 B or more by the whole wave, packed; shorter ones lane by lane
+      const uint32_t kso = k ? a.key_off[i] : 0u, vso = k ? a.val_off[i] : 0u;
+      const uint32_t kd = kb + uint32_t(ko - K0), vd = vb + uint32_t(vo - V0);
+      if (k && kl < 16) lds_put(kimg + kd, a.keys + kso, kl);
+      if (k && vl < 16) lds_put(vimg + vd, a.vals + vso, vl);
+      wave_copy_packed(k && kl >= 16, a.keys, kso, kimg, kd, kl);
+      wave_copy_packed(k && vl >= 16, a.vals, vso, vimg, vd, vl);
       __syncthreads();
       flush_img(a.okeys + (K0 - kb), kimg, kb, uint32_t(K1 - K0));
       flush_img(a.ovals + (V0 - vb), vimg, vb, uint32_t(V1 - V0));
