@@ -1114,19 +1114,36 @@ __device__ __forceinline__ uint64_t key_change_after(const RotArgs& a, uint64_t 
   return f;
 }
 
+// Two entries per thread, lifted in lockstep (their gathers in flight together): the lifting
+// is a chain of ~levels dependent gathers per entry.
 __global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
   const uint64_t n = rot_n(a);
-  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (g > n) return;
-  if (g == n) {
-    a.F0[g] = uint32_t(n);
-    return;
-  }
-  uint64_t acc = 0;
+  const uint64_t g0 = uint64_t(blockIdx.x) * 512 + threadIdx.x, g1 = g0 + 256;
+  const uint32_t top = rot_top(a);
+  const uint64_t N1 = a.n_max + 1;
   // lifting: the longest chain prefix from g whose data stays below the target
-  const uint64_t pos = lift_target(a, g, acc, n, rot_top(a));
+  uint64_t p0 = g0, p1 = g1, c0 = 0, c1 = 0;
+  for (;;) {  // top level, repeated while it fits
+    bool m0 = false, m1 = false;
+    u32x2 v0{0u, 0u}, v1{0u, 0u};
+    if (p0 < n) v0 = a.JS[top * N1 + p0];
+    if (p1 < n) v1 = a.JS[top * N1 + p1];
+    if (p0 < n && c0 + v0.y < a.target) c0 += v0.y, p0 = v0.x, m0 = true;
+    if (p1 < n && c1 + v1.y < a.target) c1 += v1.y, p1 = v1.x, m1 = true;
+    if (!m0 && !m1) break;
+  }
+  for (int k = int(top) - 1; k >= 0; --k) {
+    u32x2 v0{0u, 0u}, v1{0u, 0u};
+    if (p0 < n) v0 = a.JS[uint64_t(k) * N1 + p0];
+    if (p1 < n) v1 = a.JS[uint64_t(k) * N1 + p1];
+    if (p0 < n && c0 + v0.y < a.target) c0 += v0.y, p0 = v0.x;
+    if (p1 < n && c1 + v1.y < a.target) c1 += v1.y, p1 = v1.x;
+  }
   // s_{j*}: the first block start whose entries see D >= target
-  a.F0[g] = uint32_t(pos < n ? key_change_after(a, a.JS[pos].x, n) : n);
+  if (g0 < n) a.F0[g0] = uint32_t(p0 < n ? key_change_after(a, a.JS[p0].x, n) : n);
+  else if (g0 == n) a.F0[g0] = uint32_t(n);
+  if (g1 < n) a.F0[g1] = uint32_t(p1 < n ? key_change_after(a, a.JS[p1].x, n) : n);
+  else if (g1 == n) a.F0[g1] = uint32_t(n);
 }
 
 // ---------------------------------------------------------------- key-range shard rotation
@@ -1489,7 +1506,7 @@ int rotation_chains(const RotArgs& r, hipStream_t st) {
   hipLaunchKernelGGL(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
   const uint32_t gd = uint32_t((r.n_max + 1 + 256 * kRotPer - 1) / (256 * kRotPer));
   for (uint32_t k = 1; k < r.levels; ++k) hipLaunchKernelGGL(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
-  hipLaunchKernelGGL(rot_f_kernel, dim3(g), dim3(256), 0, st, r);
+  hipLaunchKernelGGL(rot_f_kernel, dim3(uint32_t((r.n_max + 1 + 511) / 512)), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
