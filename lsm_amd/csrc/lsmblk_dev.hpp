@@ -263,10 +263,17 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x
 // Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
 // store when whole, else conditional whole-dword stores plus at most three bytes at each
 // end (closed-form; a wave pays ~10 stores for its partial lanes, not 16 byte stores).
+#ifndef LSMBLK_NT_STORE
+#define LSMBLK_NT_STORE 1  // U: 735 vs 722 GiB/s (nt loads: no gain)
+#endif
 __device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t lo, uint32_t hi) {
   if (lo == 0 && hi == 16) {
     u32x4 q = {v[0], v[1], v[2], v[3]};
+#if LSMBLK_NT_STORE
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(dst));  // streamed: written once, read by a later pass
+#else
     *reinterpret_cast<u32x4*>(dst) = q;
+#endif
     return;
   }
   const uint32_t lo4 = (lo + 3) >> 2, hi4 = hi >> 2;  // whole dwords [lo4, hi4)

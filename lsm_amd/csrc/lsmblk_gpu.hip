@@ -77,6 +77,12 @@ __device__ __forceinline__ void lds_read16(const uint8_t* base, uint32_t x, uint
   v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
 }
 
+// cache policy of the staging loads (2 = nt: each byte is read once); timing experiments
+#ifndef LSMBLK_NT_LOAD
+#define LSMBLK_NT_LOAD 0
+#endif
+constexpr int kLdAux = LSMBLK_NT_LOAD ? 2 : 0;
+
 struct BlockHdr {
   uint32_t len, n, data_end, fks;
   bool ok;
@@ -520,7 +526,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
     u32x4 v[5];
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, 0);
+      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
       if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
@@ -1253,10 +1259,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint32_t nv = (vlead + (m.vb1 - m.vb0) + 15) >> 4;
 #pragma unroll
     for (uint32_t i = 0; i < 2; ++i)
-      if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, 0);
+      if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, kLdAux);
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, 0);
+      if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, kLdAux);
     if (l < m.n) {
       pf_ko0 = a.key_off[m.s + l];
       pf_ko1 = a.key_off[m.s + l + 1];
