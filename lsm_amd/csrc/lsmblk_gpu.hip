@@ -50,16 +50,30 @@ struct DecodeArgs {
 
 constexpr uint32_t kTile = 64;  // blocks per count tile
 
-constexpr uint32_t kDecImg = 4352;  // staged block bytes per wave (4 KiB blocks + lead + slack)
-constexpr uint32_t kDecMaxE = 128;  // entries with LDS tables (fast path)
-constexpr uint32_t kDecOut = 4096;  // LDS output image (keys + values) of a fast-path block
-
+// LDS per single-wave workgroup is exactly 8 KiB, so 20 blocks are resident per CU (5 waves per
+// SIMD; 10.3 KiB gave 15).  A 4 KiB block (up to 4098 B: the builder overshoots by 2) at any
+// 16-B lead, plus the 16-B staging round-up, fits the image.
+constexpr uint32_t kDecImg = 4128;  // staged block bytes per wave
+constexpr uint32_t kDecMaxE = 128;  // entries of a fast-path block (tables in registers, 2 per lane)
+constexpr uint32_t kDecOut = 4064;  // LDS output image (keys + values) of a fast-path block
 
 struct alignas(16) DecLds {
   uint8_t img[kDecImg];
-  uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE], vsrc[kDecMaxE];
-  uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
   alignas(16) uint8_t out[kDecOut];  // decoded key run, then (16-B aligned) value run
+};
+static_assert(sizeof(DecLds) == 8192, "decode LDS: 20 single-wave workgroups per CU");
+
+// Entry tables of a large block (kDecMaxE entries at a time).  A large block is not staged, so
+// the tables live in the unused image.
+struct DecTables {
+  uint16_t epos[kDecMaxE], pfx[kDecMaxE], sfx[kDecMaxE];
+  uint32_t kout[kDecMaxE + 1], vout[kDecMaxE + 1];
+};
+static_assert(sizeof(DecTables) <= kDecImg, "large-block tables overlay the image");
+
+// One fast-path entry, held by its lane in registers (entries l and l + 64 of the block).
+struct DecEnt {
+  uint32_t epos, p, s, kout, vout, vl;
 };
 
 // 16 bytes at LDS byte offset x (any alignment) via three 8-B reads: ds_read_b64 at a 16-B
@@ -220,14 +234,17 @@ struct LdsSink {
 // entries abut and no lane needs a chunk -> entry search.
 template <class Sink>
 __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, uint32_t lead, uint32_t n,
-                                               uint64_t E0, uint64_t K0, uint64_t V0, const Sink& out,
-                                               uint32_t skip) {
+                                               const DecEnt (&ent)[2], uint64_t E0, uint64_t K0, uint64_t V0,
+                                               const Sink& out, uint32_t skip) {
   const uint32_t l = lane_id();
   const uint8_t* img = L.img;
   const uint32_t fk = lead + 4;  // image byte of the first key
-  for (uint32_t k = l; k < n; k += 64) {
-    const uint32_t epos = L.epos[k], p = L.pfx[k], s = L.sfx[k];
-    const uint32_t kout = L.kout[k], vout = L.vout[k], vl = L.vout[k + 1] - vout;
+#pragma unroll
+  for (uint32_t it = 0; it < 2; ++it) {
+    const uint32_t k = 64 * it + l;
+    if (k >= n) continue;
+    const uint32_t epos = ent[it].epos, p = ent[it].p, s = ent[it].s;
+    const uint32_t kout = ent[it].kout, vout = ent[it].vout, vl = ent[it].vl;
     const uint32_t sb = lead + epos + 4;  // image byte of the suffix
     if (!(skip & 8)) {
       const uint64_t e = E0 + k;
@@ -296,17 +313,19 @@ __device__ __forceinline__ void flush_run(uint8_t* gdst_aligned, const uint8_t* 
 }
 
 __device__ void dec_fast_outputs(const DecodeArgs& a, DecLds& L, uint32_t lead, const BlockHdr& h,
-                                 uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K, uint32_t V, uint32_t skip) {
+                                 const DecEnt (&ent)[2], uint64_t E0, uint64_t K0, uint64_t V0, uint32_t K,
+                                 uint32_t V, uint32_t skip) {
   const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
   const uint32_t vrun = (kb + K + 15) & ~15u;  // LDS start of the value run's first chunk
-  if (vrun + vb + V + 16 <= kDecOut) {
-    dec_entry_runs(a, L, lead, h.n, E0, K0, V0, LdsSink{L.out, kb, vrun + vb}, skip);
+  // the flush reads whole 16-B chunks: the value run's last chunk must lie in the image
+  if (vrun + ((vb + V + 15) & ~15u) <= kDecOut) {
+    dec_entry_runs(a, L, lead, h.n, ent, E0, K0, V0, LdsSink{L.out, kb, vrun + vb}, skip);
     wave_sync();
     flush_run(a.keys + (K0 - kb), L.out, kb, K);
     flush_run(a.vals + (V0 - vb), L.out + vrun, vb, V);
   } else {
     const GlbSink g{make_rsrc_exact(a.keys + (K0 - kb), kb + K), make_rsrc_exact(a.vals + (V0 - vb), vb + V), kb, vb};
-    dec_entry_runs(a, L, lead, h.n, E0, K0, V0, g, skip);
+    dec_entry_runs(a, L, lead, h.n, ent, E0, K0, V0, g, skip);
   }
 }
 
@@ -433,7 +452,7 @@ __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, u
 // One entry of a large block: ts / key_off / val_off, and the key (first-key bytes below p,
 // suffix bytes from there on, one 16-B load of each source per piece, merged under byte
 // masks; byte loads where a piece would read past the block end).
-__device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecLds& L, const GlbImg& im, uint32_t k,
+__device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecTables& L, const GlbImg& im, uint32_t k,
                                               uint32_t lim, const rsrc_t& RK, uint32_t kb, uint64_t E0, uint64_t K0,
                                               uint64_t V0) {
   const rsrc_t& R = im.r;
@@ -473,7 +492,7 @@ __device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecLds&
 }
 
 // Outputs of the n entries whose tables are in L (block entries Eb - E0 .. + n), large block.
-__device__ void dec_big_outputs(const DecodeArgs& a, const DecLds& L, const rsrc_t& R, uint32_t lead,
+__device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const rsrc_t& R, uint32_t lead,
                                 const BlockHdr& h, uint32_t n, uint64_t Eb, uint64_t K0, uint64_t V0, uint32_t K,
                                 uint32_t V) {
   const uint32_t l = lane_id();
@@ -517,7 +536,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
   const uint8_t* abase = bp - lead;
   const rsrc_t R = make_rsrc(abase, lead + len);
-  const bool fits = lead + len + 16 <= kDecImg;
+  const bool fits = lead + len + 15 <= kDecImg;  // the staging writes whole 16-B chunks
 
   BlockHdr h;
   if (fits) {
@@ -545,6 +564,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   // phase 1: parse entries, block aggregates (entries, key bytes, value bytes)
   uint64_t K = 0, V = 0;
   bool bad = false;
+  DecTables& T = *reinterpret_cast<DecTables*>(L.img);  // large blocks only (not staged)
   // tables of entries [c0, c0 + cn) (cn <= kDecMaxE) at table rows 0 .. cn, output offsets
   // from the block's key / value bytes before c0 (kr, vr)
   auto parse_tables = [&](const auto& im, uint32_t c0, uint32_t cn, uint64_t& kr, uint64_t& vr) {
@@ -557,23 +577,37 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
       const uint32_t kl = p + s;
       const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
       if (k < cn) {
-        L.epos[k] = uint16_t(off);
-        L.pfx[k] = uint16_t(p);
-        L.sfx[k] = uint16_t(s);
-        L.vsrc[k] = uint16_t(off + 14 + s);
-        L.kout[k] = uint32_t(kr) + ki - kl;
-        L.vout[k] = uint32_t(vr) + vi - vl;
+        T.epos[k] = uint16_t(off);
+        T.pfx[k] = uint16_t(p);
+        T.sfx[k] = uint16_t(s);
+        T.kout[k] = uint32_t(kr) + ki - kl;
+        T.vout[k] = uint32_t(vr) + vi - vl;
       }
       kr += __shfl(ki, 63, 64);
       vr += __shfl(vi, 63, 64);
     }
     if (l == 0) {
-      L.kout[cn] = uint32_t(kr);
-      L.vout[cn] = uint32_t(vr);
+      T.kout[cn] = uint32_t(kr);
+      T.vout[cn] = uint32_t(vr);
     }
   };
-  if (fast) {
-    parse_tables(LdsImg{L.img, lead}, 0, h.n, K, V);
+  DecEnt ent[2] = {};
+  if (fast) {  // entries l and l + 64 stay in this lane's registers
+    const LdsImg im{L.img, lead};
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+      if (64 * it >= h.n) break;
+      const uint32_t k = 64 * it + l;
+      uint32_t off = 0, p = 0, s = 0, vl = 0;
+      bool ok = true;
+      if (k < h.n) ok = parse_entry(im, h, k, off, p, s, vl);
+      bad = bad || !ok;
+      const uint32_t kl = p + s;
+      const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
+      ent[it] = DecEnt{off, p, s, uint32_t(K) + ki - kl, uint32_t(V) + vi - vl, vl};
+      K += __shfl(ki, 63, 64);
+      V += __shfl(vi, 63, 64);
+    }
   } else if (big && h.n <= kDecMaxE) {
     parse_tables(GlbImg{R, lead}, 0, h.n, K, V);
   } else {
@@ -609,9 +643,9 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
 
   if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
     if (fast) {
-      dec_fast_outputs(a, L, lead, h, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
+      dec_fast_outputs(a, L, lead, h, ent, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
     } else if (big && h.n <= kDecMaxE) {
-      dec_big_outputs(a, L, R, lead, h, h.n, E0, K0, V0, uint32_t(K), uint32_t(V));
+      dec_big_outputs(a, T, R, lead, h, h.n, E0, K0, V0, uint32_t(K), uint32_t(V));
     } else if (big) {
       uint64_t kr = 0, vr = 0;
       for (uint32_t c0 = 0; c0 < h.n; c0 += kDecMaxE) {
@@ -619,7 +653,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
         wave_sync();  // the previous chunk's table reads are done
         parse_tables(GlbImg{R, lead}, c0, cn, kr, vr);
         wave_sync();
-        dec_big_outputs(a, L, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V));
+        dec_big_outputs(a, T, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V));
       }
     } else if (fits) {
       dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
