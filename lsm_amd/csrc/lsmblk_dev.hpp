@@ -255,9 +255,7 @@ struct GlbImg {
 
 // 4 bytes starting at byte offset x of a 4-byte-aligned LDS buffer.
 __device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
-  const uint32_t i = x >> 2;
-  return __builtin_amdgcn_alignbyte(w[i + 1], w[i], x & 3);
+  return *reinterpret_cast<const uint32_t*>(base + x);  // unaligned ds_read_b32
 }
 
 // Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128

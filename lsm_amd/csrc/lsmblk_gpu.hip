@@ -76,19 +76,11 @@ struct DecEnt {
   uint32_t epos, p, s, kout, vout, vl;
 };
 
-// 16 bytes at LDS byte offset x (any alignment) via three 8-B reads: ds_read_b64 at a 16-B
-// lane stride is bank-conflict free, ds_read_b32 at that stride is a 4-way conflict.
+// 16 bytes at LDS byte offset x (any alignment): one unaligned ds_read_b128 (the gfx9 unaligned
+// access mode).  Three aligned ds_read_b64 + four v_alignbyte (round 1) cost emit 4 % more time.
 __device__ __forceinline__ void lds_read16(const uint8_t* base, uint32_t x, uint32_t (&v)[4]) {
-  const uint2* q = reinterpret_cast<const uint2*>(base + (x & ~7u));
-  const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
-  const uint32_t sh = x & 3;
-  const bool hi = (x & 4) != 0;
-  const uint32_t w0 = hi ? q0.y : q0.x, w1 = hi ? q1.x : q0.y, w2 = hi ? q1.y : q1.x;
-  const uint32_t w3 = hi ? q2.x : q1.y, w4 = hi ? q2.y : q2.x;
-  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
-  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+  const u32x4 q = *reinterpret_cast<const u32x4*>(base + x);
+  v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
 }
 
 // cache policy of the staging loads (2 = nt: each byte is read once); timing experiments
