@@ -48,7 +48,9 @@ __device__ __forceinline__ void wave_sync() {
 }
 // Wave64 inclusive scan / sum of u32 with DPP (row_shr 1,2,4,8 then row_bcast 15 / 31):
 // pure VALU, no ds_bpermute traffic through the LDS crossbar.
-#define LSM_DPP(v, ctrl, rmask) __builtin_amdgcn_update_dpp(0u, (v), (ctrl), (rmask), 0xF, false)
+// (the builtin returns int: without the cast, max(uint32_t, int) resolves to the double overload
+// and every max-scan step became two v_cvt_f64 + v_max_f64)
+#define LSM_DPP(v, ctrl, rmask) uint32_t(__builtin_amdgcn_update_dpp(0u, (v), (ctrl), (rmask), 0xF, false))
 __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
   v += LSM_DPP(v, 0x111, 0xF);  // row_shr:1
   v += LSM_DPP(v, 0x112, 0xF);  // row_shr:2

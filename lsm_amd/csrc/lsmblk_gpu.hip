@@ -1298,19 +1298,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     }
   };
 
-  uint64_t bi0 = uint64_t(blockIdx.x) * kEmitWaves + wave_id();
-  if (bi0 >= lim) {
+  // The wave's next block on the fast path from bi on: blocks beyond the LDS image are flagged
+  // for emit_big_kernel on the way (rare, so their dependent metadata loads are not hidden).
+  // The prefetch of a fast block is issued in exactly two places (before the loop, and after
+  // phase 1 for the next block): a third issue site in the loop (the flagged-block path used
+  // to have one) gave the prefetch registers a second register assignment, and the waitcnt
+  // pass then drained every load in flight (vmcnt(0)) inside the chunk move of each block.
+  auto find_fast = [&](uint64_t bi, EmitMeta& m) -> bool {
+    for (; bi < lim; bi += nwaves) {
+      meta1(bi, m);
+      meta2(m);
+      if (is_fast(m)) return true;
+      if (l == 0) a.big_flag[bi] = 1;
+    }
+    return false;
+  };
+  EmitMeta cur;
+  if (!find_fast(uni64(uint64_t(blockIdx.x) * kEmitWaves + wave_id()), cur)) {
     raise_err(a.stats, err);
     return;
   }
-  EmitMeta cur;
-  meta1(uni64(bi0), cur);
-  meta2(cur);
-  bool cur_fast = is_fast(cur);
-  if (cur_fast) issue(cur);
+  issue(cur);
   for (;;) {
     const uint64_t bn = cur.bi + nwaves;
-    const bool has_next = bn < lim;
+    bool has_next = bn < lim;
     EmitMeta nxt;
     if (has_next) meta1(bn, nxt);  // level-1 of the next block (scalar loads)
     const uint32_t s = cur.s, n = cur.n;
@@ -1318,17 +1329,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint32_t kb0 = cur.kb0, kb1 = cur.kb1, vb0 = cur.vb0, vb1 = cur.vb1;
     const uint32_t klead = uint32_t((kaddr + kb0) & 15), vlead = uint32_t((vaddr + vb0) & 15);
     const uint32_t olead = uint32_t(O & 15);
-    bool nxt_fast = false;
-    if (!cur_fast) {  // handed to emit_big_kernel (its registers stay out of this loop)
-      if (l == 0) a.big_flag[cur.bi] = 1;
-      if (!has_next) break;
-      meta2(nxt);
-      nxt_fast = is_fast(nxt);
-      if (nxt_fast) issue(nxt);
-      cur = nxt;
-      cur_fast = nxt_fast;
-      continue;
-    }
+    // first key length at kimg[klead]: made uniform before the next block's level-2 loads are
+    // issued (read after them, its wait would also cover the first of them: vmcnt is in order)
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf_ko1) - kb0;
     {  // land the staged keys (plain) and values (swizzled block image at vlead)
       const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
       const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
@@ -1339,6 +1342,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       for (uint32_t i = 0; i < 5; ++i)
         if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = vq[i];
     }
+    // Every prefetched register has landed: say so to the waitcnt pass, whose own waits in the
+    // exec-skippable landing stores do not cover all paths -- it would otherwise wait for
+    // vmcnt(0) at the first use of a prefetched entry register in phase 1, i.e. for the
+    // level-2 loads below as well.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
     // level-2 of the next block: loaded now into VGPRs, made uniform after phase 1 (a
     // readfirstlane here would stall on the loads' round trip)
     uint32_t r_kb0 = 0, r_kb1 = 0, r_vb0 = 0, r_vb1 = 0;
@@ -1353,7 +1361,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // Phase 1, entry lanes: LCP against the first key, record positions (wave scan), tables,
     // and the value bytes of each value's two partial edge chunks (captured in registers: the
     // in-place move below overwrites the staged values).
-    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf_ko1) - kb0;  // first key at kimg[klead]
     const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
     for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
     uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
@@ -1430,13 +1437,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     }
     const uint32_t data_len = dc;
     if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
+    // the level-2 loads have landed on every path (on the !has_next path there were none):
+    // without this the waitcnt pass keeps them pending past the branch below and waits for
+    // the next block's whole prefetch before the chunk moves reuse their registers
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
     if (has_next) {  // next block's staging loads overlap the rest of this block
       nxt.kb0 = uni(r_kb0);
       nxt.kb1 = uni(r_kb1);
       nxt.vb0 = uni(r_vb0);
       nxt.vb1 = uni(r_vb1);
-      nxt_fast = is_fast(nxt);
-      if (nxt_fast) issue(nxt);
+      if (!is_fast(nxt)) {
+        if (l == 0) a.big_flag[nxt.bi] = 1;
+        has_next = find_fast(nxt.bi + nwaves, nxt);
+      }
+      if (has_next) issue(nxt);
     }
     wave_sync();
     // Phase 2a (ascending): image chunk -> source byte of a chunk lying wholly inside one
@@ -1528,7 +1542,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     wave_sync();
     if (!has_next) break;
     cur = nxt;
-    cur_fast = nxt_fast;
   }
   raise_err(a.stats, err);
 }
