@@ -809,6 +809,72 @@ __global__ __launch_bounds__(256) void dec_count_kernel(CountArgs a) {
                                          red[3][threadIdx.x];
 }
 
+// Count pass, staged form: one single-wave workgroup per block streams the whole block into LDS
+// with coalesced 16-B loads (4 KiB of LDS: up to 32 waves per CU) and parses every header there
+// with decode's own rules (parse_hdr / parse_entry).  Reading all of E in full lines costs less
+// than the byte loads of the header-only parse above: those touch a 64-B sector per entry, which
+// at U's 128-B entries is most of E anyway, in scattered requests.  Blocks over the image parse
+// from global memory.  Tile sums: agg_tile_kernel.
+#ifndef LSMBLK_COUNT_STAGED
+#define LSMBLK_COUNT_STAGED 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dec_count_staged_kernel(CountArgs a) {
+  __shared__ alignas(16) uint8_t img[kDecImg];
+  const uint64_t b = blockIdx.x;
+  const uint32_t l = lane_id();
+  const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
+  bool ok = !(end < start + a.tail || end - start > 0x7FFFFFF0ull);
+  const uint32_t len = ok ? uint32_t(end - start) - a.tail : 0u;
+  const uint8_t* bp = a.blocks + start;
+  const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
+  const rsrc_t R = make_rsrc(bp - lead, lead + len);
+  uint64_t K = 0, V = 0;
+  uint32_t n = 0;
+  bool bad = false;
+  auto count = [&](const auto& im) {
+    const BlockHdr h = parse_hdr(im, len);
+    if (!h.ok) {
+      bad = true;
+      return;
+    }
+    n = h.n;
+    for (uint32_t c = 0; c < h.n; c += 64) {
+      const uint32_t k = c + l;
+      uint32_t off = 0, p = 0, s = 0, vl = 0;
+      if (k < h.n && !parse_entry(im, h, k, off, p, s, vl)) bad = true;
+      K += wave_sum<uint32_t>(p + s);
+      V += wave_sum<uint32_t>(vl);
+    }
+  };
+  if (ok && lead + len + 15 <= kDecImg) {
+    const uint32_t nchunk = (lead + len + 15) >> 4;
+    u32x4 v[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(img + (l + 64 * i) * 16) = v[i];
+    wave_sync();
+    count(LdsImg{img, lead});
+  } else if (ok) {
+    count(GlbImg{R, lead});
+  }
+  uint32_t err = 0;
+  if (!ok || __ballot(bad)) {
+    err |= LSMBLK_ERR_MALFORMED;
+    n = 0;
+    K = V = 0;
+  }
+  if (l == 0) {
+    a.agg[3 * b] = n;
+    a.agg[3 * b + 1] = uint32_t(K > 0xFFFFFFFFull ? 0xFFFFFFFFull : K);
+    a.agg[3 * b + 2] = uint32_t(V > 0xFFFFFFFFull ? 0xFFFFFFFFull : V);
+    if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+  }
+  raise_err(a.stats, err);
+}
+
 // ---------------------------------------------------------------- decode pass 2: tile scan
 // One workgroup: exclusive scan of the per-tile sums; totals, capacity / overflow checks and
 // the key_off[N] / val_off[N] sentinels.
@@ -2538,7 +2604,13 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     ca.tile_sum = c->tile_sum;
     ca.stats = stats;
     ca.tail = tail;
-    hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
+    if (LSMBLK_COUNT_STAGED && nblk <= 0x7FFFFFFFull) {
+      hipLaunchKernelGGL(dec_count_staged_kernel, dim3(uint32_t(nblk)), dim3(64), 0, st, ca);
+      hipLaunchKernelGGL(agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), 0, st, c->dec_agg, nblk,
+                         c->tile_sum);
+    } else {
+      hipLaunchKernelGGL(dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, ca);
+    }
   }
   if (c->timing) (void)hipEventRecord(c->ev[1], st);
   ScanArgs sa;
