@@ -1056,6 +1056,9 @@ __global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a0) {
 }
 
 constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
+#ifndef PLAN_TWO_BLOCKS
+#define PLAN_TWO_BLOCKS 1  // two blocks per window step when the second fits the window
+#endif
 
 __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
@@ -1148,7 +1151,34 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
         }
         ++nb;
         bytes += size;
+        const uint32_t len1 = j0 + f - s;  // entries of the block just found
         s = j0 + f;
+        // The next block from entry s, on the same window's lanes f..63 (the window held no
+        // out-of-order pair, or direct would be set): a U block of ~31 entries usually ends
+        // among them, so one window step finds two blocks.  LCP with entry s = min of alcp over
+        // (f, e]: lanes <= f read the min identity; growth and estimated_size restart at s.
+        // Tried only when the lanes left are more than the block just found took (Z's ~35-entry
+        // blocks seldom fit the rest of the window: there the second scan is wasted work).
+        if (PLAN_TWO_BLOCKS && !direct && s < s1 && 64 - f > len1) {
+          const uint32_t mn = wave_incl_min31(l <= f ? kAlcpLcp : (al & kAlcpLcp));  // all lanes (DPP)
+          const uint32_t p2 = l <= f ? 0u : mn;
+          const uint32_t g2 = (valid && l >= f) ? r + 16 - p2 : 0u;
+          if (__ballot(g2 >= (1u << 25)) == 0) {
+            const uint32_t before2 = 2 + wave_incl_scan32(g2) - g2;
+            const uint64_t m2 = __ballot(l > f && (!valid || uint64_t(before2) + r + 14 > bs));
+            if (m2) {
+              const uint32_t f2 = uint32_t(__builtin_ctzll(m2));
+              const uint32_t size2 = uint32_t(__builtin_amdgcn_readlane(before2, f2));
+              if (l == 0) {
+                a.rec_first[s0 + nb] = s;
+                a.sz[s0 + nb] = size2;
+              }
+              ++nb;
+              bytes += size2;
+              s = j0 + f2;
+            }
+          }
+        }
         break;
       }
       carry += lane64(incl, 63);
