@@ -1305,7 +1305,8 @@ __global__ __launch_bounds__(256) void rot_finish_kernel(RotArgs a) {
   if (threadIdx.x == 0) {
     // SST count: the computed chain elements below n (increasing, then n), by binary search
     const uint32_t done = *a.chain_end;
-    uint32_t lo = 0, hi = done ? uint32_t(min<uint64_t>(a.sst_cap, 1ull << done)) : 1u;
+    const uint64_t cap2 = 1ull << done;  // (HIP's min<uint64_t> compiles to f64 compares)
+    uint32_t lo = 0, hi = done ? uint32_t(a.sst_cap < cap2 ? a.sst_cap : cap2) : 1u;
     if (n == 0) {
       hi = 0;
     } else {

@@ -891,7 +891,7 @@ struct ScanArgs {
 };
 
 __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
-  __shared__ uint64_t part[1024][3];
+  __shared__ uint64_t part[32][3];  // wave totals, then wave bases
   const uint32_t t = threadIdx.x;
   const uint64_t per = (a.ntiles + 1023) / 1024, lo = t * per, hi = lo + per < a.ntiles ? lo + per : a.ntiles;
   uint64_t s0 = 0, s1 = 0, s2 = 0;
@@ -900,25 +900,30 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
     s1 += a.tile_sum[3 * i + 1];
     s2 += a.tile_sum[3 * i + 2];
   }
-  part[t][0] = s0;
-  part[t][1] = s1;
-  part[t][2] = s2;
-  __syncthreads();
-  // Hillis-Steele inclusive scan over the 1024 partials
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    uint64_t x0 = 0, x1 = 0, x2 = 0;
-    if (t >= d) {
-      x0 = part[t - d][0];
-      x1 = part[t - d][1];
-      x2 = part[t - d][2];
-    }
-    __syncthreads();
-    part[t][0] += x0;
-    part[t][1] += x1;
-    part[t][2] += x2;
-    __syncthreads();
+  // block scan of the 1024 partials: wave scans, then one wave over the 16 wave totals (two
+  // barriers; a Hillis-Steele scan over LDS took twenty)
+  const uint32_t l = t & 63, w = t >> 6;
+  uint64_t i0 = wave_incl_scan<uint64_t>(s0), i1 = wave_incl_scan<uint64_t>(s1), i2 = wave_incl_scan<uint64_t>(s2);
+  if (l == 63) {
+    part[w][0] = i0;
+    part[w][1] = i1;
+    part[w][2] = i2;
   }
-  uint64_t e0 = t ? part[t - 1][0] : 0, e1 = t ? part[t - 1][1] : 0, e2 = t ? part[t - 1][2] : 0;
+  __syncthreads();
+  if (w == 0) {
+    uint64_t x0 = l < 16 ? part[l][0] : 0, x1 = l < 16 ? part[l][1] : 0, x2 = l < 16 ? part[l][2] : 0;
+    const uint64_t y0 = wave_incl_scan<uint64_t>(x0), y1 = wave_incl_scan<uint64_t>(x1), y2 = wave_incl_scan<uint64_t>(x2);
+    if (l < 16) {
+      part[16 + l][0] = y0 - x0;  // exclusive wave bases
+      part[16 + l][1] = y1 - x1;
+      part[16 + l][2] = y2 - x2;
+    }
+  }
+  __syncthreads();
+  i0 += part[16 + w][0];
+  i1 += part[16 + w][1];
+  i2 += part[16 + w][2];
+  uint64_t e0 = i0 - s0, e1 = i1 - s1, e2 = i2 - s2;
   for (uint64_t i = lo; i < hi; ++i) {
     a.tile_pre[3 * i] = e0;
     a.tile_pre[3 * i + 1] = e1;
@@ -928,7 +933,7 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
     e2 += a.tile_sum[3 * i + 2];
   }
   if (t == 1023) {
-    const uint64_t N = part[1023][0], K = part[1023][1], V = part[1023][2];
+    const uint64_t N = i0, K = i1, V = i2;
     if (a.blk_ent) a.blk_ent[a.nblk] = N;
     a.stats[0] = N;
     a.stats[1] = K;
@@ -2175,7 +2180,8 @@ __global__ __launch_bounds__(256) void meta_write_kernel(MetaArgs a) {
     const u32x4 v4 = *reinterpret_cast<const u32x4*>(img + 16 * c);
     const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
     const uint32_t lo = c == 0 ? lead : 0u;
-    const uint32_t hi = uint32_t(min<uint64_t>(16, span - 16ull * c));
+    const uint64_t rest = span - 16ull * c;  // (min<uint64_t> compiles to f64 compares)
+    const uint32_t hi = rest < 16 ? uint32_t(rest) : 16u;
     store_chunk(ga + 16 * c, v, lo, hi);
   }
 }
