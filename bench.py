@@ -220,8 +220,8 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     value = world * E * steps / t_max / GiB
     ms_per_step = t_max / steps * 1e3
     # algorithmic bytes per launch of each kernel (DESIGN.md "Kernels")
-    hdr = 8 * (nblk + 1) + 2 * nblk + 8 * n          # count: blk_off, trailers, offsets + entry headers
-    algo = {"dec_count": hdr, "dec_scan": 0, "decode": E + D + 8 * (nblk + 1) + 12 * nblk,
+    cnt = E + 8 * (nblk + 1) + 12 * nblk             # count: streams every block, agg
+    algo = {"dec_count": cnt, "dec_scan": 0, "decode": E + D + 8 * (nblk + 1) + 12 * nblk,
             "plan": 8 * (n + 1) + K + 8 * nblk, "emit": D + E + 16 * (nblk + 1)}
     dom = max(kms, key=lambda k: kms[k])
     achieved = algo[dom] / (kms[dom] * 1e-3) / 1e9

@@ -3,13 +3,13 @@
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE / WRITE_SIZE are KiB,
 and on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read
 (MI355X_MICROARCH.md, "HBM").  The doubling is calibrated for 16-B/lane loads only: the
-decode / emit / plan kernels stage with 16-B buffer loads; dec_count reads bytes (uncalibrated).
+decode / emit / plan / staged count kernels stage with 16-B buffer loads.
 usage: python tools/traffic.py PMC_DIR WORKLOAD BLOCKS OUT_JSON
 """
 import csv, glob, json, os, sys
 from collections import defaultdict
 
-NAMES = {"dec_count_kernel": "dec_count", "dec_scan_kernel": "dec_scan", "decode_kernel": "decode",
+NAMES = {"dec_count_kernel": "dec_count", "dec_count_staged_kernel": "dec_count", "dec_scan_kernel": "dec_scan", "decode_kernel": "decode",
          "plan_adj_kernel": "plan_adj", "plan_walk_kernel": "plan_walk", "emit_kernel": "emit",
          "crc_kernel<false>": "crc32", "crc_kernel<true>": "crc32_count", "agg_tile_kernel": "agg_tile"}
 root, workload, blocks, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
