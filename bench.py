@@ -212,8 +212,8 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
         ok = checked == nblk
     t_max, ok_all, checked_all = reduce_ranks(elapsed, ok, checked, world, dev)
 
-    # per-kernel durations: a short profiling pass after the timed region, HIP events recorded
-    # by liblsmblk.so on the launch stream around every kernel (diagnostics only, not timed)
+    # per-kernel durations: a short profiling pass after the timed region, each kernel launched
+    # by liblsmblk.so with dispatch start/stop events (diagnostics only, not timed)
     kms = kernel_times(ctx, step, dev, reps=3)
     if rank != 0:
         return None
@@ -803,13 +803,17 @@ def compaction_filter(kv, n, K, V, dev, stream, reps=5):
             "bytes_per_launch": 2 * D + 4 * n, "ok": bool(ok)}
 
 
-def kernel_times(ctx, step, dev, reps=3):
+def kernel_times(ctx, step, dev, reps=3, lead=3):
+    """Per-kernel ms of one step (the library's dispatch start/stop events, hipExtLaunchKernelGGL).
+    Each read follows `lead` back-to-back steps: after an idle gap (a synchronize) the first
+    kernels ran ~8 % slower than in the timed region, as the clocks had dropped."""
     import ctypes
     check(lib().lsmblk_debug_set(ctx, 2, 1))
     acc = {k: [] for k in KERNELS}
     buf = (ctypes.c_float * 5)()
     for _ in range(reps):
-        step()
+        for _ in range(lead):
+            step()
         torch.cuda.synchronize(dev)
         check(lib().lsmblk_ctx_kernel_times(ctx, buf))
         for i, k in enumerate(KERNELS):

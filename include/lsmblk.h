@@ -158,7 +158,7 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
  *   LSMBLK_DEBUG_DECODE_SKIP  decode ablation mask: 1 look-back, 2 keys, 4 values, 8 metadata */
 #define LSMBLK_DEBUG_POLL_MODE 0
 #define LSMBLK_DEBUG_DECODE_SKIP 1
-#define LSMBLK_DEBUG_KERNEL_TIMING 2 /* 1: record HIP events around every kernel launch */
+#define LSMBLK_DEBUG_KERNEL_TIMING 2 /* 1: dispatch start/stop events on every kernel launch */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* Durations (ms) of the kernels of the last timed decode / encode call on this context:
  * [0] dec_count [1] dec_scan [2] decode [3] plan [4] emit; -1 if not recorded.  Waits for

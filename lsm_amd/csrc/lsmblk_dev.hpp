@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdlib>
@@ -471,7 +472,7 @@ struct lsmblk_ctx {
   uint32_t poll = 0;             // look-back poll protocol (see gload)
   uint32_t skip = 0;             // decode ablation mask (timing experiments only)
   bool timing = false;           // record HIP events around every kernel (diagnostics)
-  hipEvent_t ev[8] = {};         // decode: 0 count 1 scan 2 decode 3 | encode: 4 plan 5 emit 6
+  hipEvent_t ev[10] = {};        // start / stop: count 0 1, scan 2 3, decode 4 5, plan 6 7, emit 8 9
   bool dec_timed = false, enc_timed = false;
   // BlockMeta sections (lsmblk_block_meta_batch)
   uint32_t* meta_rec = nullptr;     // nblk
