@@ -1036,6 +1036,13 @@ __device__ __forceinline__ uint32_t key_lcp(const PlanKeys& K, uint32_t pp, uint
   return lcp;
 }
 
+#ifndef PLAN_RING
+#define PLAN_RING 1  // walk over a ring of two LDS chunks, the next chunk's loads in flight
+#endif
+#ifndef PLAN_REC_OFF
+#define PLAN_REC_OFF 0  // 1: rec = klen + vlen from the offsets in the walk (plan_adj writes alcp only): slower, the walk is issue-sensitive
+#endif
+
 __global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
   const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -1043,7 +1050,9 @@ __global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a0) {
   const PlanKeys K = plan_keys(a);
   if (e < a.n) {
     const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
+#if !PLAN_REC_OFF
     a.rec[e] = kl + (a.val_off[e + 1] - a.val_off[e]);
+#endif
     uint32_t al = 0;
     if (e > 0) {
       const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
@@ -1065,13 +1074,159 @@ constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
 #define PLAN_TWO_BLOCKS 1  // two blocks per window step when the second fits the window
 #endif
 
-__global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
+#ifndef PLAN_FUSED
+#define PLAN_FUSED 1  // (rec, alcp) produced into the walkers' LDS rings by helper waves of the same workgroup
+#endif
+constexpr uint32_t kWalkThreads = PLAN_FUSED ? 512 : 256;
+[[maybe_unused]] constexpr uint32_t kSpinMax = 1u << 24;  // LDS hand-off polls before a wave gives up (TIMEOUT)
+
+#ifndef PLAN_PROD_BATCH
+#define PLAN_PROD_BATCH 4
+#endif
+[[maybe_unused]] constexpr uint32_t kProdBatch = PLAN_PROD_BATCH;  // entries per lane with loads in flight together
+#ifndef PLAN_CHUNK
+#define PLAN_CHUNK 512
+#endif
+[[maybe_unused]] constexpr uint32_t kChunk = PLAN_CHUNK;  // entries per producer hand-off (ring = 2 x kWalk)
+
+#if PLAN_FUSED
+// Helper wave of a walker: plan_adj's per-entry values for the walker's segment [s0, s1),
+// written chunk by chunk into the walker's ring (slot (e - s0) % kRing), never to HBM.
+// A chunk may overwrite the ring's older half once the walker's window has left it;
+// prod[0] = entries produced (relative to s0), cons[0] = walker's window start (relative).
+__device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, uint32_t s1, uint32_t* CR,
+                             uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t kRing, uint32_t& err) {
+  const uint32_t l = lane_id();
+  const uint32_t klim = K.glead + uni(a.key_off[a.n]);
+  for (uint32_t c = s0; c < s1; c += kChunk) {
+    const uint32_t cend = s1 - c < kChunk ? s1 : c + kChunk;
+    if (c - s0 + kChunk > kRing) {  // ring space: the walker's window must have passed c + kChunk - kRing
+      const uint32_t need = c - s0 + kChunk - kRing;
+      uint32_t spins = 0;
+      while (__hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+        if (++spins > kSpinMax) {
+          err |= LSMBLK_ERR_TIMEOUT;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+#pragma unroll 1
+    for (uint32_t h = 0; h < kChunk / 64; h += kProdBatch) {  // kProdBatch entries per lane at a time
+      uint32_t kp[kProdBatch], kn[kProdBatch], pp[kProdBatch], v0[kProdBatch], v1[kProdBatch];
+#pragma unroll
+      for (uint32_t i = 0; i < kProdBatch; ++i) {
+        const uint32_t e = c + 64 * (h + i) + l;
+        kp[i] = kn[i] = pp[i] = v0[i] = v1[i] = 0;
+        if (e < cend) {
+          kp[i] = a.key_off[e];
+          kn[i] = a.key_off[e + 1];
+          pp[i] = e > 0 ? a.key_off[e - 1] : 0u;
+          v0[i] = a.val_off[e];
+          v1[i] = a.val_off[e + 1];
+        }
+      }
+      u32x4 xk[kProdBatch], xp[kProdBatch];
+#pragma unroll
+      for (uint32_t i = 0; i < kProdBatch; ++i) {
+        const uint32_t e = c + 64 * (h + i) + l;
+        if (e < cend && e != s0) {
+          xk[i] = __builtin_amdgcn_raw_buffer_load_b128(K.gk, K.glead + kp[i], 0, 0);
+          xp[i] = __builtin_amdgcn_raw_buffer_load_b128(K.gk, K.glead + pp[i], 0, 0);
+        }
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kProdBatch; ++i) {
+        const uint32_t e = c + 64 * (h + i) + l;
+        if (e >= cend) continue;
+        const uint32_t kl = kn[i] - kp[i], x = (e - s0) & (kRing - 1);
+        if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
+        uint32_t al = 0;
+        if (e != s0) {  // as plan_adj_kernel: LCP with the predecessor, bit 31 = out of order
+          const uint32_t pl = kp[i] - pp[i], m = pl < kl ? pl : kl;
+          uint32_t lcp = m, w0 = 0, w1 = 0;
+          bool done = false;
+          if (K.glead + kp[i] + 16 <= klim && K.glead + pp[i] + 16 <= klim) {
+            const uint32_t P[4] = {xp[i].x, xp[i].y, xp[i].z, xp[i].w}, Q[4] = {xk[i].x, xk[i].y, xk[i].z, xk[i].w};
+#pragma unroll
+            for (uint32_t d = 0; d < 4; ++d) {
+              if (!done && 4 * d < m) {
+                if (P[d] != Q[d]) {
+                  const uint32_t z = 4 * d + (__builtin_ctz(P[d] ^ Q[d]) >> 3);
+                  if (z < m) {
+                    lcp = z;
+                    w0 = P[d];
+                    w1 = Q[d];
+                  }
+                  done = true;
+                }
+              } else {
+                done = true;
+              }
+            }
+            if (!done && m > 16) {  // equal first 16 bytes: the rest by dwords
+              for (uint32_t d = 4; 4 * d < m; ++d) {
+                const uint32_t y0 = K.dword(pp[i] + 4 * d), y1 = K.dword(kp[i] + 4 * d);
+                if (y0 != y1) {
+                  const uint32_t z = 4 * d + (__builtin_ctz(y0 ^ y1) >> 3);
+                  if (z < m) {
+                    lcp = z;
+                    w0 = y0;
+                    w1 = y1;
+                  }
+                  break;
+                }
+              }
+            }
+          } else {
+            lcp = key_lcp(K, pp[i], pl, kp[i], kl, w0, w1);
+          }
+          const uint32_t sh = 8 * (lcp & 3);
+          const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
+          al = (lcp < kAlcpLcp ? lcp : kAlcpLcp) | (sorted ? 0u : kAlcpUnsorted);
+        }
+        CR[x] = kl + (v1[i] - v0[i]);
+        CA[x] = al;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (l == 0) __hip_atomic_store(prod, cend - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+#endif
+
+// (fused: two workgroups of 8 waves per CU, so that all ~2 K segments walk at once)
+__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PLAN_FUSED ? 4 : 1))) void plan_walk_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
-  __shared__ uint32_t crec[4][kWalk], calcp[4][kWalk];
+#if PLAN_RING || PLAN_FUSED
+  constexpr uint32_t kRing = 2 * kWalk;
+#else
+  constexpr uint32_t kRing = kWalk;
+#endif
+  __shared__ uint32_t crec[4][kRing], calcp[4][kRing];
+  const uint32_t l = lane_id();
+#if PLAN_FUSED
+  // waves 0-3 walk segments, wave 4 + w produces (rec, alcp) into walker w's ring
+  __shared__ uint32_t hand_g[4], hand_prod[4], hand_cons[4];
+  const uint32_t wv = wave_id(), ww = wv & 3;
+  if (wv < 4) {
+    const uint32_t t = take_ticket(a.ticket);
+    if (l == 0) {
+      hand_g[wv] = t;
+      hand_prod[wv] = 0;
+      hand_cons[wv] = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t g = uni(hand_g[ww]);
+  uint32_t* CR = crec[ww];
+  uint32_t* CA = calcp[ww];
+#else
   uint32_t* CR = crec[wave_id()];
   uint32_t* CA = calcp[wave_id()];
-  const uint32_t l = lane_id();
   const uint32_t g = take_ticket(a.ticket);
+#endif
   if (g >= a.nseg) return;
   uint32_t err = 0;
   uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
@@ -1082,30 +1237,100 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
     if (s1 < s0) s1 = s0;
   }
   const PlanKeys K = plan_keys(a);
-  uint32_t c0 = 0, c1 = 0;  // LDS chunk = entries [c0, c1)
-  auto load_chunk = [&](uint32_t from) {
-    c0 = from;
-    c1 = s1 - from < kWalk ? s1 : from + kWalk;
-    uint32_t r[kWalk / 64], q[kWalk / 64];
+#if PLAN_FUSED
+  if (wv >= 4) {
+    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], kRing, err);
+    const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
+                          (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
+    raise_err(a.stats, werr);
+    return;
+  }
+#endif
+  // (rec, alcp) of entry e at LDS slot (e - s0) % kRing.  Ring: entries [.., ld_end) are in LDS,
+  // [pf_beg, pf_end) = [ld_end, ld_end + kWalk) in flight in registers; a window reaching past
+  // ld_end commits them (landed long before: a chunk is ~16 window steps) and issues the next.
+  // A commit overwrites the slots of entries kRing back, all behind the window (j0 > ld_end - 64).
+  uint32_t ld_end = s0, pf_beg = s0, pf_end = s0;
+#if PLAN_REC_OFF
+  uint32_t pk0[kWalk / 64], pk1[kWalk / 64], pv0[kWalk / 64], pv1[kWalk / 64];
+#else
+  uint32_t pr[kWalk / 64];
+#endif
+  uint32_t pq[kWalk / 64];
+  [[maybe_unused]] auto issue = [&](uint32_t from) {
+    pf_beg = from;
+    pf_end = s1 - from < kWalk ? s1 : from + kWalk;
 #pragma unroll
     for (uint32_t i = 0; i < kWalk / 64; ++i) {
-      const uint32_t j = c0 + 64 * i + l;
-      if (j < c1) {
-        r[i] = a.rec[j];
-        q[i] = a.alcp[j];
+      const uint32_t j = from + 64 * i + l;
+      if (j < pf_end) {
+#if PLAN_REC_OFF
+        pk0[i] = a.key_off[j];
+        pk1[i] = a.key_off[j + 1];
+        pv0[i] = a.val_off[j];
+        pv1[i] = a.val_off[j + 1];
+#else
+        pr[i] = a.rec[j];
+#endif
+        pq[i] = a.alcp[j];
       }
     }
-    wave_sync();
-#pragma unroll
-    for (uint32_t i = 0; i < kWalk / 64; ++i) {
-      const uint32_t j = 64 * i + l;
-      if (c0 + j < c1) {
-        CR[j] = r[i];
-        CA[j] = q[i];
-      }
-    }
-    wave_sync();
   };
+  [[maybe_unused]] auto commit = [&]() {
+#pragma unroll
+    for (uint32_t i = 0; i < kWalk / 64; ++i) {
+      const uint32_t j = pf_beg + 64 * i + l;
+      if (j < pf_end) {
+        const uint32_t x = (j - s0) & (kRing - 1);
+#if PLAN_REC_OFF
+        CR[x] = (pk1[i] - pk0[i]) + (pv1[i] - pv0[i]);  // klen + vlen, u32 as plan_adj's
+#else
+        CR[x] = pr[i];
+#endif
+        CA[x] = pq[i];
+      }
+    }
+    wave_sync();
+    ld_end = pf_end;
+  };
+#if PLAN_FUSED
+  (void)pf_beg;
+  (void)pf_end;
+  uint32_t known = 0;  // entries of the ring the producer has finished (relative to s0)
+  bool stalled = false;
+  auto need = [&](uint32_t j0, uint32_t wend) {
+    __hip_atomic_store(&hand_cons[ww], j0 - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (wend - s0 > known && !stalled) {
+      uint32_t spins = 0;
+      while ((known = __hip_atomic_load(&hand_prod[ww], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < wend - s0) {
+        if (++spins > kSpinMax) {
+          err |= LSMBLK_ERR_TIMEOUT;
+          stalled = true;  // walk on over stale ring data: the call fails with TIMEOUT
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+  };
+#elif PLAN_RING
+  auto need = [&](uint32_t j0, uint32_t wend) {
+    (void)j0;
+    if (wend > ld_end) {
+      commit();
+      if (ld_end < s1) issue(ld_end);
+    }
+  };
+  issue(s0);
+  need(s0, s0 + 1);
+#else
+  auto need = [&](uint32_t j0, uint32_t wend) {  // one chunk, reloaded from the window when left
+    if (!(j0 >= pf_beg && wend <= ld_end)) {
+      issue(j0);
+      commit();
+    }
+  };
+#endif
   uint32_t nb = 0;
   uint64_t bytes = 0;
   const uint64_t bs = a.block_size;
@@ -1116,13 +1341,14 @@ __global__ __launch_bounds__(256) void plan_walk_kernel(PlanArgs a0) {
     uint32_t sp = 0, sl = 0;      // key_s (direct compares only)
     for (uint32_t j0 = s;; j0 += 64) {
       const uint32_t wend = s1 - j0 < 64 ? s1 : j0 + 64;
-      if (!(j0 >= c0 && wend <= c1)) load_chunk(j0);
+      need(j0, wend);
       const uint32_t e = j0 + l;
       const bool valid = e < s1;
       uint32_t r = 0, al = kAlcpLcp;
       if (valid) {
-        r = CR[e - c0];
-        if (e != s) al = CA[e - c0];
+        const uint32_t x = (e - s0) & (kRing - 1);
+        r = CR[x];
+        if (e != s) al = CA[x];
       }
       if (!direct && __ballot(al & kAlcpUnsorted)) {  // an out-of-order pair inside this block
         direct = true;
@@ -2755,13 +2981,17 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.dnseg = dnseg;
   p.span = span ? 1u : 0u;
   c->enc_timed = c->timing;
+#if PLAN_FUSED  // plan_adj's work is done by the walk's helper waves
+  tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, 6, 7, p);
+#else
   if (in->n) {
     const uint32_t eg = uint32_t((in->n + 255) / 256);
     tlaunch(c, plan_adj_kernel, dim3(eg), dim3(256), st, 6, -1, p);
   } else if (c->timing) {
     (void)hipEventRecord(c->ev[6], st);
   }
-  tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(256), st, -1, 7, p);
+  tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, -1, 7, p);
+#endif
   // the big-block flags are cleared before emit (the start of emit_kernel to the end of
   // emit_big_kernel is what bench.py's roofline divides by)
   const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;  // blocks <= entries, <= blk_cap
