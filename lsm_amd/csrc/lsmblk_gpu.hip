@@ -1084,6 +1084,9 @@ constexpr uint32_t kWalkThreads = PLAN_FUSED ? 512 : 256;
 #define PLAN_PROD_BATCH 4
 #endif
 [[maybe_unused]] constexpr uint32_t kProdBatch = PLAN_PROD_BATCH;  // entries per lane with loads in flight together
+#ifndef PLAN_PROD_DPP
+#define PLAN_PROD_DPP 0
+#endif
 #ifndef PLAN_CHUNK
 #define PLAN_CHUNK 512
 #endif
@@ -1115,6 +1118,25 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
 #pragma unroll 1
     for (uint32_t h = 0; h < kChunk / 64; h += kProdBatch) {  // kProdBatch entries per lane at a time
       uint32_t kp[kProdBatch], kn[kProdBatch], pp[kProdBatch], v0[kProdBatch], v1[kProdBatch];
+#if PLAN_PROD_DPP
+      // one vector load per array per entry; the neighbours' offsets by wave-wide DPP shifts,
+      // the two edge lanes' from uniform (scalar) loads
+#pragma unroll
+      for (uint32_t i = 0; i < kProdBatch; ++i) {
+        const uint32_t base = c + 64 * (h + i), e = base + l;
+        kp[i] = v0[i] = 0;
+        if (e <= cend) {
+          kp[i] = a.key_off[e];
+          v0[i] = a.val_off[e];
+        }
+        const uint32_t up = base + 64 < cend ? base + 64 : cend;
+        const uint32_t ke = kconst(a.key_off)[up], ve = kconst(a.val_off)[up];
+        const uint32_t kb = base > 0 ? kconst(a.key_off)[base - 1] : 0u;
+        kn[i] = uint32_t(__builtin_amdgcn_update_dpp(int(ke), int(kp[i]), 0x130, 0xF, 0xF, false));  // wave_shl:1
+        v1[i] = uint32_t(__builtin_amdgcn_update_dpp(int(ve), int(v0[i]), 0x130, 0xF, 0xF, false));
+        pp[i] = uint32_t(__builtin_amdgcn_update_dpp(int(kb), int(kp[i]), 0x138, 0xF, 0xF, false));  // wave_shr:1
+      }
+#else
 #pragma unroll
       for (uint32_t i = 0; i < kProdBatch; ++i) {
         const uint32_t e = c + 64 * (h + i) + l;
@@ -1127,6 +1149,7 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
           v1[i] = a.val_off[e + 1];
         }
       }
+#endif
       u32x4 xk[kProdBatch], xp[kProdBatch];
 #pragma unroll
       for (uint32_t i = 0; i < kProdBatch; ++i) {
