@@ -1070,6 +1070,9 @@ __global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a0) {
 }
 
 constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
+#ifndef PLAN_STREAM
+#define PLAN_STREAM 1  // every block ending in a window found in it; open blocks carry into the next window
+#endif
 #ifndef PLAN_TWO_BLOCKS
 #define PLAN_TWO_BLOCKS 1  // two blocks per window step when the second fits the window
 #endif
@@ -1084,6 +1087,9 @@ constexpr uint32_t kWalkThreads = PLAN_FUSED ? 512 : 256;
 #define PLAN_PROD_BATCH 4
 #endif
 [[maybe_unused]] constexpr uint32_t kProdBatch = PLAN_PROD_BATCH;  // entries per lane with loads in flight together
+#ifndef PLAN_RING_ENTRIES
+#define PLAN_RING_ENTRIES 2048  // per walker (power of two, >= 2 producer chunks and >= kWalk)
+#endif
 #ifndef PLAN_PROD_DPP
 #define PLAN_PROD_DPP 0
 #endif
@@ -1223,7 +1229,8 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
 __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PLAN_FUSED ? 4 : 1))) void plan_walk_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
 #if PLAN_RING || PLAN_FUSED
-  constexpr uint32_t kRing = 2 * kWalk;
+  constexpr uint32_t kRing = PLAN_RING_ENTRIES;
+  static_assert(PLAN_FUSED ? (kRing >= 2 * kChunk && (kRing & (kRing - 1)) == 0) : kRing == 2 * kWalk, "plan ring size");
 #else
   constexpr uint32_t kRing = kWalk;
 #endif
@@ -1397,7 +1404,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
       const bool stop = !valid || (e != s && before + r + 14 > bs);
       const uint64_t m = __ballot(stop);
       if (m) {
-        const uint32_t f = uint32_t(__builtin_ctzll(m));
+        uint32_t f = uint32_t(__builtin_ctzll(m));
         const uint64_t size = lane64(before, f);
         if (l == 0) {
           a.rec_first[s0 + nb] = s;
@@ -1405,6 +1412,42 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
         }
         ++nb;
         bytes += size;
+#if PLAN_STREAM
+        s = j0 + f;
+        // Further blocks from entry s on the same window's lanes f..63 (the window held no
+        // out-of-order pair, or direct would be set): LCP with entry s = min of alcp over
+        // (f, e] (lanes <= f read the min identity); growth and estimated_size restart at s.
+        // Every block ending in the window is found here; a block still open at the window's
+        // end carries (estimated_size, running LCP) into the next window instead of restarting
+        // the walk at its first entry.
+        bool open = false;
+        while (!direct && s < s1) {
+          const uint32_t mn = wave_incl_min31(l <= f ? kAlcpLcp : (al & kAlcpLcp));  // all lanes (DPP)
+          const uint32_t p2 = l <= f ? 0u : mn;
+          const uint32_t g2 = (valid && l >= f) ? r + 16 - p2 : 0u;
+          if (__ballot(g2 >= (1u << 25)) != 0) break;  // huge entries: restart at s (64-bit path)
+          const uint32_t incl2 = wave_incl_scan32(g2);
+          const uint32_t before2 = 2 + incl2 - g2;
+          const uint64_t m2 = __ballot(l > f && (!valid || uint64_t(before2) + r + 14 > bs));
+          if (!m2) {  // block s runs past this window
+            carry = 2 + uint64_t(uint32_t(__builtin_amdgcn_readlane(incl2, 63)));
+            pmin = uint32_t(__builtin_amdgcn_readlane(mn, 63));
+            open = true;
+            break;
+          }
+          const uint32_t f2 = uint32_t(__builtin_ctzll(m2));
+          const uint32_t size2 = uint32_t(__builtin_amdgcn_readlane(before2, f2));
+          if (l == 0) {
+            a.rec_first[s0 + nb] = s;
+            a.sz[s0 + nb] = size2;
+          }
+          ++nb;
+          bytes += size2;
+          s = j0 + f2;
+          f = f2;
+        }
+        if (open) continue;  // next window, same block
+#else
         const uint32_t len1 = j0 + f - s;  // entries of the block just found
         s = j0 + f;
         // The next block from entry s, on the same window's lanes f..63 (the window held no
@@ -1433,6 +1476,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
             }
           }
         }
+#endif
         break;
       }
       carry += lane64(incl, 63);
