@@ -1088,13 +1088,13 @@ constexpr uint32_t kWalkThreads = PLAN_FUSED ? 512 : 256;
 #endif
 [[maybe_unused]] constexpr uint32_t kProdBatch = PLAN_PROD_BATCH;  // entries per lane with loads in flight together
 #ifndef PLAN_RING_ENTRIES
-#define PLAN_RING_ENTRIES 2048  // per walker (power of two, >= 2 producer chunks and >= kWalk)
+#define PLAN_RING_ENTRIES 1024  // per walker (power of two, >= 2 producer chunks): 32 KiB per workgroup, 3 per CU
 #endif
 #ifndef PLAN_PROD_DPP
 #define PLAN_PROD_DPP 0
 #endif
 #ifndef PLAN_CHUNK
-#define PLAN_CHUNK 512
+#define PLAN_CHUNK 256
 #endif
 [[maybe_unused]] constexpr uint32_t kChunk = PLAN_CHUNK;  // entries per producer hand-off (ring = 2 x kWalk)
 
@@ -1225,7 +1225,7 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
 }
 #endif
 
-// (fused: two workgroups of 8 waves per CU, so that all ~2 K segments walk at once)
+// (fused: three workgroups of 8 waves per CU, so that up to 3 K segments walk at once)
 __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PLAN_FUSED ? 4 : 1))) void plan_walk_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
 #if PLAN_RING || PLAN_FUSED
