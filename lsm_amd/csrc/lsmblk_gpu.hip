@@ -1552,6 +1552,9 @@ __device__ __forceinline__ EmitArgs resolve(const EmitArgs& a0) {
   return a;
 }
 
+#ifndef EMIT_DIRECT_CENT
+#define EMIT_DIRECT_CENT 1  // phase 1 entry lanes write the chunk -> source map (no max-scan pass)
+#endif
 constexpr uint32_t kEmitWaves = 4;
 constexpr uint32_t kEmitKCap = 1088;
 constexpr uint32_t kEmitICap = 4224;  // block image: staged values, then the encoded block (33 swizzle rows)
@@ -1791,7 +1794,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // and the value bytes of each value's two partial edge chunks (captured in registers: the
     // in-place move below overwrites the staged values).
     const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
+#if EMIT_DIRECT_CENT
+    for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = ~0u;
+#else
     for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
+#endif
     uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
 #pragma unroll
     for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
@@ -1859,9 +1866,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         L.vdst[k] = uint16_t(pos + 14 + sfx);
         L.vsrc[k] = uint16_t(vlead + vp);
         L.vlen[k] = uint16_t(vl);
+#if EMIT_DIRECT_CENT
+        // the image chunks lying wholly inside this value -> their source bytes in the staged
+        // values (every other chunk keeps ~0)
+        {
+          const uint32_t vdb = olead + pos + 14 + sfx;  // image byte of the value
+          const uint32_t srcb = vlead + vp - vdb;       // + image byte = staged byte (mod 2^32)
+          for (uint32_t c = (vdb + 15) >> 4; 16 * c + 16 <= vdb + vl; ++c) L.cent[c] = srcb + 16 * c;
+        }
+#else
         // first image chunk whose start is at or after this value's start
         const uint32_t j0 = (olead + pos + 14 + sfx + 15) >> 4;
         if (j0 < ncs && vl) atomicMax(&L.cent[j0], k);
+#endif
       }
     }
     const uint32_t data_len = dc;
@@ -1885,7 +1902,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // Phase 2a (ascending): image chunk -> source byte of a chunk lying wholly inside one
     // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
     // kEB chunk groups per batch: every LDS read of the batch is issued before its uses.
-    {
+    // (EMIT_DIRECT_CENT: the entry lanes wrote the map in phase 1)
+    if (!EMIT_DIRECT_CENT) {
       uint32_t carry = 0;
       for (uint32_t c0 = 0; c0 < ncs; c0 += 64 * kEB) {
         uint32_t kk[kEB];
