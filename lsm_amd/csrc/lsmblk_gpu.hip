@@ -1563,9 +1563,13 @@ constexpr uint32_t kEmitMaxE = 128;
 struct alignas(16) EmitLds {
   uint8_t kimg[kEmitKCap];
   uint8_t img[kEmitICap];
-  uint32_t cent[kEmitICap / 16 + 1];  // chunk -> last entry whose value starts at/before it, then its source
+  uint32_t cent[kEmitICap / 16 + 1];  // chunk -> its source byte in the staged values, ~0 if not wholly inside one value
+#if EMIT_DIRECT_CENT
+  alignas(16) uint32_t erec[4 * kEmitMaxE];  // per entry: record start | prefix << 16, suffix in kimg | value length << 16, suffix length
+#else
   uint16_t epos[kEmitMaxE], pfx[kEmitMaxE], ksrc[kEmitMaxE];  // record start, prefix, suffix in kimg
   uint16_t vdst[kEmitMaxE], vsrc[kEmitMaxE], vlen[kEmitMaxE];  // value start (block), staged start, length
+#endif
   uint64_t ts[kEmitMaxE];
 };
 
@@ -1860,12 +1864,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       dc += __shfl(incl, 63, 64);
       if (k < n) {
         const uint32_t sfx = kl - p;
+#if EMIT_DIRECT_CENT  // phase 3 and the offsets table read these on the same lane: one 16-B record
+        *reinterpret_cast<u32x4*>(L.erec + 4 * k) = u32x4{pos | (p << 16), (klead + kp + p) | (vl << 16), sfx, 0u};
+#else
         L.epos[k] = uint16_t(pos);
         L.pfx[k] = uint16_t(p);
         L.ksrc[k] = uint16_t(klead + kp + p);
         L.vdst[k] = uint16_t(pos + 14 + sfx);
         L.vsrc[k] = uint16_t(vlead + vp);
         L.vlen[k] = uint16_t(vl);
+#endif
 #if EMIT_DIRECT_CENT
         // the image chunks lying wholly inside this value -> their source bytes in the staged
         // values (every other chunk keeps ~0)
@@ -1903,7 +1911,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
     // kEB chunk groups per batch: every LDS read of the batch is issued before its uses.
     // (EMIT_DIRECT_CENT: the entry lanes wrote the map in phase 1)
-    if (!EMIT_DIRECT_CENT) {
+#if !EMIT_DIRECT_CENT
+    {
       uint32_t carry = 0;
       for (uint32_t c0 = 0; c0 < ncs; c0 += 64 * kEB) {
         uint32_t kk[kEB];
@@ -1937,6 +1946,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         }
       }
     }
+#endif
     wave_sync();
     // Phase 2b (descending): move whole-value chunks to their place in the encoded block.
     // A value only moves up (its destination follows its own header and every earlier
@@ -1970,8 +1980,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         const uint32_t k = 64 * it + l;
         if (64 * it >= n) break;
         if (k >= n) continue;
+#if EMIT_DIRECT_CENT
+        const u32x4 er = *reinterpret_cast<const u32x4*>(L.erec + 4 * k);
+        const uint32_t pos = er.x & 0xFFFF, p = er.x >> 16, ks = er.y & 0xFFFF, vl = er.y >> 16, sfx = er.z;
+        const uint32_t vd = pos + 14 + sfx;
+#else
         const uint32_t pos = L.epos[k], p = L.pfx[k], ks = L.ksrc[k], vd = L.vdst[k], vl = L.vlen[k];
         const uint32_t sfx = vd - pos - 14;
+#endif
         const uint64_t tsv = L.ts[k];
         // unaligned LDS stores (the image is not swizzled): every field is one or two stores
         uint8_t* o = L.img;
@@ -2001,7 +2017,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     wave_sync();
     // offsets table + entry count (u16 BE, `as u16`)
     for (uint32_t k = l; k < n; k += 64)
+#if EMIT_DIRECT_CENT
+      *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.erec[4 * k] & 0xFFFF));
+#else
       *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.epos[k] & 0xFFFF));
+#endif
     if (l == 0) *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * n) = uint16_t(bswap16(n & 0xFFFF));
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
