@@ -1563,7 +1563,7 @@ constexpr uint32_t kEmitMaxE = 128;
 struct alignas(16) EmitLds {
   uint8_t kimg[kEmitKCap];
   uint8_t img[kEmitICap];
-  uint32_t cent[kEmitICap / 16 + 1];  // chunk -> its source byte in the staged values, ~0 if not wholly inside one value
+  alignas(16) uint32_t cent[kEmitICap / 16 + 4];  // chunk -> its source byte in the staged values, ~0 if not wholly inside one value
 #if EMIT_DIRECT_CENT
   alignas(16) uint32_t erec[4 * kEmitMaxE];  // per entry: record start | prefix << 16, suffix in kimg | value length << 16, suffix length
 #else
@@ -1799,7 +1799,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // in-place move below overwrites the staged values).
     const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
 #if EMIT_DIRECT_CENT
-    for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = ~0u;
+    for (uint32_t j = 4 * l; j < ncs; j += 256) *reinterpret_cast<u32x4*>(L.cent + j) = u32x4{~0u, ~0u, ~0u, ~0u};
 #else
     for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
 #endif
