@@ -895,7 +895,8 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
   const uint32_t t = threadIdx.x;
   const uint64_t per = (a.ntiles + 1023) / 1024, lo = t * per, hi = lo + per < a.ntiles ? lo + per : a.ntiles;
   uint64_t s0 = 0, s1 = 0, s2 = 0;
-  for (uint64_t i = lo; i < hi; ++i) {
+#pragma unroll 8
+  for (uint64_t i = lo; i < hi; ++i) {  // (unrolled: the tiles' loads in flight together)
     s0 += a.tile_sum[3 * i];
     s1 += a.tile_sum[3 * i + 1];
     s2 += a.tile_sum[3 * i + 2];
