@@ -249,8 +249,27 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uin
                                 uint32_t nprefix, const lsmblk_kv_stream* out, uint64_t* stats,
                                 void* stream);
 
+/* Merge modes (lsmblk_merge_batch_ex, lsmblk_compact_opts.merge_mode).  The reference's compact()
+ * never merges its inputs with one MergeIterator: every task reads them through
+ * TwoMergeIterator(a, b) with a = MergeIterator(L0 SSTs) or SstConcatIterator(upper level) and b =
+ * SstConcatIterator(lower level) (src/compact.rs:170-173, 188-196, 206-215).
+ *   LSMBLK_MERGE_RUNS       run-priority merge of all runs, the lower level as the LAST run: for every
+ *                           user key, all versions of the lowest-index run holding it.  This is what
+ *                           the reference's own TwoMergeIterator tests expect (src/tests/week1_day5.rs:
+ *                           15-129: test_task1_merge_1..5) and what MergeIterator does
+ *                           (merge_iterator.rs:59-184).  Default.
+ *   LSMBLK_MERGE_TWO_LEVEL  two_merge_iterator.rs:19-93 exactly as written, with a = MergeIterator over
+ *                           runs 0..nrun-2 and b = run nrun-1; it fails week1_day5's merge_3 / merge_4:
+ *                           the stream ends with b (an empty b yields nothing; a's keys >= b's last key
+ *                           are dropped), and for a key in both, skip_b drops b's 1st, 3rd, ... version
+ *                           and the 2nd, 4th, ... come BEFORE a's versions.  Byte-identical to what the
+ *                           reference binary's compaction writes for the same inputs.
+ * DESIGN.md §3 tabulates the input classes on which the two differ. */
+#define LSMBLK_MERGE_RUNS 0u
+#define LSMBLK_MERGE_TWO_LEVEL 1u
+
 /* k-way merge of sorted runs (SURVEY.md §8 f, row 2) with MergeIterator's semantics
- * (src/iterators/merge_iterator.rs:59-184): run r = entries [run_start[r], run_start[r+1]) of `in`
+ * (src/iterators/merge_iterator.rs:59-184) = LSMBLK_MERGE_RUNS: run r = entries [run_start[r], run_start[r+1]) of `in`
  * (run_start: device u32[nrun+1], [0] = 0, [nrun] = in->n; 1 <= nrun <= 64), run 0 the highest
  * priority (MergeIterator::create's index 0, e.g. the newest L0 SST).  Heads compare by user key
  * only (src/key.rs:63-81) with the run index breaking ties, and every step advances the other
@@ -262,6 +281,9 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uin
  * the required sizes in [0..2]; SEGMENTS: bad run_start).  Asynchronous. */
 int lsmblk_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                        const lsmblk_kv_stream* out, uint64_t* stats, void* stream);
+/* lsmblk_merge_batch in merge_mode LSMBLK_MERGE_RUNS or LSMBLK_MERGE_TWO_LEVEL (run nrun-1 = b). */
+int lsmblk_merge_batch_ex(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                          uint32_t merge_mode, const lsmblk_kv_stream* out, uint64_t* stats, void* stream);
 
 /* SST rotation of compact_generate_sst (src/compact.rs:278-289) over `in`, the stream of entries
  * handed to SsTableBuilder::add (one key's versions newest first): a new SST starts before entry e
@@ -284,13 +306,15 @@ typedef struct {
   const uint8_t* prefixes;
   const uint32_t* prefix_off;  /* u32[nprefix+1] */
   uint32_t block_size;
+  uint32_t merge_mode;         /* LSMBLK_MERGE_RUNS (0) or LSMBLK_MERGE_TWO_LEVEL (run nrun-1 = the lower level) */
   uint64_t target_sst_size;
 } lsmblk_compact_opts;
 
 #define LSMBLK_COMPACT_STATS_WORDS 8
 /* compact_generate_sst (src/compact.rs:223-311) on the device for sorted runs already decoded
- * into `in` (run_start as for lsmblk_merge_batch): MergeIterator merge -> keep/drop rules -> SST
- * rotation -> SsTableBuilder block packing.  `kept` receives the entries handed to
+ * into `in` (run_start as for lsmblk_merge_batch): merge (opts->merge_mode: the run-priority merge,
+ * or the reference's TwoMergeIterator with the lower level as the last run) -> keep/drop rules ->
+ * SST rotation -> SsTableBuilder block packing.  `kept` receives the entries handed to
  * SsTableBuilder::add (capacities as for decode); the blocks of every SST are written packed to
  * `out` (16-byte aligned) with blk_off (u64[blk_cap], nblk+1 values), as lsmblk_encode_batch writes
  * them; sst_start / sst_blk (u32[sst_cap], sst_cap >= 2) receive each SST's first kept entry / first
@@ -331,7 +355,8 @@ typedef struct {
  * after it, plus the entry it rejects. */
 uint64_t lsmblk_shard_halo_entries(uint32_t block_size);
 
-/* lsmblk_compact_batch's merge + rules + gather, restricted to keys in *range (NULL: all keys):
+/* lsmblk_compact_batch's merge + rules + gather, restricted to keys in *range (NULL: all keys;
+ * opts->merge_mode must be LSMBLK_MERGE_RUNS):
  * kept receives this range's entries handed to SsTableBuilder::add.  stats: [0] kept entries [1] key
  * bytes [2] value bytes [3] error flags [4] merged entries.  Asynchronous. */
 int lsmblk_compact_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
@@ -365,15 +390,20 @@ int lsmblk_shard_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* ext, uint
 /* MemTable (src/mem_table.rs:55-158): an ordered map keyed by the key bytes only (Key's Ord ignores
  * the ts, src/key.rs:63-81), so put() of a present key replaces the entry; flush() (:131-136) yields
  * the entries in key order -- the flush source the device encoder consumes (lsmblk_encode_batch,
- * then lsmblk_sst_files_batch).  Host memory; thread-safe per memtable. */
+ * then lsmblk_sst_files_batch).  Host memory; every call takes the memtable's lock (see _get). */
 typedef struct lsmblk_memtable lsmblk_memtable;
 lsmblk_memtable* lsmblk_memtable_new(void);
 void lsmblk_memtable_free(lsmblk_memtable* m);
 int lsmblk_memtable_put(lsmblk_memtable* m, const uint8_t* key, size_t klen, uint64_t ts, const uint8_t* val,
                         size_t vlen);                                                  /* :113-127 */
-/* 1 = found (*val valid until the next put), 0 = absent (:93-99). */
+/* 1 = found, 0 = absent (:93-99).  *val points into the memtable: valid only while no put of the same
+ * key can run (single-writer use); concurrent readers use lsmblk_memtable_get_copy. */
 int lsmblk_memtable_get(lsmblk_memtable* m, const uint8_t* key, size_t klen, const uint8_t** val, size_t* vlen,
                         uint64_t* ts);
+/* get() that copies the value into val[0 .. cap) under the memtable's lock (safe against concurrent
+ * puts).  1 = found, 0 = absent, LSMBLK_E_CAPACITY = cap < *vlen (nothing copied; *vlen, *ts set). */
+int lsmblk_memtable_get_copy(lsmblk_memtable* m, const uint8_t* key, size_t klen, uint8_t* val, size_t cap,
+                             size_t* vlen, uint64_t* ts);
 size_t lsmblk_memtable_len(lsmblk_memtable* m);
 size_t lsmblk_memtable_approximate_size(lsmblk_memtable* m);                          /* :154-157 */
 /* The entries in key order as a SoA KV stream in host buffers (flush, :131-136); *n / *kbytes /

@@ -25,6 +25,8 @@ LSMBLK_E_INTERNAL = -8
 LSMBLK_E_CHECKSUM = -9
 LSMBLK_DECODE_VERIFY_CRC = 1
 LSMBLK_SHARD_LAST = 1
+LSMBLK_MERGE_RUNS = 0
+LSMBLK_MERGE_TWO_LEVEL = 1
 
 
 class LsmBlkError(RuntimeError):
@@ -41,7 +43,7 @@ class KVStreamC(ctypes.Structure):
 
 class CompactOptsC(ctypes.Structure):
     _fields_ = [("watermark", U64), ("bottom_level", ctypes.c_int32), ("nprefix", U32), ("prefixes", P),
-                ("prefix_off", P), ("block_size", U32), ("target_sst_size", U64)]
+                ("prefix_off", P), ("block_size", U32), ("merge_mode", U32), ("target_sst_size", U64)]
 
 
 class KeyRangeC(ctypes.Structure):
@@ -89,6 +91,7 @@ SIGNATURES = [
     ("lsmblk_compact_filter_batch", I, [P, ctypes.POINTER(KVStreamC), U64, I, P, P, U32,
                                         ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_merge_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_merge_batch_ex", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_sst_rotation_batch", I, [P, ctypes.POINTER(KVStreamC), U32, U64, P, U32, P, P]),
     ("lsmblk_compact_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
                                  ctypes.POINTER(KVStreamC), P, U64, P, U64, P, P, U32, P, P]),
@@ -102,6 +105,7 @@ SIGNATURES = [
     ("lsmblk_memtable_free", None, [P]),
     ("lsmblk_memtable_put", I, [P, P, S, U64, P, S]),
     ("lsmblk_memtable_get", I, [P, P, S, PP, ctypes.POINTER(S), ctypes.POINTER(U64)]),
+    ("lsmblk_memtable_get_copy", I, [P, P, S, P, S, ctypes.POINTER(S), ctypes.POINTER(U64)]),
     ("lsmblk_memtable_len", S, [P]),
     ("lsmblk_memtable_approximate_size", S, [P]),
     ("lsmblk_memtable_flush", I, [P, P, P, P, P, P, U64, U64, U64, ctypes.POINTER(U64), ctypes.POINTER(U64),

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from ._lib import (CompactOptsC, KVStreamC, KeyRangeC, LSMBLK_DECODE_VERIFY_CRC, LSMBLK_E_CAPACITY,
-                   LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
+                   LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
 
 STATS_WORDS = 4
 _ctx_lock = threading.Lock()
@@ -32,7 +32,7 @@ _ctxs = {}
 
 class _Ctx:
     """One lsmblk_ctx per (device, stream): a context's device workspace is reused by every call
-    on it, so two streams never share one.  `lock` serialises call sequences that depend on the
+    on it, so two streams never share one (release_contexts frees them).  `lock` serialises call sequences that depend on the
     workspace between calls (encode_into -> segment_blocks_into) across host threads."""
 
     def __init__(self, handle):
@@ -49,6 +49,21 @@ def _ctx_for(device: int, stream_ptr: int) -> _Ctx:
             check(lib().lsmblk_ctx_create(device, ctypes.byref(h)), "lsmblk_ctx_create")
             c = _ctxs[key] = _Ctx(h.value)
         return c
+
+
+def release_contexts(device: int = None):
+    """Destroy the cached per-(device, stream) contexts (all, or those of `device`) after their
+    work is done.  Each context keeps its own decode / encode / compaction / SST workspaces, which
+    reach several GiB for 4 GiB batches, so a caller cycling through many streams releases them
+    here; the next call on a stream creates a fresh context."""
+    with _ctx_lock:
+        keys = [k for k in _ctxs if device is None or k[0] == device]
+        for k in keys:
+            c = _ctxs.pop(k)
+            with c.lock:
+                torch.cuda.synchronize(k[0])
+                lib().lsmblk_ctx_destroy(c.h)
+    return len(keys)
 
 
 def _ctx(device: int, stream=None):
@@ -442,28 +457,33 @@ def compact_filter(kv: KVStream, watermark: int, bottom_level: bool, prefixes=()
     return out
 
 
-def merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, out: KVStream, stats, stream=None):
-    """Asynchronous MergeIterator over the runs of kv into preallocated `out` (no host sync)."""
+def merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, out: KVStream, stats, stream=None,
+               merge_mode=LSMBLK_MERGE_RUNS):
+    """Asynchronous merge of the runs of kv into preallocated `out` (no host sync): MergeIterator
+    (LSMBLK_MERGE_RUNS) or the reference's TwoMergeIterator with run nrun-1 as b
+    (LSMBLK_MERGE_TWO_LEVEL)."""
     dev = _dev_index(run_start)
     kv.check(dev, "kv")
     _need(run_start, torch.int32, "run_start", dev, nrun + 1)
     out.check(dev, "out", 0)
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     ci, co = kv._c(), out._c(*out.caps())
-    check(lib().lsmblk_merge_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun,
-                                   ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev)),
-          "lsmblk_merge_batch")
+    check(lib().lsmblk_merge_batch_ex(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun, merge_mode,
+                                      ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev)),
+          "lsmblk_merge_batch_ex")
 
 
-def merge_runs(kv: KVStream, run_start, stream=None) -> KVStream:
+def merge_runs(kv: KVStream, run_start, stream=None, merge_mode=LSMBLK_MERGE_RUNS) -> KVStream:
     """MergeIterator (reference src/iterators/merge_iterator.rs:59-184) over the sorted runs
-    kv[run_start[r]:run_start[r+1]] (run 0 = highest priority) -> the merged KVStream."""
+    kv[run_start[r]:run_start[r+1]] (run 0 = highest priority) -> the merged KVStream.
+    merge_mode=LSMBLK_MERGE_TWO_LEVEL: TwoMergeIterator(MergeIterator(runs[:-1]), runs[-1])
+    (two_merge_iterator.rs:19-93 as written)."""
     dev = torch.device("cuda", _dev_index(kv.key_off))
     rs = _u32_table(run_start, dev)
     kb, vb = kv.byte_sizes()
     out = KVStream.empty(kv.n, kb, vb, dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
-    merge_into(kv, rs, rs.numel() - 1, out, stats, stream)
+    merge_into(kv, rs, rs.numel() - 1, out, stats, stream, merge_mode)
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:
@@ -529,27 +549,29 @@ def compact_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, b
 def _opts_c(opts):
     pfx, pfo = opts["_pfx"]
     return CompactOptsC(opts.get("watermark", 0), int(bool(opts.get("bottom_level", False))), opts["_npfx"],
-                        pfx.data_ptr(), pfo.data_ptr(), opts["block_size"], opts["target_sst_size"])
+                        pfx.data_ptr(), pfo.data_ptr(), opts["block_size"], opts.get("merge_mode", LSMBLK_MERGE_RUNS),
+                        opts["target_sst_size"])
 
 
 def compact_opts(watermark=0, bottom_level=False, prefixes=(), block_size=4096, target_sst_size=2 << 20,
-                 device="cuda"):
+                 device="cuda", merge_mode=LSMBLK_MERGE_RUNS):
     """Options of lsmblk_compact_batch (prefix tables staged on the device once)."""
     return dict(watermark=watermark, bottom_level=bottom_level, block_size=block_size,
                 target_sst_size=target_sst_size, _pfx=_prefix_tables(prefixes, torch.device(device)),
-                _npfx=len(prefixes))
+                _npfx=len(prefixes), merge_mode=merge_mode)
 
 
 def compact_runs(kv: KVStream, run_start, watermark=0, bottom_level=False, prefixes=(), block_size=4096,
-                 target_sst_size=2 << 20, stream=None):
+                 target_sst_size=2 << 20, stream=None, merge_mode=LSMBLK_MERGE_RUNS):
     """compact_generate_sst (reference src/compact.rs:223-311) on the device over the sorted runs
-    of kv (run 0 = highest priority): MergeIterator merge, keep/drop rules, SST rotation, block
-    packing.  Returns dict(kept KVStream, blocks, blk_off, sst_start, sst_blk, stats)."""
+    of kv (run 0 = highest priority): merge (merge_mode, see include/lsmblk.h), keep/drop rules,
+    SST rotation, block packing.  Returns dict(kept KVStream, blocks, blk_off, sst_start, sst_blk,
+    stats)."""
     dev = torch.device("cuda", _dev_index(kv.key_off))
     rs = _u32_table(run_start, dev)
     kb, vb = kv.byte_sizes()
     buf = CompactBuffers(kv.n, kb, vb, dev, target_sst_size=target_sst_size)
-    opts = compact_opts(watermark, bottom_level, prefixes, block_size, target_sst_size, dev)
+    opts = compact_opts(watermark, bottom_level, prefixes, block_size, target_sst_size, dev, merge_mode)
     compact_into(kv, rs, rs.numel() - 1, opts, buf, stream)
     torch.cuda.synchronize(dev)
     st = _status(buf.stats)

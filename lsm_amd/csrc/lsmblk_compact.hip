@@ -111,7 +111,21 @@ struct MergeArgs {
   uint64_t* tpre;           // nc_max + 1: tile bases
   uint32_t* perm;           // n: merged position -> input index
   uint64_t* mstats;         // [0] merged entries [1] candidates (tiles) [3] error flags
+  uint32_t two;             // LSMBLK_MERGE_TWO_LEVEL: TwoMergeIterator(runs 0..nrun-2, run nrun-1)
 };
+
+// LSMBLK_MERGE_TWO_LEVEL: the reference's compact() input, TwoMergeIterator(a = MergeIterator(upper
+// runs), b = the lower level's SstConcatIterator) (src/compact.rs:170-173,188-196,206-215), followed
+// through two_merge_iterator.rs:19-93 (tests/test_merge_oracle.py pins this closed form against the
+// line-by-line iterator):
+//   * the stream ends when b does (is_valid / choose_a, :32-42,60-66): nothing at all when b is
+//     empty, and no a-entry whose user key is >= b's last key;
+//   * a key held by a only: a's versions (a = MergeIterator: the lowest upper run holding it);
+//   * a key held by b only: all of b's versions;
+//   * a key held by both: skip_b (:45-50) drops every other b version, starting with the first,
+//     and b wins the equal-key choice, so b's 2nd, 4th, ... versions come first, then a's versions.
+// Run B = nrun - 1 is b.  Survival and the merged rank inside a tile (equal keys never straddle
+// tiles) follow from the same searches as the run-priority merge.
 
 // Run starts and the per-run candidate prefix (ceil(len / kMS) candidates per run) in LDS.
 __device__ __forceinline__ void load_runs(const MergeArgs& a, uint32_t* s_rs, uint32_t* s_cb) {
@@ -268,6 +282,25 @@ __device__ __forceinline__ int kcmp16(const MergeArgs& a, const GKeys& G, const 
   return key_cmp(G, a.key_off[xg] + 16, xl - 16, a.key_off[yg] + 16, yl - 16);
 }
 
+// Two-level mode: b's last key, where the reference's stream ends.
+struct TwoEnd {
+  u32x4 k16;
+  uint32_t len, g, pos;
+  bool nonempty;
+};
+__device__ __forceinline__ TwoEnd two_end(const MergeArgs& a, const GKeys& G) {
+  TwoEnd t{};
+  const uint32_t e0 = a.run_start[a.nrun - 1], e1 = a.run_start[a.nrun];
+  t.nonempty = e1 > e0;
+  if (t.nonempty) {
+    t.g = e1 - 1;
+    t.pos = a.key_off[t.g];
+    t.len = a.key_off[t.g + 1] - t.pos;
+    t.k16 = key16(G, t.pos, t.len);
+  }
+  return t;
+}
+
 // LDS fast path: 128 threads per tile; every key's first 16 bytes in LDS.
 __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
   TileHdr& H = L.h;
@@ -280,26 +313,35 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
     L.klen[u] = len;
   }
   __syncthreads();
-  // first index of run r2's sub-range whose key is >= (x, xl)
-  auto lower = [&](uint32_t r2, const u32x4& x, uint32_t xl, uint32_t xg) -> uint32_t {
+  // first index of run r2's sub-range whose key is >= (x, xl) (> with upper)
+  auto bound = [&](uint32_t r2, const u32x4& x, uint32_t xl, uint32_t xg, bool upper) -> uint32_t {
     const uint32_t b = H.tb[r2];
     uint32_t lo = 0, hi = H.tb[r2 + 1] - b;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (kcmp16(a, G, L.kw[b + mid], L.klen[b + mid], H.lo[r2] + mid, x, xl, xg) < 0) lo = mid + 1;
+      const int c = kcmp16(a, G, L.kw[b + mid], L.klen[b + mid], H.lo[r2] + mid, x, xl, xg);
+      if (c < 0 || (upper && c == 0)) lo = mid + 1;
       else hi = mid;
     }
     return lo;
   };
+  const uint32_t B = nrun - 1;
+  TwoEnd te{};
+  if (a.two) te = two_end(a, G);
   // phase A: survival -- no lower-index run holds the key (MergeIterator advances those heads)
   for (uint32_t u = tid; u < total; u += kMTT) {
     const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
     const u32x4 x = L.kw[u];
     const uint32_t xl = L.klen[u];
-    uint32_t sv = 1;
-    for (uint32_t r2 = 0; r2 < r && sv; ++r2) {
-      const uint32_t p = lower(r2, x, xl, g), b = H.tb[r2];
-      if (p < H.tb[r2 + 1] - b && kcmp16(a, G, L.kw[b + p], L.klen[b + p], H.lo[r2] + p, x, xl, g) == 0) sv = 0;
+    bool held = false;
+    for (uint32_t r2 = 0; r2 < r && !held; ++r2) {
+      const uint32_t p = bound(r2, x, xl, g, false), b = H.tb[r2];
+      held = p < H.tb[r2 + 1] - b && kcmp16(a, G, L.kw[b + p], L.klen[b + p], H.lo[r2] + p, x, xl, g) == 0;
+    }
+    uint32_t sv = !held;
+    if (a.two) {
+      if (r == B) sv = held ? ((u - H.tb[B]) - bound(B, x, xl, g, false)) & 1u : 1u;  // skip_b
+      else sv = sv && te.nonempty && kcmp16(a, G, x, xl, g, te.k16, te.len, te.g) < 0;
     }
     L.surv[u] = uint8_t(sv);
   }
@@ -338,7 +380,8 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
       rank = L.sp[u] - H.rsp[r];
       for (uint32_t r2 = 0; r2 < nrun; ++r2) {
         if (r2 == r || H.tb[r2 + 1] == H.tb[r2]) continue;
-        const uint32_t p = lower(r2, x, xl, g);
+        // two-level: b's surviving versions of an equal key come before a's
+        const uint32_t p = bound(r2, x, xl, g, a.two && r2 == B);
         rank += L.sp[H.tb[r2] + p] - H.rsp[r2];
       }
     }
@@ -358,17 +401,21 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
     len = a.key_off[g + 1] - p;
     return p;
   };
-  auto lower = [&](uint32_t r, uint32_t xp, uint32_t xl) -> uint32_t {
+  auto bound = [&](uint32_t r, uint32_t xp, uint32_t xl, bool upper) -> uint32_t {
     uint32_t lo = 0, hi = H.tb[r + 1] - H.tb[r];
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       uint32_t ml;
       const uint32_t mp = kpos(r, mid, ml);
-      if (key_cmp(G, mp, ml, xp, xl) < 0) lo = mid + 1;
+      const int c = key_cmp(G, mp, ml, xp, xl);
+      if (c < 0 || (upper && c == 0)) lo = mid + 1;
       else hi = mid;
     }
     return lo;
   };
+  const uint32_t B = nrun - 1;
+  TwoEnd te{};
+  if (a.two) te = two_end(a, G);
   auto ld = [](const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   auto stv = [](uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   auto drain = [&]() {
@@ -379,14 +426,19 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
     const uint32_t r = find_run(H.tb, nrun, u), k = u - H.tb[r];
     uint32_t xl;
     const uint32_t xp = kpos(r, k, xl);
-    uint32_t sv = 1;
-    for (uint32_t r2 = 0; r2 < r && sv; ++r2) {
-      const uint32_t p = lower(r2, xp, xl);
+    bool held = false;
+    for (uint32_t r2 = 0; r2 < r && !held; ++r2) {
+      const uint32_t p = bound(r2, xp, xl, false);
       if (p < H.tb[r2 + 1] - H.tb[r2]) {
         uint32_t ql;
         const uint32_t qp = kpos(r2, p, ql);
-        if (key_cmp(G, qp, ql, xp, xl) == 0) sv = 0;
+        held = key_cmp(G, qp, ql, xp, xl) == 0;
       }
+    }
+    uint32_t sv = !held;
+    if (a.two) {
+      if (r == B) sv = held ? (k - bound(B, xp, xl, false)) & 1u : 1u;  // skip_b
+      else sv = sv && te.nonempty && key_cmp(G, xp, xl, te.pos, te.len) < 0;
     }
     stv(a.mrank + H.lo[r] + k, sv);
   }
@@ -426,7 +478,7 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
       for (uint32_t r2 = 0; r2 < nrun; ++r2) {
         const uint32_t m2 = H.tb[r2 + 1] - H.tb[r2];
         if (r2 == r || m2 == 0) continue;
-        const uint32_t p = lower(r2, xp, xl);
+        const uint32_t p = bound(r2, xp, xl, a.two && r2 == B);
         rank += p == m2 ? H.rsv[r2] : ld(a.sp + H.lo[r2] + p) - H.rsp[r2];
       }
     }
@@ -542,6 +594,8 @@ struct GatherArgs {
   uint64_t* stats;          // [0] kept [1] key bytes [2] value bytes [3] error flags
   const uint64_t* merr;     // the merge stage's error flags (bad run table)
   lsmblk_key_range range;   // key-range shard (has_lo / has_hi 0: unbounded)
+  uint32_t two;             // two-level merge order: the rules run as the loop (mgroup_kernel)
+  uint8_t* ksame;           // two-level: per kept entry, the loop's same_as_last_key (or null)
 };
 
 // Byte order of key (x, xl) against a range bound (y, yl) in device memory: -1, 0, 1.
@@ -612,6 +666,51 @@ __device__ __forceinline__ bool mkeep(const GatherArgs& a, uint64_t j) {
   return true;
 }
 
+__device__ __forceinline__ bool prefix_filtered(const GatherArgs& a, uint32_t i) {
+  const uint32_t k0 = a.key_off[i], kl = a.key_off[i + 1] - k0;
+  for (uint32_t f = 0; f < a.npfx; ++f) {
+    const uint32_t f0 = a.pfx_off[f], fl = a.pfx_off[f + 1] - f0;
+    if (fl > kl) continue;
+    bool m = true;
+    for (uint32_t x = 0; x < fl && m; ++x) m = a.pfx[f0 + x] == a.keys[k0 + x];
+    if (m) return true;
+  }
+  return false;
+}
+
+// Two-level merge order: a key's versions are not newest first (b's versions come before a's), so
+// the closed form of mkeep does not hold.  The thread of a key's first merged entry runs the loop
+// of compact_generate_sst (src/compact.rs:234-299) over that key's versions as written: it enters
+// every key with same_as_last_key false (keys are never empty), and `last_key` becomes the key when
+// an entry is added or dropped as a bottom-level tombstone, not when the prefix filter drops it.
+// keep[j] = kept | same_as_last_key << 1 (the rotation's "key != last_key", :279).
+__global__ __launch_bounds__(256) void mgroup_kernel(GatherArgs a) {
+  const uint64_t N = *a.nm;
+  const uint64_t j0 = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (j0 >= N) return;
+  if (j0 > 0 && a.perm[j0] < a.n_max && a.perm[j0 - 1] < a.n_max && same_key_g(a, a.perm[j0 - 1], a.perm[j0]))
+    return;
+  bool lk = false, fkbw = true;  // last_key == this key; first_key_below_watermark
+  for (uint64_t j = j0; j < N; ++j) {
+    const uint32_t i = a.perm[j];
+    if (i >= a.n_max || (j > j0 && !same_key_g(a, a.perm[j - 1], i))) break;
+    const bool same = lk, below = a.ts[i] <= a.wm, empty = a.val_off[i + 1] == a.val_off[i];
+    if (!same) fkbw = true;
+    bool kept = false;
+    if (a.bottom && !same && below && empty) {  // :244-254
+      lk = true;
+      fkbw = false;
+    } else if (!(below && same && !fkbw)) {     // :256-260
+      if (below) fkbw = false;
+      if (!(below && prefix_filtered(a, i))) {  // :262-275
+        kept = true;
+        lk = true;                              // :294-297
+      }
+    }
+    a.keep[j] = (kept ? 1u : 0u) | (same ? 2u : 0u);
+  }
+}
+
 __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
   const uint64_t N = *a.nm;
   uint32_t c = 0;
@@ -621,9 +720,19 @@ __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
     const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + threadIdx.x;
     if (j < N) {
       bool k = false;
-      if (merged_in_order(a, j)) k = in_range(a, a.perm[j]) && mkeep(a, j);
-      else atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)LSMBLK_ERR_MALFORMED);
-      a.keep[j] = k;
+      uint32_t same = 0;
+      if (merged_in_order(a, j)) {
+        if (a.two && a.rules) {
+          const uint32_t g = a.keep[j];
+          k = (g & 1u) && in_range(a, a.perm[j]);
+          same = g & 2u;
+        } else {
+          k = in_range(a, a.perm[j]) && mkeep(a, j);
+        }
+      } else {
+        atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)LSMBLK_ERR_MALFORMED);
+      }
+      a.keep[j] = (k ? 1u : 0u) | same;
       if (k) {
         const uint32_t i = a.perm[j];
         c += 1;
@@ -803,7 +912,8 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
   for (uint32_t sub = 0; sub < kGTile / 256; ++sub) {
     const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + threadIdx.x;
     if (uint64_t(blockIdx.x) * kGTile + sub * 256 >= N) break;  // uniform
-    const bool k = j < N && a.keep[j];
+    const uint32_t kf = j < N ? a.keep[j] : 0u;
+    const bool k = kf & 1u;
     const uint32_t i = k ? a.perm[j] : 0u;
     const uint32_t kl = k ? a.key_off[i + 1] - a.key_off[i] : 0u;
     const uint32_t vl = k ? a.val_off[i + 1] - a.val_off[i] : 0u;
@@ -822,6 +932,7 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
       a.okey_off[o] = uint32_t(ko);
       a.oval_off[o] = uint32_t(vo);
       a.ots[o] = a.ts[i];
+      if (a.ksame) a.ksame[o] = uint8_t(kf >> 1);
     }
     const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
     const bool staged = K1 - K0 + kb <= kGKImg && V1 - V0 + vb <= kGVImg;
@@ -912,6 +1023,8 @@ struct RotArgs {
   uint32_t* FL;             // flevels x (n_max + 1): F^(2^k); level 0 is F
   uint32_t flevels;
   uint64_t* sstate;         // kShardWords: the carry step's result
+  const uint8_t* ksame;     // two-level merge: same_as_last_key per entry from the rules loop
+                            // (null: a key equal to its predecessor's)
 };
 
 // sstate words
@@ -953,7 +1066,8 @@ __global__ __launch_bounds__(256) void rot_adj_kernel(RotArgs a) {
     const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
     int ord = 0;
     const uint32_t lcp = glcp(K, pp, pl, kp, kl, &ord);
-    al = (lcp < kRotLcp ? lcp : kRotLcp) | (ord > 0 ? kRotUnsorted : 0u) | (ord == 0 ? kRotSame : 0u);
+    const bool same = a.ksame ? a.ksame[e] != 0 : ord == 0;
+    al = (lcp < kRotLcp ? lcp : kRotLcp) | (ord > 0 ? kRotUnsorted : 0u) | (same ? kRotSame : 0u);
   }
   a.alcp[e] = al;
 }
@@ -1344,6 +1458,7 @@ struct Carve {
 struct MergePlan {
   MergeArgs m;
   uint32_t* keep;
+  uint8_t* ksame;    // two-level: same_as_last_key per kept entry
   uint64_t* gtile;   // 6 per gather tile
   uint64_t gtiles;
   uint64_t bytes;
@@ -1365,6 +1480,7 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   P.m.perm = cv.take<uint32_t>(n + 1);
   P.m.mstats = cv.take<uint64_t>(8);
   P.keep = cv.take<uint32_t>(n + 1);
+  P.ksame = cv.take<uint8_t>(n + 1);
   P.gtiles = (n + kGTile - 1) / kGTile + 1;
   P.gtile = cv.take<uint64_t>(6 * P.gtiles);
   P.bytes = cv.off;
@@ -1380,7 +1496,7 @@ int ensure_ws(lsmblk_ctx* c, uint64_t bytes) {
 int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                         uint32_t rules, uint64_t wm, int bottom, const uint8_t* pfx, const uint32_t* pfx_off,
                         uint32_t npfx, const lsmblk_key_range* range, const lsmblk_kv_stream* out, uint64_t* stats,
-                        hipStream_t st, MergePlan* plan_out) {
+                        hipStream_t st, MergePlan* plan_out, uint32_t two) {
   const uint64_t n = in->n;
   MergePlan P = plan_merge(nullptr, n, nrun);
   int rc = ensure_ws(c, P.bytes);
@@ -1393,6 +1509,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   m.n = n;
   m.run_start = run_start;
   m.nrun = nrun;
+  m.two = two;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (n == 0) {
     hipLaunchKernelGGL(merge_empty_kernel, dim3(1), dim3(64), 0, st, m.mstats, out->key_off, out->val_off,
@@ -1437,7 +1554,10 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   g.stats = stats;
   g.merr = m.mstats + 3;
   g.range = range ? *range : lsmblk_key_range{};
+  g.two = two;
+  g.ksame = two && rules ? P.ksame : nullptr;
   const uint32_t gt = uint32_t((n + kGTile - 1) / kGTile);
+  if (two && rules) hipLaunchKernelGGL(mgroup_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, g);
   hipLaunchKernelGGL(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
   hipLaunchKernelGGL(mscan_kernel, dim3(1), dim3(1024), 0, st, g);
   hipLaunchKernelGGL(mwrite_kernel, dim3(gt), dim3(256), 0, st, g);
@@ -1591,6 +1711,7 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const 
   int rc = check_merge_args(c, in, run_start, nrun, kept, stats);
   if (rc) return rc;
   if (!o || (o->nprefix && (!o->prefixes || !o->prefix_off))) return LSMBLK_E_INVAL;
+  if (o->merge_mode != LSMBLK_MERGE_RUNS) return LSMBLK_E_INVAL;  // key ranges: run-priority merge only
   if (range && ((range->has_lo && range->lo_len && !range->lo) || (range->has_hi && range->hi_len && !range->hi)))
     return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1600,7 +1721,7 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const 
   if (hipMemsetAsync(stats + 4, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
   MergePlan MP{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
-                                o->nprefix, range, kept, stats, st, &MP)))
+                                o->nprefix, range, kept, stats, st, &MP, 0)))
     return rc;
   if (in->n) hipLaunchKernelGGL(copy_u64_kernel, dim3(1), dim3(64), 0, st, stats + 4, MP.m.mstats);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
@@ -1681,7 +1802,19 @@ int lsmblk_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t
   DeviceGuard dg(c->device);
   if (!dg.ok) return LSMBLK_E_HIP;
   return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, nullptr, out, stats,
-                             reinterpret_cast<hipStream_t>(stream), nullptr);
+                             reinterpret_cast<hipStream_t>(stream), nullptr, 0);
+}
+
+int lsmblk_merge_batch_ex(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                          uint32_t merge_mode, const lsmblk_kv_stream* out, uint64_t* stats, void* stream) {
+  int rc = check_merge_args(c, in, run_start, nrun, out, stats);
+  if (rc) return rc;
+  if (merge_mode != LSMBLK_MERGE_RUNS && merge_mode != LSMBLK_MERGE_TWO_LEVEL) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, nullptr, out, stats,
+                             reinterpret_cast<hipStream_t>(stream), nullptr, merge_mode == LSMBLK_MERGE_TWO_LEVEL);
 }
 
 int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_t block_size,
@@ -1720,7 +1853,9 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if (!o || !out || !blk_off || !sst_start || !sst_blk || sst_cap < 2 || blk_cap == 0) return LSMBLK_E_INVAL;
   if (o->block_size == 0 || o->target_sst_size == 0 || (o->nprefix && (!o->prefixes || !o->prefix_off)))
     return LSMBLK_E_INVAL;
+  if (o->merge_mode != LSMBLK_MERGE_RUNS && o->merge_mode != LSMBLK_MERGE_TWO_LEVEL) return LSMBLK_E_INVAL;
   if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return LSMBLK_E_INVAL;
+  const uint32_t two = o->merge_mode == LSMBLK_MERGE_TWO_LEVEL;
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
   if (!dg.ok) return LSMBLK_E_HIP;
@@ -1738,7 +1873,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
   MergePlan MP{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
-                                o->nprefix, nullptr, kept, fst, st, &MP)))
+                                o->nprefix, nullptr, kept, fst, st, &MP, two)))
     return rc;
   R = plan_rot(c->cws, M.bytes, n, o->target_sst_size);
   hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
@@ -1751,6 +1886,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   r.starts = sst_start;
   r.sst_cap = sst_cap;
   r.stats = rst;
+  r.ksame = two ? MP.ksame : nullptr;
   if ((rc = rotation_locked(c, r, st))) return rc;
   lsmblk_kv_stream ks = *kept;
   ks.n = n;  // bound; the encode reads the kept count from fst[0]

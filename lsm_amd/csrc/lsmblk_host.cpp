@@ -400,6 +400,23 @@ int lsmblk_memtable_get(lsmblk_memtable* m, const uint8_t* key, size_t klen, con
   return 1;
 }
 
+int lsmblk_memtable_get_copy(lsmblk_memtable* m, const uint8_t* key, size_t klen, uint8_t* val, size_t cap,
+                             size_t* vlen, uint64_t* ts) {
+  if (!m || (klen && !key) || !vlen || (cap && !val)) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(m->mu);
+  auto it = m->map.find(std::string(reinterpret_cast<const char*>(key), klen));
+  if (it == m->map.end()) {
+    *vlen = 0;
+    return 0;
+  }
+  const std::string& v = it->second.val;
+  *vlen = v.size();
+  if (ts) *ts = it->second.ts;
+  if (v.size() > cap) return LSMBLK_E_CAPACITY;
+  if (!v.empty()) std::memcpy(val, v.data(), v.size());  // under the lock: a put may replace it
+  return 1;
+}
+
 size_t lsmblk_memtable_len(lsmblk_memtable* m) {
   if (!m) return 0;
   std::lock_guard<std::mutex> g(m->mu);

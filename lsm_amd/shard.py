@@ -440,7 +440,12 @@ def _compact_dist(shards, group):
     for s in shards:
         if s.dev.type == "cuda":
             torch.cuda.synchronize(s.dev)   # the carry-in may come from another range's stream
-        c = s.carry(c.to(s.dev)).clone()
+            with torch.cuda.stream(s.stream):  # the carry kernel and its copy on the shard's stream
+                c = s.carry(c.to(s.dev)).clone()
+        else:
+            c = s.carry(c.to(s.dev)).clone()
+    if shards[-1].dev.type == "cuda":
+        shards[-1].stream.synchronize()     # the carry-out is read on the exchange's stream
     if rank + 1 < world:
         dist.send(c.to(cdev), dst=rank + 1, group=group)
     for s in shards:

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import batch
-from ._lib import LsmBlkError, check, lib
+from ._lib import LSMBLK_E_CAPACITY, LsmBlkError, check, lib
 
 
 class MemTable:
@@ -41,11 +41,18 @@ class MemTable:
         check(lib().lsmblk_memtable_put(self.h, key, len(key), ts, value, len(value)), "memtable put")
 
     def get(self, key: bytes):
-        v, n, t = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_uint64()
-        found = lib().lsmblk_memtable_get(self.h, key, len(key), ctypes.byref(v), ctypes.byref(n), ctypes.byref(t))
+        """(value, ts) or None; the value is copied under the memtable's lock."""
+        n, t = ctypes.c_size_t(), ctypes.c_uint64()
+        buf = ctypes.create_string_buffer(256)
+        for _ in range(8):  # a concurrent put may grow the value between the size probe and the copy
+            found = lib().lsmblk_memtable_get_copy(self.h, key, len(key), buf, len(buf), ctypes.byref(n),
+                                                   ctypes.byref(t))
+            if found != LSMBLK_E_CAPACITY:
+                break
+            buf = ctypes.create_string_buffer(max(n.value, 1))
         if found < 0:
             raise LsmBlkError(found, "memtable get")
-        return (ctypes.string_at(v, n.value) if n.value else b"", t.value) if found else None
+        return (buf.raw[:n.value], t.value) if found else None
 
     def __len__(self):
         return lib().lsmblk_memtable_len(self.h)

@@ -318,6 +318,45 @@ def merge_runs(runs):
     return drain(MergeIterator([ListIter(r) for r in runs]))
 
 
+def two_merge_iter(runs):
+    """The iterator compact() hands to compact_generate_sst (src/compact.rs:170-173, 206-215):
+    TwoMergeIterator(MergeIterator(runs[:-1]), runs[-1] as the lower level's SstConcatIterator)."""
+    return TwoMergeIterator(MergeIterator([ListIter(r) for r in runs[:-1]]), ListIter(runs[-1]))
+
+
+def two_merge_runs(runs):
+    return drain(two_merge_iter(runs))
+
+
+def two_merge_rule(runs):
+    """The closed form the GPU evaluates for LSMBLK_MERGE_TWO_LEVEL (lsmblk_compact.hip), b =
+    runs[-1]: nothing past b's last key kb (and nothing at all for an empty b); a key of the upper
+    runs only: its lowest-index upper run's versions (below kb); a key of b only: all of b's
+    versions; a key of both: b's 2nd, 4th, ... versions, then (below kb) the upper run's."""
+    upper, b = runs[:-1], runs[-1]
+    if not b:
+        return []
+    kb = b[-1][0]
+    owner, av, bv = {}, {}, {}
+    for r, run in enumerate(upper):
+        for e in run:
+            if owner.setdefault(e[0], r) == r:
+                av.setdefault(e[0], []).append(e)
+    for e in b:
+        bv.setdefault(e[0], []).append(e)
+    out = []
+    for k in sorted(set(av) | set(bv)):
+        if k > kb:
+            break
+        if k in av:
+            out += bv.get(k, [])[1::2]
+            if k < kb:
+                out += av[k]
+        else:
+            out += bv[k]
+    return out
+
+
 def merge_runs_rule(runs):
     """The closed form the GPU merge evaluates: for every user key, all the versions held by the
     lowest-index run containing that key, in that run's order; keys ascending."""

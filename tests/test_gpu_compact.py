@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from lsm_amd import batch, synth
-from lsm_amd._lib import LSMBLK_E_INVAL, LSMBLK_E_MALFORMED, LsmBlkError
+from lsm_amd._lib import LSMBLK_E_INVAL, LSMBLK_E_MALFORMED, LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LsmBlkError
 from oracle import oracle as O
 from oracle import pyref
 
@@ -121,6 +121,107 @@ def test_merge_errors():
     with pytest.raises(LsmBlkError) as e:
         batch.merge_runs(to_dev(bad), rs)
     assert e.value.status == LSMBLK_E_MALFORMED
+
+
+# ---------------------------------------------------------------- two-level (TwoMergeIterator) input
+from test_merge_oracle import DIFF_CLASSES, WEEK1_DAY5  # noqa: E402  (fixture tables, CPU-side data)
+
+TWO = LSMBLK_MERGE_TWO_LEVEL
+
+
+def gpu_merge_mode(runs, mode):
+    kv, rs = kv_runs(runs)
+    return dev_entries(batch.merge_runs(to_dev(kv), rs, merge_mode=mode))
+
+
+def ref_compact(it, wm, bottom, pf, bs, target):
+    try:
+        return pyref.compact_generate_sst(it, wm, bottom, pf, bs, target)
+    except AssertionError:  # the reference panics building an empty SST
+        return None
+
+
+def check_compact_mode(runs, mode, wm, bottom, pf, bs, target):
+    """lsmblk_compact_batch in `mode` == compact_generate_sst over MergeIterator(runs) (RUNS) or over
+    TwoMergeIterator(MergeIterator(runs[:-1]), runs[-1]) (TWO_LEVEL), line by line."""
+    it = pyref.two_merge_iter(runs) if mode == TWO else pyref.MergeIterator([pyref.ListIter(r) for r in runs])
+    want = ref_compact(it, wm, bottom, pf, bs, target)
+    kv, rs = kv_runs(runs)
+    got = batch.compact_runs(to_dev(kv), rs, wm, bottom, pf, bs, target, merge_mode=mode)
+    if want is None:
+        assert got["stats"][2] == 0 and got["stats"][5] == 0
+        return got
+    assert dev_entries(got["kept"]) == [e for _, es in want for e in es]
+    assert got["blocks"].cpu().numpy().tobytes() == b"".join(b for sst, _ in want for b in sst)
+    np.testing.assert_array_equal(np.diff(got["sst_blk"].cpu().numpy().view(np.uint32).astype(np.int64)),
+                                  [len(s) for s, _ in want])
+    np.testing.assert_array_equal(np.diff(got["sst_start"].cpu().numpy().view(np.uint32).astype(np.int64)),
+                                  [len(e) for _, e in want])
+    return got
+
+
+@pytest.mark.parametrize("case", sorted(WEEK1_DAY5))
+def test_week1_day5_fixtures_through_hip(case):
+    """src/tests/week1_day5.rs:15-129 through lsmblk_merge_batch_ex and lsmblk_compact_batch with b
+    (the lower level) as the last run: LSMBLK_MERGE_RUNS meets every expectation; TWO_LEVEL gives
+    what two_merge_iterator.rs as written gives (merge_2, merge_3, merge_4a differ)."""
+    a, b, want = WEEK1_DAY5[case]
+    assert gpu_merge_mode([a, b], LSMBLK_MERGE_RUNS) == want
+    assert gpu_merge_mode([a, b], TWO) == pyref.two_merge_runs([a, b])
+    for mode in (LSMBLK_MERGE_RUNS, TWO):
+        check_compact_mode([a, b], mode, 0, False, (), 4096, 1 << 20)
+        check_compact_mode([a, b], mode, 0, False, (), 16, 40)  # one entry per block, several SSTs
+
+
+@pytest.mark.parametrize("case", sorted(DIFF_CLASSES))
+def test_two_merge_difference_classes_through_hip(case):
+    runs, runs_merge, two_merge = DIFF_CLASSES[case]
+    assert gpu_merge_mode(runs, LSMBLK_MERGE_RUNS) == runs_merge
+    assert gpu_merge_mode(runs, TWO) == two_merge
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_two_level_random_runs_vs_iterator(seed):
+    """Multi-version b, empty runs, upper keys past b's last key; the compaction rules over the
+    two-level order (b's older versions before a's newer ones) run as the reference's loop."""
+    rng = np.random.default_rng(300 + seed)
+    runs = random_runs(rng, int(rng.integers(1, 6)), int(rng.integers(1, 150)), max_versions=5, maxlen=7)
+    assert gpu_merge_mode(runs, TWO) == pyref.two_merge_runs(runs)
+    for wm, bottom, pf, bs, target in ((0, False, (), 64, 200), (500, True, (), 128, 300),
+                                       (500, False, (b"a",), 96, 1), (10**6, True, (b"ab",), 4096, 1 << 20),
+                                       (300, True, (b"b",), 48, 100)):
+        check_compact_mode(runs, TWO, wm, bottom, pf, bs, target)
+
+
+def test_two_level_synthetic_and_big_tiles():
+    """Tile-sized inputs (LDS tiles) and one hot key with thousands of versions in a and b (the
+    one-wave global path), against the closed form restated in oracle/pyref.py."""
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(30000, nrun=5, seed=11, versions=3, tombstone=0.1)
+    kv = O.KV(keys, ko, vals, vo, ts)
+    ents = kv.entries()
+    runs = [ents[rs[r]:rs[r + 1]] for r in range(5)]
+    runs[-1] = runs[-1][:len(runs[-1]) * 3 // 4]  # b ends before the upper runs do
+    assert gpu_merge_mode(runs, TWO) == pyref.two_merge_rule(runs)
+    hot, rng = b"hot-key", np.random.default_rng(5)
+    big = []
+    for r in range(4):
+        run = [(b"a%05d" % i, 5, b"v%d" % r) for i in sorted(rng.choice(3000, 200, replace=False))]
+        run += [(hot, int(t), b"h%d" % r) for t in range(3000 - r, 0, -1)]
+        run += [(b"z" * 300 + b"%04d" % i, 1, b"w") for i in sorted(rng.choice(2000, 150, replace=False))]
+        big.append(run)
+    assert gpu_merge_mode(big, TWO) == pyref.two_merge_rule(big)
+    assert gpu_merge_mode(big, LSMBLK_MERGE_RUNS) == pyref.merge_runs_rule(big)
+
+
+def test_two_level_mode_rejected_for_key_ranges():
+    kv, rs = kv_runs([kvs([("a", "1")]), kvs([("b", "2")])])
+    d = to_dev(kv)
+    opts = batch.compact_opts(0, False, (), 4096, 1 << 20, merge_mode=TWO)
+    kept = batch.KVStream.empty(d.n, 16, 16, torch.device("cuda"))
+    stats = torch.zeros(5, dtype=torch.int64, device="cuda")
+    with pytest.raises(LsmBlkError) as e:
+        batch.compact_merge_into(d, batch._u32_table(rs, "cuda"), 2, opts, None, kept, stats)
+    assert e.value.status == LSMBLK_E_INVAL
 
 
 # ---------------------------------------------------------------- SST rotation

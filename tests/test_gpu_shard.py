@@ -153,3 +153,47 @@ def test_ranges_read_only_their_blocks_decode_merge_encode():
     res, _ = run_ranges(None, None, opts, splitters, inputs)
     want, kept, bases = check_against_single_stream(kv, rs, res, wm, True, bs, target)
     check_each_range_against_resumed_oracle(kept, res, bases, bs, target)
+
+
+def _shards_on_own_streams(d, rs, opts, splitters):
+    out = []
+    for r in range(len(splitters) + 1):
+        lo, hi = shard.range_of(r, splitters)
+        out.append(shard.RangeShard(d, rs, opts, lo, hi, stream=torch.cuda.Stream()))
+    return out
+
+
+def test_ranges_on_distinct_streams_local():
+    """compact_local with every RangeShard on its own HIP stream: the carry chain crosses streams."""
+    rng = np.random.default_rng(21)
+    kv, rs = case(77, versions=2, nkeys=8000)
+    d = to_dev(kv)
+    bs, target, wm = 1024, 8 << 10, int(kv.ts.max()) // 2
+    opts = batch.compact_opts(wm, True, block_size=bs, target_sst_size=target)
+    res = shard.compact_local(_shards_on_own_streams(d, rs, opts, pick_splitters(kv, rng, 5)))
+    check_against_single_stream(kv, rs, res, wm, True, bs, target)
+
+
+def test_ranges_on_distinct_streams_compact_dist_single_rank():
+    """compact_dist's driver (gloo, world 1, R = 4 ranges on distinct streams): the ranges' carry
+    chain and the carry-out read after it, each on the right stream."""
+    import os
+    import socket
+    import torch.distributed as dist
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(22)
+        kv, rs = case(78, versions=3, nkeys=6000)
+        d = to_dev(kv)
+        bs, target = 4096, 24 << 10
+        opts = batch.compact_opts(0, False, block_size=bs, target_sst_size=target)
+        res = shard.compact_dist(_shards_on_own_streams(d, rs, opts, pick_splitters(kv, rng, 3)))
+        check_against_single_stream(kv, rs, res, 0, False, bs, target)
+    finally:
+        dist.destroy_process_group()

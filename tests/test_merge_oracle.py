@@ -108,6 +108,93 @@ def test_two_merge_iterator_quirks_and_intended_regime():
     assert got == [(b"a", 4, b"b4"), (b"a", 9, b"a9"), (b"z", 1, b"z")]
 
 
+# ---------------------------------------------------------------- week1_day5: TwoMergeIterator
+# src/tests/week1_day5.rs:15-129 (MockIterator pairs, ts 0): (a, b, expected), b = the lower level.
+W5_1 = kvs([("a", "1.1"), ("b", "2.1"), ("c", "3.1")])
+W5_2 = kvs([("a", "1.2"), ("b", "2.2"), ("c", "3.2"), ("d", "4.2")])
+W5_3 = kvs([("b", "2.2"), ("c", "3.2"), ("d", "4.2")])
+WEEK1_DAY5 = {
+    "merge_1": (W5_1, W5_2, kvs([("a", "1.1"), ("b", "2.1"), ("c", "3.1"), ("d", "4.2")])),      # :16-38
+    "merge_2": (W5_2, W5_1, kvs([("a", "1.2"), ("b", "2.2"), ("c", "3.2"), ("d", "4.2")])),      # :41-63
+    "merge_3": (W5_3, W5_1, kvs([("a", "1.1"), ("b", "2.2"), ("c", "3.2"), ("d", "4.2")])),      # :66-87
+    "merge_4a": (W5_3, [], W5_3),                                                                # :90-105
+    "merge_4b": ([], W5_3, W5_3),                                                                # :106-120
+    "merge_5": ([], [], []),                                                                     # :124-129
+}
+# what two_merge_iterator.rs as written yields where it differs from week1_day5's expectation
+TWO_MERGE_AS_WRITTEN = {
+    "merge_2": kvs([("a", "1.2"), ("b", "2.2")]),  # a holds b's last key "c": a's c and d are lost
+    "merge_3": kvs([("a", "1.1"), ("b", "2.2")]),  # b ends after "c": a's c and d are lost
+    "merge_4a": [],                                # empty b: nothing at all
+}
+
+
+@pytest.mark.parametrize("case", sorted(WEEK1_DAY5))
+def test_week1_day5_fixtures(case):
+    """The run-priority merge (LSMBLK_MERGE_RUNS: a's runs first, b last) gives every expectation of
+    week1_day5.rs; the reference's TwoMergeIterator as written fails merge_2, merge_3 and merge_4a."""
+    a, b, want = WEEK1_DAY5[case]
+    for merge in (pyref.merge_runs, pyref.merge_runs_rule, c_merge):
+        assert merge([a, b]) == want
+    got = pyref.two_merge_runs([a, b])
+    assert got == TWO_MERGE_AS_WRITTEN.get(case, want)
+    assert pyref.two_merge_rule([a, b]) == got
+
+
+# Input classes on which the reference binary's compaction input (TwoMergeIterator) differs from
+# the run-priority merge; DESIGN.md section 3 reproduces this table.  (a runs..., b): both outputs.
+DIFF_CLASSES = {
+    "b exhausted before a": (
+        [kvs([("a", "A"), ("x", "X"), ("y", "Y")]), kvs([("a", "b"), ("m", "M")])],
+        kvs([("a", "A"), ("m", "M"), ("x", "X"), ("y", "Y")]),
+        kvs([("a", "A"), ("m", "M")])),
+    "empty b": (
+        [kvs([("a", "A"), ("c", "C")]), []],
+        kvs([("a", "A"), ("c", "C")]),
+        []),
+    "a holds b's last key": (
+        [kvs([("a", "A"), ("m", "M2")]), kvs([("a", "b"), ("m", "M1")])],
+        kvs([("a", "A"), ("m", "M2")]),
+        kvs([("a", "A")])),
+    ">= 2 b versions of a key a holds": (
+        [[(b"k", 9, b"a9")], [(b"k", 5, b"b5"), (b"k", 4, b"b4"), (b"k", 3, b"b3"), (b"k", 2, b"b2"), (b"z", 1, b"z")]],
+        [(b"k", 9, b"a9"), (b"z", 1, b"z")],
+        [(b"k", 4, b"b4"), (b"k", 2, b"b2"), (b"k", 9, b"a9"), (b"z", 1, b"z")]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(DIFF_CLASSES))
+def test_two_merge_difference_classes(case):
+    runs, runs_merge, two_merge = DIFF_CLASSES[case]
+    assert pyref.merge_runs(runs) == runs_merge == pyref.merge_runs_rule(runs)
+    assert pyref.two_merge_runs(runs) == two_merge == pyref.two_merge_rule(runs)
+    assert runs_merge != two_merge
+
+
+def test_two_merge_agrees_in_the_intended_regime():
+    """One version per key in b and b's last key above every upper key: the two modes agree."""
+    rng = np.random.default_rng(7)
+    for _ in range(30):
+        runs = random_runs(rng, int(rng.integers(2, 6)), 40, max_versions=3)
+        b = sorted({e[0] for r in runs[:-1] for e in r} | {e[0] for e in runs[-1]})
+        runs[-1] = [(k, 0, b"lower") for k in b] + [(b"\xff", 0, b"end")]
+        assert pyref.two_merge_runs(runs) == pyref.merge_runs(runs)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_two_merge_rule_equals_iterator(seed):
+    """The closed form the GPU evaluates == two_merge_iterator.rs line by line, on random runs with
+    multi-version keys in b, empty runs, upper keys beyond b's last key."""
+    rng = np.random.default_rng(1000 + seed)
+    runs = random_runs(rng, int(rng.integers(1, 6)), int(rng.integers(1, 50)), max_versions=5)
+    assert pyref.two_merge_rule(runs) == pyref.two_merge_runs(runs)
+
+
+def compact_two_ref(runs, wm, bottom, pf, bs, target):
+    """compact_generate_sst over the reference's TwoMergeIterator input, line by line."""
+    return pyref.compact_generate_sst(pyref.two_merge_iter(runs), wm, bottom, pf, bs, target)
+
+
 def compact_ref(runs, wm, bottom, pf, bs, target):
     """compact_generate_sst over MergeIterator (restated line by line): [(blocks, entries)]."""
     return pyref.compact_generate_sst(pyref.MergeIterator([pyref.ListIter(r) for r in runs]),

@@ -173,3 +173,20 @@ def test_gpu_sst_read_blocks_round_trip_and_crc():
     bad[t.block_meta[mid].offset + 3] ^= 0x40
     with pytest.raises(LsmBlkError):
         S.SsTable(bytes(bad)).decode_blocks()
+
+
+def test_memtable_get_copies_under_the_lock():
+    """get() copies the value under the memtable's lock (lsmblk_memtable_get_copy): values larger
+    than the first buffer, replaced values, absent keys, and the capacity error of the raw call."""
+    import ctypes
+    from lsm_amd._lib import LSMBLK_E_CAPACITY, lib
+    mt = S.MemTable()
+    mt.put(b"k", 1, b"x" * 5000)
+    assert mt.get(b"k") == (b"x" * 5000, 1)
+    mt.put(b"k", 2, b"short")
+    assert mt.get(b"k") == (b"short", 2) and mt.get(b"nope") is None
+    mt.put(b"e", 3, b"")
+    assert mt.get(b"e") == (b"", 3)
+    n, t, buf = ctypes.c_size_t(), ctypes.c_uint64(), ctypes.create_string_buffer(2)
+    assert lib().lsmblk_memtable_get_copy(mt.h, b"k", 1, buf, 2, ctypes.byref(n), ctypes.byref(t)) == LSMBLK_E_CAPACITY
+    assert n.value == 5 and t.value == 2

@@ -46,6 +46,20 @@ def functions():
         yield name, f"    pub fn {name}({', '.join(params)}){r};"
 
 
+def splice(doc):
+    """INTEGRATION.md with its extern block replaced by the current header's functions."""
+    head, rest = doc.split('extern "C" {\n', 1)
+    _, tail = rest.split("\n}\n", 1)
+    body = "\n".join(line for _, line in functions())
+    return head + 'extern "C" {\n' + body + "\n}\n" + tail
+
+
 if __name__ == "__main__":
-    for _, line in functions():
-        print(line)
+    import sys
+    if "--write" in sys.argv:
+        p = os.path.join(ROOT, "INTEGRATION.md")
+        doc = splice(open(p).read())
+        open(p, "w").write(doc)
+    else:
+        for _, line in functions():
+            print(line)
