@@ -24,10 +24,12 @@ def _random_bytes(rng, n):
 
 def _sorted_keys16(rng, n, key_slice=(0, 1)):
     """n sorted unique 16-B keys spread uniformly over the 128-bit space, or over slice s of w
-    equal slices of it (key_slice = (s, w): a storage shard of a key-range-partitioned dataset)."""
-    s, w = key_slice
+    equal slices of it (key_slice = (s, w): a storage shard of a key-range-partitioned dataset),
+    or over `span` consecutive slices from s (key_slice = (s, w, span))."""
+    s, w = key_slice[:2]
+    span = key_slice[2] if len(key_slice) > 2 else 1
     width = (2 ** 64 - 1) // w
-    step = np.uint64(width // max(n, 1))
+    step = np.uint64(width * span // max(n, 1))
     hi = np.uint64(s * width) + np.arange(n, dtype=np.uint64) * step + rng.integers(0, int(step), n, dtype=np.uint64)
     lo = rng.integers(0, 2 ** 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
     k = np.empty((n, 16), np.uint8)

@@ -93,3 +93,23 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 2 and r.stdout == ""
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("world,fail", [(2, 1), (3, 0)])
+def test_bench_launcher_fails_fast_when_a_rank_dies(world, fail):
+    """One rank exits early (before joining the gloo group, so the others block in the
+    rendezvous): the launcher terminates the rest and returns non-zero within seconds, printing
+    no bench line."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run",
+                        "--dry-run-fail-rank", str(fail)], capture_output=True, text=True, timeout=100, env=env)
+    dt = time.time() - t0
+    assert r.returncode != 0 and r.stdout.strip() == "", (r.returncode, r.stdout)
+    assert f"rank {fail} exited with status 3" in r.stderr
+    assert dt < 60, dt

@@ -198,6 +198,54 @@ def test_oversize_entries_and_u16_wrap():
     np.testing.assert_array_equal(blocks.cpu().numpy(), ref_blocks)
 
 
+def _encode_and_decode_like_oracle(kv, seg, bs):
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, bs)
+    assert rc == 0
+    blocks, blk_off = batch.encode_kv(to_dev(kv), seg, bs)
+    np.testing.assert_array_equal(blk_off.cpu().numpy().view(np.uint64), ref_off)
+    got = blocks.cpu().numpy()
+    assert len(got) == len(ref_blocks) and np.flatnonzero(got != ref_blocks).size == 0
+    # the wrapped blocks do not decode to the input; the GPU must decode (or reject) them exactly
+    # as the oracle's Block::decode + iterator restatement does
+    rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
+    db, do = dev_blocks(ref_blocks, ref_off)
+    if rc == 0:
+        assert_kv_equal(batch.decode_blocks(db, do), ref_kv)
+    else:
+        with pytest.raises(LsmBlkError) as e:
+            batch.decode_blocks(db, do)
+        assert e.value.status == rc
+    return ref_blocks, ref_off, rc
+
+
+def test_u16_wrap_long_keys_prefix_and_suffix_len():
+    """builder.rs:63-64: `prefix as u16` and `(key_len - prefix) as u16` for keys of 64 KiB and
+    more (block_size 1 MiB, so several such keys share a block)."""
+    rng = np.random.default_rng(17)
+    base = bytes(rng.integers(0, 256, 70000, dtype=np.uint8))
+    ents = [(base + b"%03d" % i, 10 + i, b"val%d" % i) for i in range(12)]
+    ents += [(b"\xff" * 66000 + b"%02d" % i, 99, b"") for i in range(3)]  # suffix_len wraps too
+    kv = O.KV.from_entries(ents)
+    blocks, off, rc = _encode_and_decode_like_oracle(kv, [0, kv.n], 1 << 20)
+    assert len(off) == 2
+    e1 = 4 + len(ents[0][0]) + 10 + len(ents[0][2])  # entry 1's offset
+    lcp = next(i for i, (x, y) in enumerate(zip(ents[0][0], ents[1][0])) if x != y)
+    assert int.from_bytes(bytes(blocks[e1:e1 + 2]), "big") == lcp & 0xFFFF and lcp > 65535
+
+
+def test_u16_wrap_offsets_and_entry_count_big_block_size():
+    """builder.rs:61 (`offset as u16`) and block.rs:20 (`offsets.len() as u16`): block_size
+    2 MiB > 65538, 70000 entries in one block: offsets past 64 KiB and the count wrap."""
+    n = 70000
+    ents = [(int(i).to_bytes(3, "big"), i, b"") for i in range(1, n + 1)]
+    kv = O.KV.from_entries(ents)
+    blocks, off, rc = _encode_and_decode_like_oracle(kv, [0, kv.n], 2 << 20)
+    assert len(off) == 2
+    assert int.from_bytes(bytes(blocks[-2:]), "big") == n & 0xFFFF
+    # and a batch mixing wrapped and ordinary blocks: segments of 20000 entries each
+    _encode_and_decode_like_oracle(kv, [0, 5, 20005, 40005, n], 1 << 20)
+
+
 def test_one_entry_segments():
     kv = O.KV(*synth.gen_uniform(500, seed=9))
     roundtrip_check(kv, np.arange(kv.n + 1, dtype=np.uint32), 4096)
