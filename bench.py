@@ -72,6 +72,8 @@ def parse(argv=None):
                    help="launcher self-test: ranks join a gloo group and report the world, no GPU work")
     p.add_argument("--dry-run-fail-rank", type=int, default=None,
                    help="launcher self-test: this rank exits with status 3 before joining the group")
+    p.add_argument("--decode-two-pass", action="store_true",
+                   help="diagnostics (A/B): count + scan + decode instead of the single-pass decode")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
     return p.parse_args(argv)
@@ -203,6 +205,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     stream = torch.cuda.current_stream(dev)
     ctx = batch._ctx(local, stream)
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
+    check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
 
     def step(ev=None):
         if ev is not None:
@@ -943,7 +946,7 @@ def kernel_times(ctx, step, dev, reps=3, lead=3):
 def ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream):
     from lsm_amd._lib import lib as L
     res = {}
-    for mask in sorted({0, 1, 2, 4, 8, 14, 15, args.ablate}):
+    for mask in sorted({0, 2, 4, 8, 14, 1024, 2048, 3072, args.ablate}):
         check(L().lsmblk_debug_set(ctx, 1, mask))
         for _ in range(2):
             batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)

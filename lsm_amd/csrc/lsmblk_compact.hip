@@ -33,19 +33,13 @@
 
 namespace {
 
-#ifndef LSMBLK_MS
-#define LSMBLK_MS 128
-#endif
-constexpr uint32_t kMS = LSMBLK_MS;  // every kMS-th entry of a run is a merge candidate
+constexpr uint32_t kMS = 128;  // every kMS-th entry of a run is a merge candidate
 constexpr uint32_t kMaxRuns = 64;   // runs per merge (one lane per run in the tile kernels)
-#ifndef LSMBLK_MTE
-#define LSMBLK_MTE 512
-#endif
 // Tile entries with LDS tables (larger tiles: the one-wave global path).  Tile sizes are about
 // exponential with mean kMS (the gaps between consecutive candidates of all runs), so the limit
 // trades the global path's share against residency: merge_tile on config C took 5.3 / 3.1 / 2.8 /
 // 2.8 / 3.5 / 6.9 ms at 256 / 384 / 512 / 640 / 1024 / 2048.
-constexpr uint32_t kMTE = LSMBLK_MTE;
+constexpr uint32_t kMTE = 512;
 constexpr uint32_t kMTT = 128;      // threads per tile workgroup
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 

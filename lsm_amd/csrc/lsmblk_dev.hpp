@@ -146,7 +146,7 @@ __device__ __forceinline__ void publish(uint64_t* arr, uint64_t idx, const uint6
 // Wave-parallel decoupled look-back: lane j inspects predecessor (pred - j).  Returns false
 // on timeout (then excl is garbage and the caller raises LSMBLK_ERR_TIMEOUT).
 template <int NQ>
-__device__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self, uint32_t tag,
+__device__ __forceinline__ bool lookback(const uint64_t* agg, const uint64_t* inc, uint64_t self, uint32_t tag,
                          uint32_t poll, uint64_t (&excl)[NQ]) {
   const uint32_t l = lane_id();
   const uint64_t want_agg = (uint64_t(tag) << 2) | 1, want_inc = (uint64_t(tag) << 2) | 2;
@@ -264,17 +264,10 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint8_t* base, uint32_t x
 // Store bytes [lo, hi) (0 <= lo < hi <= 16) of a 16-B chunk at dst (16-aligned): one b128
 // store when whole, else conditional whole-dword stores plus at most three bytes at each
 // end (closed-form; a wave pays ~10 stores for its partial lanes, not 16 byte stores).
-#ifndef LSMBLK_NT_STORE
-#define LSMBLK_NT_STORE 1  // U: 735 vs 722 GiB/s (nt loads: no gain)
-#endif
 __device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4], uint32_t lo, uint32_t hi) {
   if (lo == 0 && hi == 16) {
-    u32x4 q = {v[0], v[1], v[2], v[3]};
-#if LSMBLK_NT_STORE
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(dst));  // streamed: written once, read by a later pass
-#else
-    *reinterpret_cast<u32x4*>(dst) = q;
-#endif
+    // streamed: written once, read by a later pass (nt stores: U 735 against 722 GiB/s)
+    __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<u32x4*>(dst));
     return;
   }
   const uint32_t lo4 = (lo + 3) >> 2, hi4 = hi >> 2;  // whole dwords [lo4, hi4)
@@ -465,9 +458,12 @@ struct lsmblk_ctx {
   uint64_t seg_cap = 0;
   uint32_t* rec_first = nullptr; // n+1
   uint32_t* blk_first = nullptr;
-  uint32_t* ent = nullptr;       // 3 per entry: rec, alcp, block sizes (plan passes)
+  uint32_t* ent = nullptr;       // per (segment-local) block: its encoded size (plan walk)
   uint32_t* big_list = nullptr;  // n+1 u32: emit_big_kernel's per-block flags (bytes)
   uint64_t rec_cap = 0;
+  uint64_t* d1_gran = nullptr;   // single-pass decode look-back granules (uncached): 3 + 3 per tile of
+  uint64_t d1_blk_cap = 0;       //   kDW blocks (aggregate, inclusive prefix); blocks covered
+  bool dec_two_pass = false;     // diagnostics: the count + scan + decode path instead (A/B)
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
   uint32_t skip = 0;             // decode ablation mask (timing experiments only)

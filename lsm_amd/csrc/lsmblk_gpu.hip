@@ -40,26 +40,24 @@ struct DecodeArgs {
   uint64_t* ts;
   uint64_t entry_cap, key_cap, val_cap;
   uint64_t* stats;
-  const uint32_t* agg;        // per-block (entries, key bytes, value bytes), from dec_count_kernel
+  const uint32_t* agg;        // per-block (entries, key bytes, value bytes), from the count pass (dec_count_staged_kernel or the CRC pass)
   const uint64_t* tile_pre;   // per-tile exclusive prefix (entries, key bytes, value bytes)
   uint32_t tail;              // bytes after each block inside its range (4: the framing CRC)
   uint64_t* blk_ent;          // optional: first entry index of every block
   uint32_t skip;  // ablation mask (lsmblk_debug_set, timing experiments only): 2 keys,
                   // 4 values, 8 per-entry metadata, 256 stop after staging, 512 after the tables
+  // single-pass decode (decode1_kernel): look-back state, uncached granules tagged with `tag`
+  uint64_t* tagg;             // 3 per kDW-block tile: the tile's (entries, key bytes, value bytes)
+  uint64_t* tinc;             // 3 per tile: inclusive prefix through the tile
+  uint32_t tag, poll;
 };
 
 constexpr uint32_t kTile = 64;  // blocks per count tile
 
 // LDS reads per lane issued together before their uses (one LDS round trip per batch instead
 // of one per read): flushes, value copies, chunk moves.
-#ifndef LSMBLK_LDS_BATCH
-#define LSMBLK_LDS_BATCH 2  // decode: 2 measured 1 % faster per step than 1, 4 slower (1.64 vs 1.58 ms)
-#endif
-constexpr uint32_t kLB = LSMBLK_LDS_BATCH;
-#ifndef LSMBLK_EMIT_BATCH
-#define LSMBLK_EMIT_BATCH 1  // emit holds the next block's prefetch: 2 and 4 spill
-#endif
-constexpr uint32_t kEB = LSMBLK_EMIT_BATCH;
+constexpr uint32_t kLB = 2;  // decode: 2 measured 1 % faster per step than 1, 4 slower (1.64 vs 1.58 ms)
+constexpr uint32_t kEB = 1;  // emit holds the next block's prefetch: 2 and 4 spill
 
 
 // LDS per single-wave workgroup is exactly 8 KiB, so 20 blocks are resident per CU (5 waves per
@@ -67,13 +65,13 @@ constexpr uint32_t kEB = LSMBLK_EMIT_BATCH;
 // 16-B lead, plus the 16-B staging round-up, fits the image.
 constexpr uint32_t kDecImg = 4128;  // staged block bytes per wave
 constexpr uint32_t kDecMaxE = 128;  // entries of a fast-path block (tables in registers, 2 per lane)
-constexpr uint32_t kDecOut = 4064;  // LDS output image (keys + values) of a fast-path block
+constexpr uint32_t kDecOut = 4032;  // LDS output image (keys + values) of a fast-path block
 
 struct alignas(16) DecLds {
   uint8_t img[kDecImg];
   alignas(16) uint8_t out[kDecOut];  // decoded key run, then (16-B aligned) value run
 };
-static_assert(sizeof(DecLds) == 8192, "decode LDS: 20 single-wave workgroups per CU");
+static_assert(sizeof(DecLds) == 8160, "decode LDS: 20 blocks per CU, with room for decode1's shared words");
 
 // Entry tables of a large block (kDecMaxE entries at a time).  A large block is not staged, so
 // the tables live in the unused image.
@@ -95,11 +93,8 @@ __device__ __forceinline__ void lds_read16(const uint8_t* base, uint32_t x, uint
   v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
 }
 
-// cache policy of the staging loads (2 = nt: each byte is read once); timing experiments
-#ifndef LSMBLK_NT_LOAD
-#define LSMBLK_NT_LOAD 0
-#endif
-constexpr int kLdAux = LSMBLK_NT_LOAD ? 2 : 0;
+// cache policy of the staging loads (default; nt loads measured no gain)
+constexpr int kLdAux = 0;
 
 struct BlockHdr {
   uint32_t len, n, data_end, fks;
@@ -402,10 +397,7 @@ __device__ __forceinline__ void copy_run(const rsrc_t& RS, uint32_t so, uint32_t
 // The same copy by the whole wave (len >= 16, wave-uniform arguments): lane j moves pieces
 // j, j + 64, ... so a wave instruction moves 1 KiB of contiguous bytes.  Values of
 // kCoop bytes or more go this way: one long value no longer keeps 63 lanes idle.
-#ifndef LSMBLK_COOP
-#define LSMBLK_COOP 16  // M: 799 / 830-846 / 840 GiB/s at 256 / 32 / 16 (every run of 16 B or more packed)
-#endif
-constexpr uint32_t kCoop = LSMBLK_COOP;
+constexpr uint32_t kCoop = 16;  // M: 799 / 830-846 / 840 GiB/s at 256 / 32 / 16 (every run of 16 B or more packed)
 __device__ __forceinline__ void copy_run_wave(const rsrc_t& RS, uint32_t so, const rsrc_t& RD, uint32_t dof,
                                               uint32_t len) {
   const uint32_t l = lane_id();
@@ -700,11 +692,321 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
   decode_block(a, lds, blockIdx.x);
 }
 
+// ---------------------------------------------------------------- single-pass decode
+// E is read once.  A workgroup decodes kDW consecutive blocks, one wave each (a look-back tile).
+// Every wave stages and parses its block as decode_block does and puts the block's (entries,
+// key bytes, value bytes) in LDS.  Wave 0, the tile's leader, then publishes the tile aggregate,
+// finds the tile's base by a decoupled look-back over earlier tiles (uncached granules), publishes
+// the tile's inclusive prefix and hands the base to the other waves through LDS -- while they
+// compose their key and value runs in their LDS output images at 16-B alignment 0, work that needs
+// no base.  The flush reads the image shifted by the base's alignment (unaligned ds_read_b128) and
+// writes aligned 16-B chunks.
+// Measured on the way (1 Mi U blocks): one block per workgroup, with a look-back tile of 16 blocks
+// summed from per-block uncached granules: 3.0 ms, of which the waits were 1.6 ms (an uncached
+// round trip under the full HBM load costs microseconds); with a dispatch ticket per block
+// instead of blockIdx: 12 ms (one atomic on one word by a million waves, ~11 ns each); waiting for
+// tile t-1's inclusive prefix instead of looking back: the prefixes became a serial chain.
+constexpr uint32_t kDW = 4;  // blocks (waves) per workgroup = per look-back tile
+
+__device__ __forceinline__ uint64_t sat47(uint64_t v) { return v > (1ull << 47) - 1 ? (1ull << 47) - 1 : v; }
+
+// Lanes 0..2 publish (x0, x1, x2) as three granules (scalars, not an array the lane would index:
+// that compiled to a scratch round trip).
+__device__ __forceinline__ void publish3(uint64_t* arr, uint64_t idx, uint64_t x0, uint64_t x1, uint64_t x2,
+                                         uint32_t tag, uint32_t flag, uint32_t poll) {
+  const uint32_t l = lane_id();
+  const uint64_t x = l == 0 ? x0 : (l == 1 ? x1 : x2);
+  if (l < 3) gstore(arr + 3 * idx + l, (sat47(x) << 16) | (uint64_t(tag) << 2) | flag, poll);
+}
+
+// The workgroup's shared words (after the waves' images).
+struct Dec1Shared {
+  uint32_t n[kDW], k[kDW], v[kDW];  // the blocks' aggregates (k: saturated at 2^31 - 1)
+  uint32_t ready;                   // bit w: wave w's aggregate is in place
+  uint32_t base_ready;              // the leader's base is in place
+  uint32_t err;                     // the leader's error flags (look-back timeout)
+  uint32_t pad;
+  uint64_t X[3];                    // the tile's base: all earlier tiles' entries, key bytes, value bytes
+};
+static_assert(kDW * sizeof(DecLds) + sizeof(Dec1Shared) <= 32768, "decode1: five workgroups (20 blocks) per CU");
+
+// Sum of the aggregates of all tiles before t: tile t-1's inclusive prefix if it is there at once,
+// else a wave-parallel look-back over the tile aggregates.
+__device__ __forceinline__ bool d1_tiles(const DecodeArgs& a, uint64_t t, uint64_t (&x)[3]) {
+  x[0] = x[1] = x[2] = 0;
+  if (t == 0) return true;
+  const uint32_t l = lane_id();
+  const uint64_t want = (uint64_t(a.tag) << 2) | 2;
+  uint64_t g = want;
+  if (l < 3) g = gload(a.tinc + 3 * (t - 1) + l, 0);
+  if (!__ballot((g & 0xFFFF) != want)) {
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) x[q] = uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(g >> 16), q))) |
+                                          (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(g >> 48), q))) << 32);
+    return true;
+  }
+  return lookback<3>(a.tagg, a.tinc, t, a.tag, a.poll, x);
+}
+
+// The store half of the fast path after the base is known: the key or value run composed at
+// alignment 0 is flushed to its unaligned global place (LDS read shifted back by the base's 16-B
+// phase, aligned 16-B global stores).
+__device__ __forceinline__ void flush_run_shifted(uint8_t* gdst_aligned, const uint8_t* lds_run, uint32_t lo,
+                                                  uint32_t len) {
+  const uint32_t end = lo + len, nc = (end + 15) >> 4;
+  const uint32_t l = lane_id();
+  for (uint32_t c0 = 0; c0 < nc; c0 += 64 * kLB) {
+    u32x4 q[kLB];
+#pragma unroll
+    for (uint32_t j = 0; j < kLB; ++j) {
+      const uint32_t c = c0 + 64 * j + l;
+      if (c < nc) q[j] = *reinterpret_cast<const u32x4*>(lds_run + 16 * c - lo);  // run byte 16 c - lo
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kLB; ++j) {
+      const uint32_t c = c0 + 64 * j + l;
+      if (c < nc) {
+        const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+        store_chunk(gdst_aligned + 16 * c, v, 16 * c < lo ? lo - 16 * c : 0u, min(end - 16 * c, 16u));
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lds_ld_acq(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ void decode1_block(const DecodeArgs& a, DecLds& L, Dec1Shared& S, uint32_t w, uint64_t b) {
+  const uint32_t l = lane_id();
+  uint32_t err = 0;
+  const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
+  uint32_t len = 0;
+  if (end < start + a.tail || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
+  else len = uint32_t(end - start) - a.tail;
+  const uint8_t* bp = a.blocks + start;
+  const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
+  const rsrc_t R = make_rsrc(bp - lead, lead + len);
+  const bool fits = lead + len + 15 <= kDecImg;
+
+  BlockHdr h;
+  if (fits) {
+    const uint32_t nchunk = (lead + len + 15) >> 4;
+    u32x4 v[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
+    wave_sync();
+    h = parse_hdr(LdsImg{L.img, lead}, len);
+  } else {
+    h = parse_hdr(GlbImg{R, lead}, len);
+  }
+  if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
+  const bool fast = fits && h.n <= kDecMaxE;
+  const bool big = !fits;
+
+  uint64_t K = 0, V = 0;
+  bool bad = false;
+  DecEnt ent[2] = {};
+  if (fast) {
+    const LdsImg im{L.img, lead};
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+      if (64 * it >= h.n) break;
+      const uint32_t k = 64 * it + l;
+      uint32_t off = 0, p = 0, s = 0, vl = 0;
+      bool ok = true;
+      if (k < h.n) ok = parse_entry(im, h, k, off, p, s, vl);
+      bad = bad || !ok;
+      const uint32_t kl = p + s;
+      const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
+      ent[it] = DecEnt{off, p, s, uint32_t(K) + ki - kl, uint32_t(V) + vi - vl, vl};
+      K += __shfl(ki, 63, 64);
+      V += __shfl(vi, 63, 64);
+    }
+  } else {
+    for (uint32_t c = 0; c < h.n; c += 64) {
+      const uint32_t k = c + l;
+      uint32_t off = 0, p = 0, s = 0, vl = 0;
+      bool ok = true;
+      if (k < h.n) {
+        if (fits) ok = parse_entry(LdsImg{L.img, lead}, h, k, off, p, s, vl);
+        else ok = parse_entry(GlbImg{R, lead}, h, k, off, p, s, vl);
+      }
+      bad = bad || !ok;
+      K += wave_sum<uint64_t>(p + s);
+      V += wave_sum<uint64_t>(vl);
+    }
+  }
+  if (__ballot(bad)) err |= LSMBLK_ERR_MALFORMED;
+  if (K > 0x7FFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;  // one block's keys cannot fit a batch's u32 offsets anyway
+  uint64_t agg[3] = {h.n, K, V};
+  if (err) agg[0] = agg[1] = agg[2] = 0;
+  // this block's aggregate, for the leader and the later waves of the tile
+  if (l == 0) {
+    S.n[w] = uint32_t(agg[0]);
+    S.k[w] = uint32_t(agg[1]);
+    S.v[w] = uint32_t(agg[2]);
+    __hip_atomic_fetch_or(&S.ready, 1u << w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+
+  const uint64_t t = b / kDW;
+  const uint32_t nw = uint32_t(min(uint64_t(kDW), a.nblk - t * kDW));  // blocks of this tile
+  uint32_t spins = 0;
+  auto lds_wait = [&](const uint32_t* p, uint32_t want_mask) {
+    while ((lds_ld_acq(p) & want_mask) != want_mask) {
+      if (++spins > kSpinLimit) {
+        err |= LSMBLK_ERR_TIMEOUT;
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  if (w == 0) {
+    // leader: the tile aggregate, the look-back, the inclusive prefix, the base for the others
+    lds_wait(&S.ready, (1u << nw) - 1);
+    uint64_t A0 = 0, A1 = 0, A2 = 0;
+    for (uint32_t i = 0; i < nw; ++i) {
+      A0 += S.n[i];
+      A1 += S.k[i];
+      A2 += S.v[i];
+    }
+    publish3(a.tagg, t, A0, A1, A2, a.tag, 1, a.poll);
+    uint64_t X[3];
+    if (!d1_tiles(a, t, X)) {
+      err |= LSMBLK_ERR_TIMEOUT;
+      X[0] = X[1] = X[2] = 0;
+    }
+    publish3(a.tinc, t, X[0] + A0, X[1] + A1, X[2] + A2, a.tag, 2, a.poll);
+    if (l == 0) {
+      S.X[0] = X[0];
+      S.X[1] = X[1];
+      S.X[2] = X[2];
+      S.err = err & LSMBLK_ERR_TIMEOUT;
+      __hip_atomic_store(&S.base_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+
+  // the work that needs no base: the fast path composes its runs at alignment 0
+  const uint32_t vrun = (uint32_t(K) + 15) & ~15u;
+  const bool composed = fast && !err && h.n && vrun + uint32_t(V) + 15 <= kDecOut;
+  if (composed) {
+    dec_entry_runs(a, L, lead, h.n, ent, 0, 0, 0, LdsSink{L.out, 0, vrun}, a.skip | 8);
+    wave_sync();
+  }
+
+  // the base: the tile's base + the tile's earlier blocks
+  if (w != 0) lds_wait(&S.base_ready, 1u);
+  err |= S.err;
+  uint64_t E0 = S.X[0], K0 = S.X[1], V0 = S.X[2];
+  for (uint32_t i = 0; i < w; ++i) {
+    E0 += S.n[i];
+    K0 += S.k[i];
+    V0 += S.v[i];
+  }
+  E0 = uni64(E0);
+  K0 = uni64(K0);
+  V0 = uni64(V0);
+  if (a.blk_ent && l == 0) a.blk_ent[b] = E0;
+  const uint64_t Et = E0 + agg[0], Kt = K0 + agg[1], Vt = V0 + agg[2];
+  if (Kt > 0xFFFFFFFFull || Vt > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+  if (Et > a.entry_cap || Kt > a.key_cap || Vt > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
+  if (b + 1 == a.nblk && l == 0) {  // totals, required sizes and the sentinels (as dec_scan_kernel)
+    if (a.blk_ent) a.blk_ent[a.nblk] = Et;
+    a.stats[0] = Et;
+    a.stats[1] = Kt;
+    a.stats[2] = Vt;
+    if (Et <= a.entry_cap) {
+      a.key_off[Et] = uint32_t(Kt);
+      a.val_off[Et] = uint32_t(Vt);
+    }
+  }
+
+  if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
+    if (composed) {
+      if (!(a.skip & 8)) {
+#pragma unroll
+        for (uint32_t it = 0; it < 2; ++it) {
+          const uint32_t k = 64 * it + l;
+          if (k >= h.n) continue;
+          const uint64_t e = E0 + k;
+          const u32x2 q = *reinterpret_cast<const u32x2*>(L.img + lead + ent[it].epos + 4 + ent[it].s);
+          a.ts[e] = __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
+          a.key_off[e] = uint32_t(K0 + ent[it].kout);
+          a.val_off[e] = uint32_t(V0 + ent[it].vout);
+        }
+      }
+      const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
+      flush_run_shifted(a.keys + (K0 - kb), L.out, kb, uint32_t(K));
+      flush_run_shifted(a.vals + (V0 - vb), L.out + vrun, vb, uint32_t(V));
+    } else if (fast) {
+      dec_fast_outputs(a, L, lead, h, ent, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
+    } else if (big) {
+      DecTables& T = *reinterpret_cast<DecTables*>(L.img);  // large blocks are not staged
+      uint64_t kr = 0, vr = 0;
+      for (uint32_t c0 = 0; c0 < h.n; c0 += kDecMaxE) {
+        const uint32_t cn = min(kDecMaxE, h.n - c0);
+        wave_sync();  // the previous chunk's table reads are done
+        const GlbImg im{R, lead};
+        for (uint32_t c = 0; c < cn; c += 64) {
+          const uint32_t k = c + l;
+          uint32_t off = 0, p = 0, s = 0, vl = 0;
+          if (k < cn) parse_entry(im, h, c0 + k, off, p, s, vl);
+          const uint32_t kl = p + s;
+          const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
+          if (k < cn) {
+            T.epos[k] = uint16_t(off);
+            T.pfx[k] = uint16_t(p);
+            T.sfx[k] = uint16_t(s);
+            T.kout[k] = uint32_t(kr) + ki - kl;
+            T.vout[k] = uint32_t(vr) + vi - vl;
+          }
+          kr += __shfl(ki, 63, 64);
+          vr += __shfl(vi, 63, 64);
+        }
+        if (l == 0) {
+          T.kout[cn] = uint32_t(kr);
+          T.vout[cn] = uint32_t(vr);
+        }
+        wave_sync();
+        dec_big_outputs(a, T, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V));
+      }
+    } else {
+      dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
+    }
+  }
+  raise_err(a.stats, err);
+}
+
+// Block b = kDW * workgroup + wave.  Waiting is only ever for lower-indexed blocks, and
+// workgroups are dispatched in index order (round-robin over the XCDs, in order on each), so
+// every block waited for has been dispatched before the waiter.  (A dispatch ticket per block --
+// one atomic on one word by a million waves -- serialised at ~11 ns per block.)  All waits are
+// bounded (kSpinLimit): a violation reports TIMEOUT instead of hanging.
+__global__ __launch_bounds__(64 * kDW) void decode1_kernel(DecodeArgs a) {
+  __shared__ DecLds lds[kDW];
+  __shared__ Dec1Shared S;
+  const uint32_t w = wave_id();
+  if (threadIdx.x == 0) {
+    S.ready = 0;
+    S.base_ready = 0;
+    S.err = 0;
+  }
+  __syncthreads();
+  const uint64_t b = uint64_t(blockIdx.x) * kDW + w;
+  if (b < a.nblk) {
+    decode1_block(a, lds[w], S, w, b);
+  } else if (lane_id() == 0) {  // no block: an empty aggregate for the leader
+    S.n[w] = S.k[w] = S.v[w] = 0;
+    __hip_atomic_fetch_or(&S.ready, 1u << w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
 // ---------------------------------------------------------------- decode pass 1: count
-// Header-only parse of every block (trailer, offsets table, 4-6 header bytes per entry) ->
-// per-block (entries, key bytes, value bytes) and per-tile sums.  16 lanes per block, four
-// blocks in flight per wave, one 64-block tile per workgroup.  Plain global byte loads:
-// every address is validated against the block length before it is dereferenced.
+// (the two-pass decode: the CRC-verifying read path and the A/B diagnostic)
 struct CountArgs {
   const uint8_t* blocks;
   const uint64_t* blk_off;
@@ -715,109 +1017,12 @@ struct CountArgs {
   uint32_t tail;        // bytes after each block inside its range (4: the framing CRC)
 };
 
-__device__ __forceinline__ uint32_t gb16(const uint8_t* p, uint32_t i) {
-  return (uint32_t(p[i]) << 8) | p[i + 1];
-}
-
-__global__ __launch_bounds__(256) void dec_count_kernel(CountArgs a) {
-  __shared__ uint64_t red[4][3];
-  const uint32_t l = lane_id(), w = wave_id(), grp = l >> 4, sl = l & 15;
-  const uint64_t tile = blockIdx.x;
-  uint64_t tn = 0, tk = 0, tv = 0;
-  uint32_t err = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < 4; ++r) {
-    const uint64_t b = tile * kTile + w * 16 + r * 4 + grp;
-    uint32_t n = 0;
-    uint64_t K = 0, V = 0;
-    bool ok = true;
-    if (b < a.nblk) {
-      const uint64_t start = a.blk_off[b], end = a.blk_off[b + 1];
-      ok = end >= start + a.tail && end - start <= 0x7FFFFFF0ull;
-      const uint32_t len = ok ? uint32_t(end - start) - a.tail : 0u;
-      const uint8_t* p = a.blocks + start;
-      ok = ok && len >= 2;
-      if (ok) {
-        n = gb16(p, len - 2);
-        ok = 2 + 2 * n <= len;
-      }
-      uint32_t data_end = ok ? len - 2 - 2 * n : 0u, fks = 0;
-      if (ok && n) {
-        ok = data_end >= 4;
-        if (ok) {
-          fks = gb16(p, 2);
-          ok = 4 + fks + 8 <= data_end;
-        }
-      }
-      if (!ok) n = 0;
-      for (uint32_t k = sl; k < n; k += 16) {
-        const uint32_t off = gb16(p, data_end + 2 * k);
-        bool e_ok = off + 4 <= data_end;
-        uint32_t ps = 0, ss = 0, vl = 0;
-        if (e_ok) {
-          ps = gb16(p, off);
-          ss = gb16(p, off + 2);
-          e_ok = off + 4 + ss + 10 <= data_end && ps <= fks && ps + ss > 0;
-        }
-        if (e_ok) {
-          vl = gb16(p, off + 12 + ss);
-          e_ok = off + 14 + ss + vl <= data_end;
-        }
-        ok = ok && e_ok;
-        K += ps + ss;
-        V += vl;
-      }
-    }
-    // reduce over the 16 lanes of this block
-#pragma unroll
-    for (uint32_t d = 8; d >= 1; d >>= 1) {
-      K += __shfl_xor(K, d, 16);
-      V += __shfl_xor(V, d, 16);
-      ok = __shfl_xor(int(ok), d, 16) && ok;
-    }
-    if (!ok) {
-      err |= LSMBLK_ERR_MALFORMED;
-      n = 0;
-      K = V = 0;
-    }
-    if (b < a.nblk && sl == 0) {
-      a.agg[3 * b] = n;
-      a.agg[3 * b + 1] = uint32_t(K > 0xFFFFFFFFull ? 0xFFFFFFFFull : K);
-      a.agg[3 * b + 2] = uint32_t(V > 0xFFFFFFFFull ? 0xFFFFFFFFull : V);
-      if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
-    }
-    if (sl == 0) {
-      tn += n;
-      tk += K;
-      tv += V;
-    }
-  }
-  tn = wave_sum(tn);
-  tk = wave_sum(tk);
-  tv = wave_sum(tv);
-  if (l == 0) {
-    red[w][0] = tn;
-    red[w][1] = tk;
-    red[w][2] = tv;
-  }
-#pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
-  raise_err(a.stats, err);
-  __syncthreads();
-  if (threadIdx.x < 3)
-    a.tile_sum[3 * tile + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                         red[3][threadIdx.x];
-}
-
-// Count pass, staged form: one single-wave workgroup per block streams the whole block into LDS
-// with coalesced 16-B loads (4 KiB of LDS: up to 32 waves per CU) and parses every header there
-// with decode's own rules (parse_hdr / parse_entry).  Reading all of E in full lines costs less
-// than the byte loads of the header-only parse above: those touch a 64-B sector per entry, which
-// at U's 128-B entries is most of E anyway, in scattered requests.  Blocks over the image parse
-// from global memory.  Tile sums: agg_tile_kernel.
-#ifndef LSMBLK_COUNT_STAGED
-#define LSMBLK_COUNT_STAGED 1
-#endif
+// Count pass: one single-wave workgroup per block streams the whole block into LDS with
+// coalesced 16-B loads (4 KiB of LDS: up to 32 waves per CU) and parses every header there with
+// decode's own rules (parse_hdr / parse_entry).  Reading all of E in full lines costs less than
+// a header-only parse with byte loads (round 1: 0.86 against 0.75 ms): those touch a 64-B sector
+// per entry, which at U's 128-B entries is most of E anyway, in scattered requests.  Blocks over
+// the image parse from global memory.  Tile sums: agg_tile_kernel.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dec_count_staged_kernel(CountArgs a) {
   __shared__ alignas(16) uint8_t img[kDecImg];
   const uint64_t b = blockIdx.x;
@@ -952,15 +1157,13 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(ScanArgs a) {
 
 // ================================================================ encode: plan
 // The greedy block walk of SsTableBuilder (table/builder.rs:48-65 over BlockBuilder::add,
-// block/builder.rs:54-73) in two passes:
-//   plan_adj_kernel   all entries in parallel: rec = klen + vlen, alcp = LCP with the
-//                     predecessor key, bit 31 set when the pair is out of order.
-//   plan_walk_kernel  one wave per segment walks the blocks over LDS chunks of (rec, alcp):
-//                     for non-decreasing keys LCP(first key, key_e) = min of alcp over
-//                     (first, e], so each block boundary is a min-scan, a sum-scan and a
-//                     ballot over 64 candidate entries; a block holding an out-of-order pair
-//                     compares with its first key directly.  Segment totals by decoupled
-//                     look-back, then the dense block tables.
+// block/builder.rs:54-73), plan_walk_kernel: one walker wave per segment walks the blocks over
+// an LDS ring of per-entry (rec = klen + vlen, alcp = LCP with the predecessor key, bit 31 set
+// when the pair is out of order) that a helper wave of the same workgroup computes just ahead of
+// it.  For non-decreasing keys LCP(first key, key_e) = min of alcp over (first, e], so each block
+// boundary is a min-scan, a sum-scan and a ballot over 64 candidate entries; a block holding an
+// out-of-order pair compares with its first key directly.  Segment totals by decoupled look-back,
+// then the dense block tables.
 struct PlanArgs {
   const uint8_t* keys;
   const uint32_t* key_off;
@@ -969,8 +1172,6 @@ struct PlanArgs {
   const uint32_t* seg_start;
   uint32_t nseg;
   uint32_t block_size;
-  uint32_t* rec;        // n: klen + vlen
-  uint32_t* alcp;       // n: see above
   uint32_t* sz;         // scratch, n+1: encoded size per (segment-local) block
   uint32_t* rec_first;  // scratch, n+1
   uint32_t* blk_first;  // dense, n+1
@@ -1037,75 +1238,22 @@ __device__ __forceinline__ uint32_t key_lcp(const PlanKeys& K, uint32_t pp, uint
   return lcp;
 }
 
-#ifndef PLAN_RING
-#define PLAN_RING 1  // walk over a ring of two LDS chunks, the next chunk's loads in flight
-#endif
-#ifndef PLAN_REC_OFF
-#define PLAN_REC_OFF 0  // 1: rec = klen + vlen from the offsets in the walk (plan_adj writes alcp only): slower, the walk is issue-sensitive
-#endif
 
-__global__ __launch_bounds__(256) void plan_adj_kernel(PlanArgs a0) {
-  const PlanArgs a = resolve(a0);
-  const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  uint32_t err = 0;
-  const PlanKeys K = plan_keys(a);
-  if (e < a.n) {
-    const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
-#if !PLAN_REC_OFF
-    a.rec[e] = kl + (a.val_off[e + 1] - a.val_off[e]);
-#endif
-    uint32_t al = 0;
-    if (e > 0) {
-      const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
-      uint32_t w0, w1;
-      const uint32_t lcp = key_lcp(K, pp, pl, kp, kl, w0, w1);
-      const uint32_t m = pl < kl ? pl : kl, sh = 8 * (lcp & 3);
-      const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
-      al = (lcp < kAlcpLcp ? lcp : kAlcpLcp) | (sorted ? 0u : kAlcpUnsorted);
-    }
-    a.alcp[e] = al;
-    if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
-  }
-  err = __ballot(err != 0) ? LSMBLK_ERR_EMPTY_KEY : 0u;
-  raise_err(a.stats, err);
-}
+constexpr uint32_t kWalkThreads = 512;  // 4 walker waves + their 4 helper (producer) waves
+constexpr uint32_t kSpinMax = 1u << 24;  // LDS hand-off polls before a wave gives up (TIMEOUT)
+constexpr uint32_t kProdBatch = 4;       // entries per helper lane with loads in flight together (2: 0.41 ms,
+                                         // 8: 128 VGPRs and a spill, against 0.39)
+constexpr uint32_t kRing = 1024;         // (rec, alcp) ring entries per walker (power of two, >= 2 chunks):
+                                         // 32 KiB per workgroup, three per CU
+constexpr uint32_t kChunk = 256;         // entries per producer hand-off (1024 / 512 / 256: 0.39 / 0.376 /
+                                         // 0.371 ms)
 
-constexpr uint32_t kWalk = 1024;  // rec / alcp entries per LDS chunk
-#ifndef PLAN_STREAM
-#define PLAN_STREAM 1  // every block ending in a window found in it; open blocks carry into the next window
-#endif
-#ifndef PLAN_TWO_BLOCKS
-#define PLAN_TWO_BLOCKS 1  // two blocks per window step when the second fits the window
-#endif
-
-#ifndef PLAN_FUSED
-#define PLAN_FUSED 1  // (rec, alcp) produced into the walkers' LDS rings by helper waves of the same workgroup
-#endif
-constexpr uint32_t kWalkThreads = PLAN_FUSED ? 512 : 256;
-[[maybe_unused]] constexpr uint32_t kSpinMax = 1u << 24;  // LDS hand-off polls before a wave gives up (TIMEOUT)
-
-#ifndef PLAN_PROD_BATCH
-#define PLAN_PROD_BATCH 4
-#endif
-[[maybe_unused]] constexpr uint32_t kProdBatch = PLAN_PROD_BATCH;  // entries per lane with loads in flight together
-#ifndef PLAN_RING_ENTRIES
-#define PLAN_RING_ENTRIES 1024  // per walker (power of two, >= 2 producer chunks): 32 KiB per workgroup, 3 per CU
-#endif
-#ifndef PLAN_PROD_DPP
-#define PLAN_PROD_DPP 0
-#endif
-#ifndef PLAN_CHUNK
-#define PLAN_CHUNK 256
-#endif
-[[maybe_unused]] constexpr uint32_t kChunk = PLAN_CHUNK;  // entries per producer hand-off (ring = 2 x kWalk)
-
-#if PLAN_FUSED
 // Helper wave of a walker: plan_adj's per-entry values for the walker's segment [s0, s1),
 // written chunk by chunk into the walker's ring (slot (e - s0) % kRing), never to HBM.
 // A chunk may overwrite the ring's older half once the walker's window has left it;
 // prod[0] = entries produced (relative to s0), cons[0] = walker's window start (relative).
 __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, uint32_t s1, uint32_t* CR,
-                             uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t kRing, uint32_t& err) {
+                             uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t& err) {
   const uint32_t l = lane_id();
   const uint32_t klim = K.glead + uni(a.key_off[a.n]);
   for (uint32_t c = s0; c < s1; c += kChunk) {
@@ -1125,25 +1273,6 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
 #pragma unroll 1
     for (uint32_t h = 0; h < kChunk / 64; h += kProdBatch) {  // kProdBatch entries per lane at a time
       uint32_t kp[kProdBatch], kn[kProdBatch], pp[kProdBatch], v0[kProdBatch], v1[kProdBatch];
-#if PLAN_PROD_DPP
-      // one vector load per array per entry; the neighbours' offsets by wave-wide DPP shifts,
-      // the two edge lanes' from uniform (scalar) loads
-#pragma unroll
-      for (uint32_t i = 0; i < kProdBatch; ++i) {
-        const uint32_t base = c + 64 * (h + i), e = base + l;
-        kp[i] = v0[i] = 0;
-        if (e <= cend) {
-          kp[i] = a.key_off[e];
-          v0[i] = a.val_off[e];
-        }
-        const uint32_t up = base + 64 < cend ? base + 64 : cend;
-        const uint32_t ke = kconst(a.key_off)[up], ve = kconst(a.val_off)[up];
-        const uint32_t kb = base > 0 ? kconst(a.key_off)[base - 1] : 0u;
-        kn[i] = uint32_t(__builtin_amdgcn_update_dpp(int(ke), int(kp[i]), 0x130, 0xF, 0xF, false));  // wave_shl:1
-        v1[i] = uint32_t(__builtin_amdgcn_update_dpp(int(ve), int(v0[i]), 0x130, 0xF, 0xF, false));
-        pp[i] = uint32_t(__builtin_amdgcn_update_dpp(int(kb), int(kp[i]), 0x138, 0xF, 0xF, false));  // wave_shr:1
-      }
-#else
 #pragma unroll
       for (uint32_t i = 0; i < kProdBatch; ++i) {
         const uint32_t e = c + 64 * (h + i) + l;
@@ -1156,7 +1285,6 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
           v1[i] = a.val_off[e + 1];
         }
       }
-#endif
       u32x4 xk[kProdBatch], xp[kProdBatch];
 #pragma unroll
       for (uint32_t i = 0; i < kProdBatch; ++i) {
@@ -1224,20 +1352,13 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
     if (l == 0) __hip_atomic_store(prod, cend - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
-#endif
 
 // (fused: three workgroups of 8 waves per CU, so that up to 3 K segments walk at once)
-__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PLAN_FUSED ? 4 : 1))) void plan_walk_kernel(PlanArgs a0) {
+__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4))) void plan_walk_kernel(PlanArgs a0) {
   const PlanArgs a = resolve(a0);
-#if PLAN_RING || PLAN_FUSED
-  constexpr uint32_t kRing = PLAN_RING_ENTRIES;
-  static_assert(PLAN_FUSED ? (kRing >= 2 * kChunk && (kRing & (kRing - 1)) == 0) : kRing == 2 * kWalk, "plan ring size");
-#else
-  constexpr uint32_t kRing = kWalk;
-#endif
+  static_assert(kRing >= 2 * kChunk && (kRing & (kRing - 1)) == 0, "plan ring size");
   __shared__ uint32_t crec[4][kRing], calcp[4][kRing];
   const uint32_t l = lane_id();
-#if PLAN_FUSED
   // waves 0-3 walk segments, wave 4 + w produces (rec, alcp) into walker w's ring
   __shared__ uint32_t hand_g[4], hand_prod[4], hand_cons[4];
   const uint32_t wv = wave_id(), ww = wv & 3;
@@ -1253,11 +1374,6 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
   const uint32_t g = uni(hand_g[ww]);
   uint32_t* CR = crec[ww];
   uint32_t* CA = calcp[ww];
-#else
-  uint32_t* CR = crec[wave_id()];
-  uint32_t* CA = calcp[wave_id()];
-  const uint32_t g = take_ticket(a.ticket);
-#endif
   if (g >= a.nseg) return;
   uint32_t err = 0;
   uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
@@ -1268,65 +1384,15 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
     if (s1 < s0) s1 = s0;
   }
   const PlanKeys K = plan_keys(a);
-#if PLAN_FUSED
   if (wv >= 4) {
-    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], kRing, err);
+    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err);
     const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
                           (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
     raise_err(a.stats, werr);
     return;
   }
-#endif
-  // (rec, alcp) of entry e at LDS slot (e - s0) % kRing.  Ring: entries [.., ld_end) are in LDS,
-  // [pf_beg, pf_end) = [ld_end, ld_end + kWalk) in flight in registers; a window reaching past
-  // ld_end commits them (landed long before: a chunk is ~16 window steps) and issues the next.
-  // A commit overwrites the slots of entries kRing back, all behind the window (j0 > ld_end - 64).
-  uint32_t ld_end = s0, pf_beg = s0, pf_end = s0;
-#if PLAN_REC_OFF
-  uint32_t pk0[kWalk / 64], pk1[kWalk / 64], pv0[kWalk / 64], pv1[kWalk / 64];
-#else
-  uint32_t pr[kWalk / 64];
-#endif
-  uint32_t pq[kWalk / 64];
-  [[maybe_unused]] auto issue = [&](uint32_t from) {
-    pf_beg = from;
-    pf_end = s1 - from < kWalk ? s1 : from + kWalk;
-#pragma unroll
-    for (uint32_t i = 0; i < kWalk / 64; ++i) {
-      const uint32_t j = from + 64 * i + l;
-      if (j < pf_end) {
-#if PLAN_REC_OFF
-        pk0[i] = a.key_off[j];
-        pk1[i] = a.key_off[j + 1];
-        pv0[i] = a.val_off[j];
-        pv1[i] = a.val_off[j + 1];
-#else
-        pr[i] = a.rec[j];
-#endif
-        pq[i] = a.alcp[j];
-      }
-    }
-  };
-  [[maybe_unused]] auto commit = [&]() {
-#pragma unroll
-    for (uint32_t i = 0; i < kWalk / 64; ++i) {
-      const uint32_t j = pf_beg + 64 * i + l;
-      if (j < pf_end) {
-        const uint32_t x = (j - s0) & (kRing - 1);
-#if PLAN_REC_OFF
-        CR[x] = (pk1[i] - pk0[i]) + (pv1[i] - pv0[i]);  // klen + vlen, u32 as plan_adj's
-#else
-        CR[x] = pr[i];
-#endif
-        CA[x] = pq[i];
-      }
-    }
-    wave_sync();
-    ld_end = pf_end;
-  };
-#if PLAN_FUSED
-  (void)pf_beg;
-  (void)pf_end;
+  // (rec, alcp) of entry e at LDS slot (e - s0) % kRing, written by the helper wave; `need` waits
+  // until the window's entries are in and tells the helper where the window starts.
   uint32_t known = 0;  // entries of the ring the producer has finished (relative to s0)
   bool stalled = false;
   auto need = [&](uint32_t j0, uint32_t wend) {
@@ -1344,24 +1410,6 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
   };
-#elif PLAN_RING
-  auto need = [&](uint32_t j0, uint32_t wend) {
-    (void)j0;
-    if (wend > ld_end) {
-      commit();
-      if (ld_end < s1) issue(ld_end);
-    }
-  };
-  issue(s0);
-  need(s0, s0 + 1);
-#else
-  auto need = [&](uint32_t j0, uint32_t wend) {  // one chunk, reloaded from the window when left
-    if (!(j0 >= pf_beg && wend <= ld_end)) {
-      issue(j0);
-      commit();
-    }
-  };
-#endif
   uint32_t nb = 0;
   uint64_t bytes = 0;
   const uint64_t bs = a.block_size;
@@ -1413,7 +1461,6 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
         }
         ++nb;
         bytes += size;
-#if PLAN_STREAM
         s = j0 + f;
         // Further blocks from entry s on the same window's lanes f..63 (the window held no
         // out-of-order pair, or direct would be set): LCP with entry s = min of alcp over
@@ -1448,36 +1495,6 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(PL
           f = f2;
         }
         if (open) continue;  // next window, same block
-#else
-        const uint32_t len1 = j0 + f - s;  // entries of the block just found
-        s = j0 + f;
-        // The next block from entry s, on the same window's lanes f..63 (the window held no
-        // out-of-order pair, or direct would be set): a U block of ~31 entries usually ends
-        // among them, so one window step finds two blocks.  LCP with entry s = min of alcp over
-        // (f, e]: lanes <= f read the min identity; growth and estimated_size restart at s.
-        // Tried only when the lanes left are more than the block just found took (Z's ~35-entry
-        // blocks seldom fit the rest of the window: there the second scan is wasted work).
-        if (PLAN_TWO_BLOCKS && !direct && s < s1 && 64 - f > len1) {
-          const uint32_t mn = wave_incl_min31(l <= f ? kAlcpLcp : (al & kAlcpLcp));  // all lanes (DPP)
-          const uint32_t p2 = l <= f ? 0u : mn;
-          const uint32_t g2 = (valid && l >= f) ? r + 16 - p2 : 0u;
-          if (__ballot(g2 >= (1u << 25)) == 0) {
-            const uint32_t before2 = 2 + wave_incl_scan32(g2) - g2;
-            const uint64_t m2 = __ballot(l > f && (!valid || uint64_t(before2) + r + 14 > bs));
-            if (m2) {
-              const uint32_t f2 = uint32_t(__builtin_ctzll(m2));
-              const uint32_t size2 = uint32_t(__builtin_amdgcn_readlane(before2, f2));
-              if (l == 0) {
-                a.rec_first[s0 + nb] = s;
-                a.sz[s0 + nb] = size2;
-              }
-              ++nb;
-              bytes += size2;
-              s = j0 + f2;
-            }
-          }
-        }
-#endif
         break;
       }
       carry += lane64(incl, 63);
@@ -1553,9 +1570,6 @@ __device__ __forceinline__ EmitArgs resolve(const EmitArgs& a0) {
   return a;
 }
 
-#ifndef EMIT_DIRECT_CENT
-#define EMIT_DIRECT_CENT 1  // phase 1 entry lanes write the chunk -> source map (no max-scan pass)
-#endif
 constexpr uint32_t kEmitWaves = 4;
 constexpr uint32_t kEmitKCap = 1088;
 constexpr uint32_t kEmitICap = 4224;  // block image: staged values, then the encoded block (33 swizzle rows)
@@ -1565,12 +1579,7 @@ struct alignas(16) EmitLds {
   uint8_t kimg[kEmitKCap];
   uint8_t img[kEmitICap];
   alignas(16) uint32_t cent[kEmitICap / 16 + 4];  // chunk -> its source byte in the staged values, ~0 if not wholly inside one value
-#if EMIT_DIRECT_CENT
   alignas(16) uint32_t erec[4 * kEmitMaxE];  // per entry: record start | prefix << 16, suffix in kimg | value length << 16, suffix length
-#else
-  uint16_t epos[kEmitMaxE], pfx[kEmitMaxE], ksrc[kEmitMaxE];  // record start, prefix, suffix in kimg
-  uint16_t vdst[kEmitMaxE], vsrc[kEmitMaxE], vlen[kEmitMaxE];  // value start (block), staged start, length
-#endif
   uint64_t ts[kEmitMaxE];
 };
 
@@ -1799,11 +1808,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // and the value bytes of each value's two partial edge chunks (captured in registers: the
     // in-place move below overwrites the staged values).
     const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
-#if EMIT_DIRECT_CENT
     for (uint32_t j = 4 * l; j < ncs; j += 256) *reinterpret_cast<u32x4*>(L.cent + j) = u32x4{~0u, ~0u, ~0u, ~0u};
-#else
-    for (uint32_t j = l; j < ncs; j += 64) L.cent[j] = 0;
-#endif
     uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
 #pragma unroll
     for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
@@ -1865,17 +1870,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       dc += __shfl(incl, 63, 64);
       if (k < n) {
         const uint32_t sfx = kl - p;
-#if EMIT_DIRECT_CENT  // phase 3 and the offsets table read these on the same lane: one 16-B record
         *reinterpret_cast<u32x4*>(L.erec + 4 * k) = u32x4{pos | (p << 16), (klead + kp + p) | (vl << 16), sfx, 0u};
-#else
-        L.epos[k] = uint16_t(pos);
-        L.pfx[k] = uint16_t(p);
-        L.ksrc[k] = uint16_t(klead + kp + p);
-        L.vdst[k] = uint16_t(pos + 14 + sfx);
-        L.vsrc[k] = uint16_t(vlead + vp);
-        L.vlen[k] = uint16_t(vl);
-#endif
-#if EMIT_DIRECT_CENT
         // the image chunks lying wholly inside this value -> their source bytes in the staged
         // values (every other chunk keeps ~0)
         {
@@ -1883,11 +1878,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
           const uint32_t srcb = vlead + vp - vdb;       // + image byte = staged byte (mod 2^32)
           for (uint32_t c = (vdb + 15) >> 4; 16 * c + 16 <= vdb + vl; ++c) L.cent[c] = srcb + 16 * c;
         }
-#else
-        // first image chunk whose start is at or after this value's start
-        const uint32_t j0 = (olead + pos + 14 + sfx + 15) >> 4;
-        if (j0 < ncs && vl) atomicMax(&L.cent[j0], k);
-#endif
       }
     }
     const uint32_t data_len = dc;
@@ -1912,42 +1902,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
     // kEB chunk groups per batch: every LDS read of the batch is issued before its uses.
     // (EMIT_DIRECT_CENT: the entry lanes wrote the map in phase 1)
-#if !EMIT_DIRECT_CENT
-    {
-      uint32_t carry = 0;
-      for (uint32_t c0 = 0; c0 < ncs; c0 += 64 * kEB) {
-        uint32_t kk[kEB];
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j) {
-          const uint32_t c = c0 + 64 * j + l;
-          kk[j] = c < ncs ? L.cent[c] : 0u;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j) {
-          kk[j] = max(wave_incl_max32(kk[j]), carry);
-          carry = __builtin_amdgcn_readlane(kk[j], 63);
-        }
-        int32_t vd[kEB], ve[kEB];
-        uint32_t vs[kEB];
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j) {
-          if (c0 + 64 * j + l < ncs) {
-            vd[j] = int32_t(L.vdst[kk[j]]);
-            ve[j] = vd[j] + int32_t(L.vlen[kk[j]]);
-            vs[j] = L.vsrc[kk[j]];
-          }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j) {
-          const uint32_t c = c0 + 64 * j + l;
-          if (c < ncs) {
-            const int32_t x = int32_t(16 * c) - int32_t(olead);  // block byte of the chunk
-            L.cent[c] = (kk[j] < n && x >= vd[j] && x + 16 <= ve[j]) ? vs[j] + uint32_t(x - vd[j]) : ~0u;
-          }
-        }
-      }
-    }
-#endif
     wave_sync();
     // Phase 2b (descending): move whole-value chunks to their place in the encoded block.
     // A value only moves up (its destination follows its own header and every earlier
@@ -1981,14 +1935,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         const uint32_t k = 64 * it + l;
         if (64 * it >= n) break;
         if (k >= n) continue;
-#if EMIT_DIRECT_CENT
         const u32x4 er = *reinterpret_cast<const u32x4*>(L.erec + 4 * k);
         const uint32_t pos = er.x & 0xFFFF, p = er.x >> 16, ks = er.y & 0xFFFF, vl = er.y >> 16, sfx = er.z;
         const uint32_t vd = pos + 14 + sfx;
-#else
-        const uint32_t pos = L.epos[k], p = L.pfx[k], ks = L.ksrc[k], vd = L.vdst[k], vl = L.vlen[k];
-        const uint32_t sfx = vd - pos - 14;
-#endif
         const uint64_t tsv = L.ts[k];
         // unaligned LDS stores (the image is not swizzled): every field is one or two stores
         uint8_t* o = L.img;
@@ -2018,11 +1967,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     wave_sync();
     // offsets table + entry count (u16 BE, `as u16`)
     for (uint32_t k = l; k < n; k += 64)
-#if EMIT_DIRECT_CENT
       *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.erec[4 * k] & 0xFFFF));
-#else
-      *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.epos[k] & 0xFFFF));
-#endif
     if (l == 0) *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * n) = uint16_t(bswap16(n & 0xFFFF));
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
@@ -2078,7 +2023,7 @@ __global__ __launch_bounds__(256) void crc_verify_kernel(const uint8_t* blocks, 
   raise_err(stats, err);
 }
 
-// Per-64-block tile sums of agg (what dec_count_kernel writes beside agg), one wave per tile.
+// Per-64-block tile sums of agg (the count pass writes agg), one wave per tile.
 __global__ __launch_bounds__(256) void agg_tile_kernel(const uint32_t* agg, uint64_t nblk, uint64_t* tile_sum) {
   const uint64_t tile = uint64_t(blockIdx.x) * 4 + wave_id(), b = tile * kTile + lane_id();
   if (tile * kTile >= nblk) return;
@@ -2133,7 +2078,7 @@ struct CrcArgs {
   const CrcTabs* tabs;
   uint64_t* stats;
   // optional (the verifying decode): per-block (entries, key bytes, value bytes) exactly as
-  // dec_count_kernel computes them, parsed from the staged block -- one read of E for both
+  // the count pass computes them, parsed from the staged block -- one read of E for both
   uint32_t* agg;
 };
 
@@ -2781,6 +2726,17 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
     if ((rc = grow(&c->tile_pre, &cap, tiles, 3))) return rc;
     c->tile_cap = cap;
   }
+  if (blocks > c->d1_blk_cap) {
+    // one arena: 3 granules per kDW-block tile (aggregate), then 3 per tile (inclusive prefix)
+    const uint64_t nb = blocks + blocks / 4 + 1024;
+    cap = 0;  // (grow frees the old arena)
+    if ((rc = grow(&c->d1_gran, &cap, 6 * ((nb + kDW - 1) / kDW + 1), 1, kStatusFlags))) {
+      c->d1_blk_cap = 0;
+      return rc;
+    }
+    c->d1_blk_cap = nb;
+    c->epoch = 0;  // the fresh arena is zeroed; the next call starts a new epoch sequence
+  }
   if (segs > c->seg_cap) {
     cap = c->seg_cap;
     if ((rc = grow(&c->seg_agg, &cap, segs, 2, kStatusFlags))) return rc;
@@ -2795,7 +2751,7 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
     cap = c->rec_cap;
     if ((rc = grow(&c->blk_first, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
-    if ((rc = grow(&c->ent, &cap, entries + 1, 3))) return rc;
+    if ((rc = grow(&c->ent, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
     if ((rc = grow(&c->big_list, &cap, entries + 1, 1))) return rc;
     c->rec_cap = cap;
@@ -2809,6 +2765,10 @@ int next_epoch(lsmblk_ctx* c, hipStream_t st) {
     if (c->seg_cap) {
       if (hipMemsetAsync(c->seg_agg, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
       if (hipMemsetAsync(c->seg_inc, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    }
+    if (c->d1_blk_cap) {
+      const uint64_t words = 6 * ((c->d1_blk_cap + kDW - 1) / kDW + 1);
+      if (hipMemsetAsync(c->d1_gran, 0, words * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     }
     c->epoch = 0;
   }
@@ -2878,6 +2838,7 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->vcrc);
   (void)hipFree(c->sws);
   (void)hipFree(c->rws);
+  (void)hipFree(c->d1_gran);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2890,6 +2851,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->poll = value;
   } else if (key == LSMBLK_DEBUG_DECODE_SKIP) {
     c->skip = value;
+  } else if (key == LSMBLK_DEBUG_TWO_PASS_DECODE) {
+    c->dec_two_pass = value != 0;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->ev[0]) {
       DeviceGuard dg(c->device);
@@ -2941,7 +2904,7 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
                            void* stream) {
   if (!c || !blk_off || !out || !stats) return LSMBLK_E_INVAL;
   if (!aligned16(out->keys) || !aligned16(out->vals) || !out->key_off || !out->val_off) return LSMBLK_E_INVAL;
-  if (nblk >= 0xFFFFFFFFull || tail > 16) return LSMBLK_E_INVAL;
+  if (nblk > 0x7FFFFFFFull || tail > 16) return LSMBLK_E_INVAL;  // one workgroup (or wave) per block
   if ((flags & LSMBLK_DECODE_VERIFY_CRC) && tail != 4) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
@@ -2967,46 +2930,6 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   }
   const uint64_t ntiles = (nblk + kTile - 1) / kTile;
   c->dec_timed = c->timing;
-  if (flags & LSMBLK_DECODE_VERIFY_CRC) {
-    if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    // one pass over E: the CRC of every block and its (entries, key bytes, value bytes), in
-    // place of dec_count_kernel's second read of the headers
-    if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st, c->dec_agg)))
-      return rc;
-    hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
-                       c->vcrc, c->meta_cstats, stats);
-    tlaunch(c, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), st, -1, 1, (const uint32_t*)c->dec_agg, nblk,
-            c->tile_sum);
-  } else {
-    CountArgs ca;
-    ca.blocks = blocks;
-    ca.blk_off = blk_off;
-    ca.nblk = nblk;
-    ca.agg = c->dec_agg;
-    ca.tile_sum = c->tile_sum;
-    ca.stats = stats;
-    ca.tail = tail;
-    if (LSMBLK_COUNT_STAGED && nblk <= 0x7FFFFFFFull) {
-      tlaunch(c, dec_count_staged_kernel, dim3(uint32_t(nblk)), dim3(64), st, 0, -1, ca);
-      tlaunch(c, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), st, -1, 1, (const uint32_t*)c->dec_agg,
-              nblk, c->tile_sum);
-    } else {
-      tlaunch(c, dec_count_kernel, dim3(uint32_t(ntiles)), dim3(256), st, 0, 1, ca);
-    }
-  }
-  ScanArgs sa;
-  sa.tile_sum = c->tile_sum;
-  sa.tile_pre = c->tile_pre;
-  sa.ntiles = ntiles;
-  sa.key_off = out->key_off;
-  sa.val_off = out->val_off;
-  sa.entry_cap = out->entry_cap;
-  sa.key_cap = out->key_cap;
-  sa.val_cap = out->val_cap;
-  sa.stats = stats;
-  sa.blk_ent = blk_ent;
-  sa.nblk = nblk;
-  tlaunch(c, dec_scan_kernel, dim3(1), dim3(1024), st, 2, 3, sa);
   DecodeArgs a;
   a.blocks = blocks;
   a.blk_off = blk_off;
@@ -3025,6 +2948,60 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   a.tail = tail;
   a.blk_ent = blk_ent;
   a.skip = c->skip;
+  a.tagg = a.tinc = nullptr;
+  a.tag = a.poll = 0;
+  if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && !c->dec_two_pass) {
+    // single pass: E is read once (decode1_kernel)
+    if ((rc = next_epoch(c, st))) return rc;
+    a.tagg = c->d1_gran;
+    a.tinc = a.tagg + 3 * ((c->d1_blk_cap + kDW - 1) / kDW + 1);
+    a.tag = c->epoch;
+    a.poll = c->poll;
+    tlaunch(c, decode1_kernel, dim3(uint32_t((nblk + kDW - 1) / kDW)), dim3(64 * kDW), st, 4, 5, a);
+    if (c->timing) {  // the count and scan slots of lsmblk_ctx_kernel_times read 0
+      (void)hipEventRecord(c->ev[0], st);
+      (void)hipEventRecord(c->ev[1], st);
+      (void)hipEventRecord(c->ev[2], st);
+      (void)hipEventRecord(c->ev[3], st);
+    }
+    return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  }
+  if (flags & LSMBLK_DECODE_VERIFY_CRC) {
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    // one pass over E: the CRC of every block and its (entries, key bytes, value bytes), in
+    // place of the count pass's second read of E
+    if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st, c->dec_agg)))
+      return rc;
+    hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
+                       c->vcrc, c->meta_cstats, stats);
+    tlaunch(c, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), st, -1, 1, (const uint32_t*)c->dec_agg, nblk,
+            c->tile_sum);
+  } else {
+    CountArgs ca;
+    ca.blocks = blocks;
+    ca.blk_off = blk_off;
+    ca.nblk = nblk;
+    ca.agg = c->dec_agg;
+    ca.tile_sum = c->tile_sum;
+    ca.stats = stats;
+    ca.tail = tail;
+    tlaunch(c, dec_count_staged_kernel, dim3(uint32_t(nblk)), dim3(64), st, 0, -1, ca);
+    tlaunch(c, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), st, -1, 1, (const uint32_t*)c->dec_agg,
+            nblk, c->tile_sum);
+  }
+  ScanArgs sa;
+  sa.tile_sum = c->tile_sum;
+  sa.tile_pre = c->tile_pre;
+  sa.ntiles = ntiles;
+  sa.key_off = out->key_off;
+  sa.val_off = out->val_off;
+  sa.entry_cap = out->entry_cap;
+  sa.key_cap = out->key_cap;
+  sa.val_cap = out->val_cap;
+  sa.stats = stats;
+  sa.blk_ent = blk_ent;
+  sa.nblk = nblk;
+  tlaunch(c, dec_scan_kernel, dim3(1), dim3(1024), st, 2, 3, sa);
   tlaunch(c, decode_kernel, dim3(uint32_t(nblk)), dim3(64), st, 4, 5, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -3068,10 +3045,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.seg_start = seg_start;
   p.nseg = nseg;
   p.block_size = block_size;
-  const uint64_t ecap = c->rec_cap;  // rows of the per-entry plan arrays
-  p.rec = c->ent;
-  p.alcp = c->ent + ecap;
-  p.sz = c->ent + 2 * ecap;
+  p.sz = c->ent;
   p.rec_first = c->rec_first;
   p.blk_first = c->blk_first;
   p.blk_off = blk_off;
@@ -3087,17 +3061,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.dnseg = dnseg;
   p.span = span ? 1u : 0u;
   c->enc_timed = c->timing;
-#if PLAN_FUSED  // plan_adj's work is done by the walk's helper waves
   tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, 6, 7, p);
-#else
-  if (in->n) {
-    const uint32_t eg = uint32_t((in->n + 255) / 256);
-    tlaunch(c, plan_adj_kernel, dim3(eg), dim3(256), st, 6, -1, p);
-  } else if (c->timing) {
-    (void)hipEventRecord(c->ev[6], st);
-  }
-  tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, -1, 7, p);
-#endif
   // the big-block flags are cleared before emit (the start of emit_kernel to the end of
   // emit_big_kernel is what bench.py's roofline divides by)
   const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;  // blocks <= entries, <= blk_cap
