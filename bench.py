@@ -72,8 +72,8 @@ def parse(argv=None):
                    help="launcher self-test: ranks join a gloo group and report the world, no GPU work")
     p.add_argument("--dry-run-fail-rank", type=int, default=None,
                    help="launcher self-test: this rank exits with status 3 before joining the group")
-    p.add_argument("--decode-two-pass", action="store_true",
-                   help="diagnostics (A/B): count + scan + decode instead of the single-pass decode")
+    p.add_argument("--decode-single-pass", action="store_true",
+                   help="diagnostics (A/B): the single-pass look-back decode instead of count + scan + decode")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
     return p.parse_args(argv)
@@ -205,7 +205,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     stream = torch.cuda.current_stream(dev)
     ctx = batch._ctx(local, stream)
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
-    check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
+    check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_single_pass else 0))
 
     def step(ev=None):
         if ev is not None:

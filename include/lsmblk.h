@@ -159,7 +159,7 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
 #define LSMBLK_DEBUG_POLL_MODE 0
 #define LSMBLK_DEBUG_DECODE_SKIP 1
 #define LSMBLK_DEBUG_KERNEL_TIMING 2 /* 1: dispatch start/stop events on every kernel launch */
-#define LSMBLK_DEBUG_TWO_PASS_DECODE 3 /* 1: count + scan + decode instead of the single pass (A/B) */
+#define LSMBLK_DEBUG_SINGLE_PASS_DECODE 3 /* 1: the single-pass look-back decode instead of count + scan + decode (A/B) */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* Durations (ms) of the kernels of the last timed decode / encode call on this context:
  * [0] dec_count [1] dec_scan [2] decode [3] plan [4] emit; -1 if not recorded.  Waits for

@@ -463,7 +463,7 @@ struct lsmblk_ctx {
   uint64_t rec_cap = 0;
   uint64_t* d1_gran = nullptr;   // single-pass decode look-back granules (uncached): 3 + 3 per tile of
   uint64_t d1_blk_cap = 0;       //   kDW blocks (aggregate, inclusive prefix); blocks covered
-  bool dec_two_pass = false;     // diagnostics: the count + scan + decode path instead (A/B)
+  bool dec_single_pass = false;  // diagnostics: the single-pass look-back decode instead (A/B)
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
   uint32_t skip = 0;             // decode ablation mask (timing experiments only)

@@ -2851,8 +2851,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->poll = value;
   } else if (key == LSMBLK_DEBUG_DECODE_SKIP) {
     c->skip = value;
-  } else if (key == LSMBLK_DEBUG_TWO_PASS_DECODE) {
-    c->dec_two_pass = value != 0;
+  } else if (key == LSMBLK_DEBUG_SINGLE_PASS_DECODE) {
+    c->dec_single_pass = value != 0;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->ev[0]) {
       DeviceGuard dg(c->device);
@@ -2950,8 +2950,8 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   a.skip = c->skip;
   a.tagg = a.tinc = nullptr;
   a.tag = a.poll = 0;
-  if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && !c->dec_two_pass) {
-    // single pass: E is read once (decode1_kernel)
+  if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && c->dec_single_pass) {
+    // single pass: E is read once (decode1_kernel; diagnostic, slower at U: DESIGN.md section 8)
     if ((rc = next_epoch(c, st))) return rc;
     a.tagg = c->d1_gran;
     a.tinc = a.tagg + 3 * ((c->d1_blk_cap + kDW - 1) / kDW + 1);
