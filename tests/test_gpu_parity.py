@@ -615,3 +615,25 @@ def test_verifying_decode_counts_in_the_crc_pass(gen, n, bs):
         with pytest.raises(LsmBlkError) as e:
             batch.decode_blocks(db, do, tail=4, verify=True)
         assert e.value.status == LSMBLK_E_MALFORMED
+
+
+@pytest.mark.parametrize("cfg,n", [("U", 30000), ("Z", 30000), ("M", 4000)])
+def test_single_pass_decode_path(cfg, n):
+    """The single-pass look-back decode (LSMBLK_DEBUG_SINGLE_PASS_DECODE, the A/B alternative to
+    count + scan + decode) gives the oracle's stream and block entry index."""
+    from lsm_amd._lib import lib
+    kv = O.KV(*synth.GENERATORS[cfg](n, seed=21))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 128 << 10)
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, synth.BLOCK_SIZE[cfg])
+    rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
+    assert rc == 0
+    ctx = batch._ctx(0)
+    lib().lsmblk_debug_set(ctx, 3, 1)
+    try:
+        for shift in (0, 5):
+            db, do = dev_blocks(ref_blocks, ref_off, shift)
+            assert_kv_equal(batch.decode_blocks(db, do), ref_kv)
+        out, ent = batch.decode_blocks(*dev_blocks(ref_blocks, ref_off), with_blk_ent=True)
+        np.testing.assert_array_equal(ent.cpu().numpy().view(np.uint64)[-1], kv.n)
+    finally:
+        lib().lsmblk_debug_set(ctx, 3, 0)
