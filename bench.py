@@ -72,8 +72,12 @@ def parse(argv=None):
                    help="launcher self-test: ranks join a gloo group and report the world, no GPU work")
     p.add_argument("--dry-run-fail-rank", type=int, default=None,
                    help="launcher self-test: this rank exits with status 3 before joining the group")
-    p.add_argument("--decode-single-pass", action="store_true",
-                   help="diagnostics (A/B): the single-pass look-back decode instead of count + scan + decode")
+    p.add_argument("--decode-two-pass", action="store_true",
+                   help="diagnostics (A/B): count + tile scan + decode (three launches) instead of the lagged decode")
+    p.add_argument("--decode-lag", type=int, default=None,
+                   help="diagnostics (A/B): blocks the lagged decode counts ahead of its decodes (default 8192)")
+    p.add_argument("--ablate-lag", action="store_true", help="diagnostics: the lagged decode's ablation masks")
+    p.add_argument("--ablate-only", action="store_true", help="diagnostics: time only mask 0 and --ablate")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
     return p.parse_args(argv)
@@ -205,7 +209,9 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     stream = torch.cuda.current_stream(dev)
     ctx = batch._ctx(local, stream)
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
-    check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_single_pass else 0))
+    check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
+    if args.decode_lag is not None:
+        check(lib().lsmblk_debug_set(ctx, 4, args.decode_lag))
 
     def step(ev=None):
         if ev is not None:
@@ -946,7 +952,13 @@ def kernel_times(ctx, step, dev, reps=3, lead=3):
 def ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream):
     from lsm_amd._lib import lib as L
     res = {}
-    for mask in sorted({0, 2, 4, 8, 14, 1024, 2048, 3072, args.ablate}):
+    masks = {0, 2, 4, 8, 14, 256, 1024, 2048, 3072, 256 | 3072, args.ablate}
+    if args.ablate_only:
+        masks = {0, args.ablate}
+    elif args.ablate_lag:  # lagged decode: no count, no wait, no early base load, no tile finish, no publish
+        masks = {0, 1024, 3072, 3072 | 4096, 3072 | 8192, 3072 | 8192 | 16384, 3072 | 4096 | 8192 | 16384,
+                 256 | 3072 | 4096 | 8192 | 16384}
+    for mask in sorted(masks):
         check(L().lsmblk_debug_set(ctx, 1, mask))
         for _ in range(2):
             batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
@@ -958,6 +970,26 @@ def ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream):
         torch.cuda.synchronize()
         res[mask] = round(e0.elapsed_time(e1) / args.steps, 3)
     check(L().lsmblk_debug_set(ctx, 1, 0))
+    if args.ablate_lag or args.ablate_only:  # the lagged decode's per-tile realtime trace over one call
+        import ctypes
+        import numpy as _np
+        check(L().lsmblk_debug_set(ctx, 5, 1))
+        batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
+        NW = 16 + 8 * 32768
+        w = (ctypes.c_uint64 * NW)()
+        check(L().lsmblk_debug_counters(ctx, w, NW))
+        check(L().lsmblk_debug_set(ctx, 5, 0))
+        tr = _np.frombuffer(w, dtype=_np.uint64)[16:].reshape(-1, 8).astype(_np.int64)
+        nt = min(len(tr), (nblk + 63) // 64)
+        tr, m = tr[:nt], slice(1, max(2, nt - 256))
+        q = lambda x: {p: round(float(_np.percentile(x, p)) / 100, 2) for p in (10, 50, 90, 99)}  # us (100 MHz)
+        print(json.dumps({"trace_us": {
+            "first_count_to_finish_start": q(tr[:, 0] - tr[:, 4]),
+            "finish_duration": q(tr[:, 1] - tr[:, 0]),
+            "finish_done_to_decoder_start": q(tr[m, 5] - tr[m, 1]),
+            "decoder_wait": q(tr[m, 3] - tr[m, 2]),
+            "decoder_start_to_wait": q(tr[m, 2] - tr[m, 5]),
+            "kernel_span_us": round(float((tr[:, 3].max() - tr[:, 4].min()) / 100), 1)}}), flush=True)
     polls = {}
     for pm in (0, 1, 2):
         check(L().lsmblk_debug_set(ctx, 0, pm))

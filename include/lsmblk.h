@@ -159,8 +159,15 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
 #define LSMBLK_DEBUG_POLL_MODE 0
 #define LSMBLK_DEBUG_DECODE_SKIP 1
 #define LSMBLK_DEBUG_KERNEL_TIMING 2 /* 1: dispatch start/stop events on every kernel launch */
-#define LSMBLK_DEBUG_SINGLE_PASS_DECODE 3 /* 1: the single-pass look-back decode instead of count + scan + decode (A/B) */
+#define LSMBLK_DEBUG_TWO_PASS_DECODE 3 /* 1: count + tile scan + decode (three launches) instead of the lagged decode (A/B) */
+#define LSMBLK_DEBUG_DECODE_LAG 4 /* blocks the lagged decode counts ahead of its decodes (>= 128; default 8192) */
+#define LSMBLK_DEBUG_COUNTERS 5 /* 1: the lagged decode records a realtime trace per tile (lsmblk_debug_counters) */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
+/* The trace of the last lagged decode with LSMBLK_DEBUG_COUNTERS on (n <= 16 + 8 * 32768 words;
+ * synchronizes).  Words 16 + 8 t + k, 100 MHz s_memrealtime stamps of 64-block tile t: k = 0 tile
+ * finish starts, 1 the tile's bases are published, 2 / 3 its first decoder's base wait begins /
+ * ends, 4 its first count starts, 5 its first decoder starts. */
+int lsmblk_debug_counters(lsmblk_ctx* ctx, uint64_t* out, uint32_t n);
 /* Durations (ms) of the kernels of the last timed decode / encode call on this context:
  * [0] dec_count [1] dec_scan [2] decode [3] plan [4] emit; -1 if not recorded.  Waits for
  * the recorded events. */

@@ -82,6 +82,7 @@ SIGNATURES = [
     ("lsmblk_ctx_reserve", I, [P, U64, U64, U64]),
     ("lsmblk_debug_set", I, [P, I, U32]),
     ("lsmblk_ctx_kernel_times", I, [P, ctypes.POINTER(ctypes.c_float)]),
+    ("lsmblk_debug_counters", I, [P, ctypes.POINTER(ctypes.c_uint64), U32]),
     ("lsmblk_decode_batch", I, [P, P, P, U64, ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_decode_batch_ex", I, [P, P, P, U64, U32, U32, ctypes.POINTER(KVStreamC), P, P, P]),
     ("lsmblk_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, P, U64, P, U64, P, P]),

@@ -461,9 +461,12 @@ struct lsmblk_ctx {
   uint32_t* ent = nullptr;       // per (segment-local) block: its encoded size (plan walk)
   uint32_t* big_list = nullptr;  // n+1 u32: emit_big_kernel's per-block flags (bytes)
   uint64_t rec_cap = 0;
-  uint64_t* d1_gran = nullptr;   // single-pass decode look-back granules (uncached): 3 + 3 per tile of
-  uint64_t d1_blk_cap = 0;       //   kDW blocks (aggregate, inclusive prefix); blocks covered
-  bool dec_single_pass = false;  // diagnostics: the single-pass look-back decode instead (A/B)
+  uint64_t* lag_gran = nullptr;  // lagged decode granules (uncached): 3 aggregate + 3 base per block,
+  uint64_t lag_blk_cap = 0;      //   then 3 aggregate + 3 inclusive per 64-block tile; blocks covered
+  bool dec_two_pass = false;     // diagnostics: count + scan + decode instead of the lagged decode (A/B)
+  uint32_t dec_lag = 8192;       // blocks the lagged decode's counts run ahead of its decodes
+  uint64_t* dbg = nullptr;       // debug cycle counters (LSMBLK_DEBUG_COUNTERS), 16 words
+  bool dbg_on = false;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
   uint32_t skip = 0;             // decode ablation mask (timing experiments only)

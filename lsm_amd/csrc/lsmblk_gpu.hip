@@ -45,14 +45,27 @@ struct DecodeArgs {
   uint32_t tail;              // bytes after each block inside its range (4: the framing CRC)
   uint64_t* blk_ent;          // optional: first entry index of every block
   uint32_t skip;  // ablation mask (lsmblk_debug_set, timing experiments only): 2 keys,
-                  // 4 values, 8 per-entry metadata, 256 stop after staging, 512 after the tables
-  // single-pass decode (decode1_kernel): look-back state, uncached granules tagged with `tag`
-  uint64_t* tagg;             // 3 per kDW-block tile: the tile's (entries, key bytes, value bytes)
+                  // 4 values, 8 per-entry metadata, 256 stop after staging, 512 after the tables;
+                  // lagged decode: 1024 no count (aggregates 0), 2048 no wait for the base
+  // lagged decode (decode_lag_kernel): uncached granules tagged with `tag`
+  uint64_t* bagg;             // 3 per block: the block's (entries, key bytes, value bytes), from its count
+  uint64_t* bbase;            // 3 per block: the block's output base (entries, key bytes, value bytes)
+  uint64_t* tagg;             // 3 per kTile-block tile: the tile's aggregate
   uint64_t* tinc;             // 3 per tile: inclusive prefix through the tile
+  uint64_t lag;               // workgroup j counts block j and decodes block j - lag
+  uint64_t* dbg;              // optional realtime trace per tile (lsmblk_debug_counters)
   uint32_t tag, poll;
 };
 
 constexpr uint32_t kTile = 64;  // blocks per count tile
+// debug buffer (LSMBLK_DEBUG_COUNTERS): 16 reserved words, then an 8-word s_memrealtime (100 MHz)
+// trace per tile for the first kDbgTiles tiles: [0] finish start [1] bases published [2] first
+// decoder's base wait begins [3] ends [4] the tile's first count starts [5] its first decoder starts
+constexpr uint32_t kDbgTiles = 32768, kDbgWords = 16 + 8 * kDbgTiles;
+__device__ __forceinline__ void dbg_trace(uint64_t* dbg, uint64_t t, uint32_t k) {
+  if (dbg && t < kDbgTiles && lane_id() == 0) dbg[16 + 8 * t + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 
 // LDS reads per lane issued together before their uses (one LDS round trip per batch instead
 // of one per read): flushes, value copies, chunk moves.
@@ -71,7 +84,7 @@ struct alignas(16) DecLds {
   uint8_t img[kDecImg];
   alignas(16) uint8_t out[kDecOut];  // decoded key run, then (16-B aligned) value run
 };
-static_assert(sizeof(DecLds) == 8160, "decode LDS: 20 blocks per CU, with room for decode1's shared words");
+static_assert(sizeof(DecLds) == 8160, "decode LDS: 20 blocks per CU");
 
 // Entry tables of a large block (kDecMaxE entries at a time).  A large block is not staged, so
 // the tables live in the unused image.
@@ -534,20 +547,32 @@ __device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const r
   }
 }
 
-__device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
+// Decode block b = [start, end) of the block stream.  mid() runs after the block's staging loads
+// are issued and before they are written to LDS (the lagged decode counts another block through
+// the image there, its loads issued before these).
+// post() runs once the staging has landed, pre_wait() before the wait for the output base.
+template <bool lagm, class Mid, class Post, class PreWait>
+__device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_t start, uint64_t end, Mid&& mid,
+                             Post&& post, PreWait&& pre_wait) {
   const uint32_t l = lane_id();
   uint32_t err = 0;
-  // output-base loads depend only on b: issue them first, they land during staging + parse
+  // output-base loads depend only on b: issue them first, they land during staging + parse.
+  // Lagged decode: the block's base granules (lanes 0-2); two-pass: the tile prefix + the
+  // aggregates of the tile's earlier blocks.
   const uint64_t tb = b / kTile, jb = b % kTile;
   uint32_t cn = 0, ck = 0, cv = 0;
-  if (l < jb) {
-    const uint64_t q = tb * kTile + l;
-    cn = a.agg[3 * q];
-    ck = a.agg[3 * q + 1];
-    cv = a.agg[3 * q + 2];
+  uint64_t tp0 = 0, tp1 = 0, tp2 = 0, gb = 0;
+  if constexpr (lagm) {
+    if (l < 3 && !(a.skip & 4096)) gb = gload(a.bbase + 3 * b + l, 0);  // (4096: ablation)
+  } else {
+    if (l < jb) {
+      const uint64_t q = tb * kTile + l;
+      cn = a.agg[3 * q];
+      ck = a.agg[3 * q + 1];
+      cv = a.agg[3 * q + 2];
+    }
+    tp0 = a.tile_pre[3 * tb], tp1 = a.tile_pre[3 * tb + 1], tp2 = a.tile_pre[3 * tb + 2];
   }
-  const uint64_t tp0 = a.tile_pre[3 * tb], tp1 = a.tile_pre[3 * tb + 1], tp2 = a.tile_pre[3 * tb + 2];
-  const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
   uint32_t len = 0;
   if (end < start + a.tail || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
   else len = uint32_t(end - start) - a.tail;
@@ -562,15 +587,35 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
     // all loads in flight before the first LDS write (kDecImg / 1 KiB = at most 5 per lane)
     const uint32_t nchunk = (lead + len + 15) >> 4;
     u32x4 v[5];
+    if constexpr (lagm) {
+      // Issued by inline asm so that the compiler can neither sink them below mid() (it did, below
+      // the whole count) nor wait for them inside it: mid()'s own waits count only the loads the
+      // compiler issued, so they over-wait by these (safe: returns are in issue order).  Landed
+      // by the explicit vmcnt(0) below, before any store is issued after them.
+      const uint32_t o = 16 * l, o4 = o + 4096;
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v[0]) : "v"(o), "s"(R));
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:1024" : "=v"(v[1]) : "v"(o), "s"(R));
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:2048" : "=v"(v[2]) : "v"(o), "s"(R));
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:3072" : "=v"(v[3]) : "v"(o), "s"(R));
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v[4]) : "v"(o4), "s"(R));
+      mid();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-    for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);
+      for (uint32_t i = 0; i < 5; ++i) asm volatile("" : "+v"(v[i]));  // defined here for the compiler
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);  // 0 past the block
+    }
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
       if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
     wave_sync();
+    post();
     h = parse_hdr(LdsImg{L.img, lead}, len);
   } else {
+    mid();
+    post();
     h = parse_hdr(GlbImg{R, lead}, len);
   }
   if (a.skip & 256) return;  // ablation: staging only
@@ -648,17 +693,48 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
   uint64_t agg[3] = {h.n, K, V};
   if (err) agg[0] = agg[1] = agg[2] = 0;
 
+  pre_wait();
   // output bases: tile prefix + this tile's earlier blocks
   uint64_t excl[3];
-  excl[0] = tp0 + wave_sum(cn);
-  excl[1] = tp1 + wave_sum(ck);
-  excl[2] = tp2 + wave_sum(cv);
+  if constexpr (lagm) {
+    // the block's base, published by its tile's last counter (normally long since there)
+    const uint64_t want = (uint64_t(a.tag) << 2) | 2;
+    uint32_t spins = 0;
+    if (b % kTile == 0) dbg_trace(a.dbg, b / kTile, 2);
+    while (!(a.skip & 2048) && __ballot(l < 3 && (gb & 0xFFFF) != want)) {  // (2048: ablation, no wait)
+      if (++spins > kSpinLimit) {
+        err |= LSMBLK_ERR_TIMEOUT;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (l < 3 && (gb & 0xFFFF) != want) gb = gload(a.bbase + 3 * b + l, a.poll);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q)
+      excl[q] = uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(gb >> 16), q))) |
+                (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(gb >> 48), q))) << 32);
+    if (b % kTile == 0) dbg_trace(a.dbg, b / kTile, 3);
+  } else {
+    excl[0] = tp0 + wave_sum(cn);
+    excl[1] = tp1 + wave_sum(ck);
+    excl[2] = tp2 + wave_sum(cv);
+  }
   wave_sync();
   const uint64_t E0 = excl[0], K0 = excl[1], V0 = excl[2];
   if (a.blk_ent && l == 0) a.blk_ent[b] = E0;
   const uint64_t Et = E0 + agg[0], Kt = K0 + agg[1], Vt = V0 + agg[2];
   if (Kt > 0xFFFFFFFFull || Vt > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
   if (Et > a.entry_cap || Kt > a.key_cap || Vt > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
+  if (lagm && b + 1 == a.nblk && l == 0) {  // totals, required sizes and the sentinels (as dec_scan_kernel)
+    if (a.blk_ent) a.blk_ent[a.nblk] = Et;
+    a.stats[0] = Et;
+    a.stats[1] = Kt;
+    a.stats[2] = Vt;
+    if (Et <= a.entry_cap) {
+      a.key_off[Et] = uint32_t(Kt);
+      a.val_off[Et] = uint32_t(Vt);
+    }
+  }
 
   if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
     if (fast) {
@@ -689,24 +765,26 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b) {
 // count + scan passes.
 __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
   __shared__ DecLds lds;
-  decode_block(a, lds, blockIdx.x);
+  const uint64_t b = blockIdx.x;
+  decode_block<false>(a, lds, b, uni64(a.blk_off[b]), uni64(a.blk_off[b + 1]), [] {}, [] {}, [] {});
 }
 
-// ---------------------------------------------------------------- single-pass decode
-// E is read once.  A workgroup decodes kDW consecutive blocks, one wave each (a look-back tile).
-// Every wave stages and parses its block as decode_block does and puts the block's (entries,
-// key bytes, value bytes) in LDS.  Wave 0, the tile's leader, then publishes the tile aggregate,
-// finds the tile's base by a decoupled look-back over earlier tiles (uncached granules), publishes
-// the tile's inclusive prefix and hands the base to the other waves through LDS -- while they
-// compose their key and value runs in their LDS output images at 16-B alignment 0, work that needs
-// no base.  The flush reads the image shifted by the base's alignment (unaligned ds_read_b128) and
-// writes aligned 16-B chunks.
-// Measured on the way (1 Mi U blocks): one block per workgroup, with a look-back tile of 16 blocks
-// summed from per-block uncached granules: 3.0 ms, of which the waits were 1.6 ms (an uncached
-// round trip under the full HBM load costs microseconds); with a dispatch ticket per block
-// instead of blockIdx: 12 ms (one atomic on one word by a million waves, ~11 ns each); waiting for
-// tile t-1's inclusive prefix instead of looking back: the prefixes became a serial chain.
-constexpr uint32_t kDW = 4;  // blocks (waves) per workgroup = per look-back tile
+// ---------------------------------------------------------------- lagged decode (one launch)
+// E is read from HBM once.  Workgroup j counts block j (stages it, parses its headers with decode's
+// rules, publishes its (entries, key bytes, value bytes) as a tagged granule) and then decodes
+// block j - lag.  The counts run `lag` blocks ahead of the decodes, so:
+//   * a block's output base is ready long before its decode starts: the last counter of each
+//     64-block tile sums the tile, finds the tile's prefix by a decoupled look-back over tiles and
+//     publishes every block's base (one granule triple per block, read by its decoder);
+//   * the decode's second read of the block comes from the Infinity Cache: between the two reads
+//     the chip reads `lag` further blocks and writes their decoded bytes (~8 KiB each; lag 8192
+//     = 67 MB of the 256 MB cache).
+// Every wait is on lower-indexed workgroups (dispatch is in index order), bounded by kSpinLimit
+// (then TIMEOUT).  The two-pass path (count, tile scan, decode: three launches) remains for the
+// CRC-verifying read and as the A/B diagnostic.
+// Measured before: a single pass holding each block in LDS across its
+// look-back (tiles of 4 blocks, one wave each) took 3.4 ms against 2.3 for the two passes -- the
+// look-back waits idle the LDS that bounds decode's residency.
 
 __device__ __forceinline__ uint64_t sat47(uint64_t v) { return v > (1ull << 47) - 1 ? (1ull << 47) - 1 : v; }
 
@@ -719,290 +797,194 @@ __device__ __forceinline__ void publish3(uint64_t* arr, uint64_t idx, uint64_t x
   if (l < 3) gstore(arr + 3 * idx + l, (sat47(x) << 16) | (uint64_t(tag) << 2) | flag, poll);
 }
 
-// The workgroup's shared words (after the waves' images).
-struct Dec1Shared {
-  uint32_t n[kDW], k[kDW], v[kDW];  // the blocks' aggregates (k: saturated at 2^31 - 1)
-  uint32_t ready;                   // bit w: wave w's aggregate is in place
-  uint32_t base_ready;              // the leader's base is in place
-  uint32_t err;                     // the leader's error flags (look-back timeout)
-  uint32_t pad;
-  uint64_t X[3];                    // the tile's base: all earlier tiles' entries, key bytes, value bytes
+// (entries, key bytes, value bytes) of block [start, end) with decode's rules; malformed ->
+// (0, 0, 0), bad.  cnt_issue issues the staging loads (a block that fits the image), cnt_finish
+// lands them in img and parses there (else parses from global memory).
+struct BlkCount {
+  uint32_t n;
+  uint64_t K, V;
+  bool bad;
 };
-static_assert(kDW * sizeof(DecLds) + sizeof(Dec1Shared) <= 32768, "decode1: five workgroups (20 blocks) per CU");
-
-// Sum of the aggregates of all tiles before t: tile t-1's inclusive prefix if it is there at once,
-// else a wave-parallel look-back over the tile aggregates.
-__device__ __forceinline__ bool d1_tiles(const DecodeArgs& a, uint64_t t, uint64_t (&x)[3]) {
-  x[0] = x[1] = x[2] = 0;
-  if (t == 0) return true;
+struct CntPre {
+  rsrc_t R;
+  uint32_t len, lead;
+  bool ok, staged;
+  u32x4 v[5];
+};
+__device__ __forceinline__ CntPre cnt_issue(const uint8_t* blocks, uint32_t tail, uint64_t start, uint64_t end) {
   const uint32_t l = lane_id();
-  const uint64_t want = (uint64_t(a.tag) << 2) | 2;
-  uint64_t g = want;
-  if (l < 3) g = gload(a.tinc + 3 * (t - 1) + l, 0);
-  if (!__ballot((g & 0xFFFF) != want)) {
-#pragma unroll
-    for (uint32_t q = 0; q < 3; ++q) x[q] = uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(g >> 16), q))) |
-                                          (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(g >> 48), q))) << 32);
-    return true;
-  }
-  return lookback<3>(a.tagg, a.tinc, t, a.tag, a.poll, x);
-}
-
-// The store half of the fast path after the base is known: the key or value run composed at
-// alignment 0 is flushed to its unaligned global place (LDS read shifted back by the base's 16-B
-// phase, aligned 16-B global stores).
-__device__ __forceinline__ void flush_run_shifted(uint8_t* gdst_aligned, const uint8_t* lds_run, uint32_t lo,
-                                                  uint32_t len) {
-  const uint32_t end = lo + len, nc = (end + 15) >> 4;
-  const uint32_t l = lane_id();
-  for (uint32_t c0 = 0; c0 < nc; c0 += 64 * kLB) {
-    u32x4 q[kLB];
-#pragma unroll
-    for (uint32_t j = 0; j < kLB; ++j) {
-      const uint32_t c = c0 + 64 * j + l;
-      if (c < nc) q[j] = *reinterpret_cast<const u32x4*>(lds_run + 16 * c - lo);  // run byte 16 c - lo
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kLB; ++j) {
-      const uint32_t c = c0 + 64 * j + l;
-      if (c < nc) {
-        const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-        store_chunk(gdst_aligned + 16 * c, v, 16 * c < lo ? lo - 16 * c : 0u, min(end - 16 * c, 16u));
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t lds_ld_acq(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ void decode1_block(const DecodeArgs& a, DecLds& L, Dec1Shared& S, uint32_t w, uint64_t b) {
-  const uint32_t l = lane_id();
-  uint32_t err = 0;
-  const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
-  uint32_t len = 0;
-  if (end < start + a.tail || end - start > 0x7FFFFFF0ull) err |= LSMBLK_ERR_MALFORMED;
-  else len = uint32_t(end - start) - a.tail;
-  const uint8_t* bp = a.blocks + start;
-  const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
-  const rsrc_t R = make_rsrc(bp - lead, lead + len);
-  const bool fits = lead + len + 15 <= kDecImg;
-
-  BlockHdr h;
-  if (fits) {
-    const uint32_t nchunk = (lead + len + 15) >> 4;
-    u32x4 v[5];
+  CntPre C;
+  C.ok = !(end < start + tail || end - start > 0x7FFFFFF0ull);
+  C.len = C.ok ? uint32_t(end - start) - tail : 0u;
+  const uint8_t* bp = blocks + start;
+  C.lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
+  C.R = make_rsrc(bp - C.lead, C.lead + C.len);
+  C.staged = C.ok && C.lead + C.len + 15 <= kDecImg;
+  if (C.staged) {
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);
-#pragma unroll
-    for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
-    wave_sync();
-    h = parse_hdr(LdsImg{L.img, lead}, len);
-  } else {
-    h = parse_hdr(GlbImg{R, lead}, len);
+      C.v[i] = __builtin_amdgcn_raw_buffer_load_b128(C.R, (l + 64 * i) * 16, 0, kLdAux);  // 0 past the block
   }
-  if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
-  const bool fast = fits && h.n <= kDecMaxE;
-  const bool big = !fits;
-
-  uint64_t K = 0, V = 0;
+  return C;
+}
+__device__ __forceinline__ BlkCount cnt_finish(const CntPre& C, uint8_t* img) {
+  const uint32_t l = lane_id();
+  BlkCount r{0, 0, 0, false};
   bool bad = false;
-  DecEnt ent[2] = {};
-  if (fast) {
-    const LdsImg im{L.img, lead};
-#pragma unroll
-    for (uint32_t it = 0; it < 2; ++it) {
-      if (64 * it >= h.n) break;
-      const uint32_t k = 64 * it + l;
-      uint32_t off = 0, p = 0, s = 0, vl = 0;
-      bool ok = true;
-      if (k < h.n) ok = parse_entry(im, h, k, off, p, s, vl);
-      bad = bad || !ok;
-      const uint32_t kl = p + s;
-      const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
-      ent[it] = DecEnt{off, p, s, uint32_t(K) + ki - kl, uint32_t(V) + vi - vl, vl};
-      K += __shfl(ki, 63, 64);
-      V += __shfl(vi, 63, 64);
+  auto count = [&](const auto& im) {
+    const BlockHdr h = parse_hdr(im, C.len);
+    if (!h.ok) {
+      bad = true;
+      return;
     }
-  } else {
+    r.n = h.n;
     for (uint32_t c = 0; c < h.n; c += 64) {
       const uint32_t k = c + l;
       uint32_t off = 0, p = 0, s = 0, vl = 0;
-      bool ok = true;
-      if (k < h.n) {
-        if (fits) ok = parse_entry(LdsImg{L.img, lead}, h, k, off, p, s, vl);
-        else ok = parse_entry(GlbImg{R, lead}, h, k, off, p, s, vl);
-      }
-      bad = bad || !ok;
-      K += wave_sum<uint64_t>(p + s);
-      V += wave_sum<uint64_t>(vl);
+      if (k < h.n && !parse_entry(im, h, k, off, p, s, vl)) bad = true;
+      r.K += wave_sum<uint32_t>(p + s);
+      r.V += wave_sum<uint32_t>(vl);
+    }
+  };
+  if (C.staged) {
+    const uint32_t nchunk = (C.lead + C.len + 15) >> 4;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(img + (l + 64 * i) * 16) = C.v[i];
+    wave_sync();
+    count(LdsImg{img, C.lead});
+  } else if (C.ok) {
+    count(GlbImg{C.R, C.lead});
+  }
+  if (!C.ok || __ballot(bad)) {
+    r.bad = true;
+    r.n = 0;
+    r.K = r.V = 0;
+  }
+  return r;
+}
+
+// The last counter of tile t: waits for the tile's aggregates, publishes the tile aggregate, looks
+// back over the tiles for its prefix, publishes the inclusive prefix and every block's base.
+__device__ void lag_tile_finish(const DecodeArgs& a, uint64_t t, uint32_t& err) {
+  const uint32_t l = lane_id();
+  dbg_trace(a.dbg, t, 0);
+  const uint64_t b0 = t * kTile, nb = min(uint64_t(kTile), a.nblk - b0);
+  const uint64_t want = (uint64_t(a.tag) << 2) | 1;
+  uint64_t g0 = want, g1 = want, g2 = want;  // lanes >= nb read as present zeros
+  const bool mine = l < nb;
+  if (mine) {
+    g0 = gload(a.bagg + 3 * (b0 + l), 0);
+    g1 = gload(a.bagg + 3 * (b0 + l) + 1, 0);
+    g2 = gload(a.bagg + 3 * (b0 + l) + 2, 0);
+  }
+  uint32_t spins = 0;
+  for (;;) {
+    const bool here = (g0 & 0xFFFF) == want && (g1 & 0xFFFF) == want && (g2 & 0xFFFF) == want;
+    if (!__ballot(!here)) break;
+    if (++spins > kSpinLimit) {
+      err |= LSMBLK_ERR_TIMEOUT;
+      return;  // the decoders of this tile time out too: the call reports TIMEOUT
+    }
+    __builtin_amdgcn_s_sleep(1);
+    if (!here) {
+      g0 = gload(a.bagg + 3 * (b0 + l), a.poll);
+      g1 = gload(a.bagg + 3 * (b0 + l) + 1, a.poll);
+      g2 = gload(a.bagg + 3 * (b0 + l) + 2, a.poll);
     }
   }
-  if (__ballot(bad)) err |= LSMBLK_ERR_MALFORMED;
-  if (K > 0x7FFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;  // one block's keys cannot fit a batch's u32 offsets anyway
-  uint64_t agg[3] = {h.n, K, V};
-  if (err) agg[0] = agg[1] = agg[2] = 0;
-  // this block's aggregate, for the leader and the later waves of the tile
-  if (l == 0) {
-    S.n[w] = uint32_t(agg[0]);
-    S.k[w] = uint32_t(agg[1]);
-    S.v[w] = uint32_t(agg[2]);
-    __hip_atomic_fetch_or(&S.ready, 1u << w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-
-  const uint64_t t = b / kDW;
-  const uint32_t nw = uint32_t(min(uint64_t(kDW), a.nblk - t * kDW));  // blocks of this tile
-  uint32_t spins = 0;
-  auto lds_wait = [&](const uint32_t* p, uint32_t want_mask) {
-    while ((lds_ld_acq(p) & want_mask) != want_mask) {
-      if (++spins > kSpinLimit) {
+  const uint64_t x0 = mine ? g0 >> 16 : 0, x1 = mine ? g1 >> 16 : 0, x2 = mine ? g2 >> 16 : 0;
+  const uint64_t i0 = wave_incl_scan<uint64_t>(x0), i1 = wave_incl_scan<uint64_t>(x1), i2 = wave_incl_scan<uint64_t>(x2);
+  const uint64_t A[3] = {lane64(i0, 63), lane64(i1, 63), lane64(i2, 63)};
+  uint64_t X[3] = {0, 0, 0};
+  if (t == 0) {
+    publish3(a.tinc, t, A[0], A[1], A[2], a.tag, 2, a.poll);
+  } else {
+    publish3(a.tagg, t, A[0], A[1], A[2], a.tag, 1, a.poll);
+    // tile t-1's inclusive prefix if it is there at once, else the wave-parallel look-back
+    const uint64_t wi = (uint64_t(a.tag) << 2) | 2;
+    uint64_t g = wi;
+    if (l < 3) g = gload(a.tinc + 3 * (t - 1) + l, 0);
+    if (!__ballot(l < 3 && (g & 0xFFFF) != wi)) {
+#pragma unroll
+      for (uint32_t q = 0; q < 3; ++q)
+        X[q] = uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(g >> 16), q))) |
+               (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(g >> 48), q))) << 32);
+    } else {
+      if (!lookback<3>(a.tagg, a.tinc, t, a.tag, a.poll, X)) {
         err |= LSMBLK_ERR_TIMEOUT;
         return;
       }
-      __builtin_amdgcn_s_sleep(1);
     }
-  };
-  if (w == 0) {
-    // leader: the tile aggregate, the look-back, the inclusive prefix, the base for the others
-    lds_wait(&S.ready, (1u << nw) - 1);
-    uint64_t A0 = 0, A1 = 0, A2 = 0;
-    for (uint32_t i = 0; i < nw; ++i) {
-      A0 += S.n[i];
-      A1 += S.k[i];
-      A2 += S.v[i];
-    }
-    publish3(a.tagg, t, A0, A1, A2, a.tag, 1, a.poll);
-    uint64_t X[3];
-    if (!d1_tiles(a, t, X)) {
-      err |= LSMBLK_ERR_TIMEOUT;
-      X[0] = X[1] = X[2] = 0;
-    }
-    publish3(a.tinc, t, X[0] + A0, X[1] + A1, X[2] + A2, a.tag, 2, a.poll);
-    if (l == 0) {
-      S.X[0] = X[0];
-      S.X[1] = X[1];
-      S.X[2] = X[2];
-      S.err = err & LSMBLK_ERR_TIMEOUT;
-      __hip_atomic_store(&S.base_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    publish3(a.tinc, t, X[0] + A[0], X[1] + A[1], X[2] + A[2], a.tag, 2, a.poll);
   }
-
-  // the work that needs no base: the fast path composes its runs at alignment 0
-  const uint32_t vrun = (uint32_t(K) + 15) & ~15u;
-  const bool composed = fast && !err && h.n && vrun + uint32_t(V) + 15 <= kDecOut;
-  if (composed) {
-    dec_entry_runs(a, L, lead, h.n, ent, 0, 0, 0, LdsSink{L.out, 0, vrun}, a.skip | 8);
-    wave_sync();
+  if (mine) {
+    const uint64_t tg = (uint64_t(a.tag) << 2) | 2;
+    gstore(a.bbase + 3 * (b0 + l), (sat47(X[0] + i0 - x0) << 16) | tg, a.poll);
+    gstore(a.bbase + 3 * (b0 + l) + 1, (sat47(X[1] + i1 - x1) << 16) | tg, a.poll);
+    gstore(a.bbase + 3 * (b0 + l) + 2, (sat47(X[2] + i2 - x2) << 16) | tg, a.poll);
   }
-
-  // the base: the tile's base + the tile's earlier blocks
-  if (w != 0) lds_wait(&S.base_ready, 1u);
-  err |= S.err;
-  uint64_t E0 = S.X[0], K0 = S.X[1], V0 = S.X[2];
-  for (uint32_t i = 0; i < w; ++i) {
-    E0 += S.n[i];
-    K0 += S.k[i];
-    V0 += S.v[i];
+  if (a.dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dbg_trace(a.dbg, t, 1);
   }
-  E0 = uni64(E0);
-  K0 = uni64(K0);
-  V0 = uni64(V0);
-  if (a.blk_ent && l == 0) a.blk_ent[b] = E0;
-  const uint64_t Et = E0 + agg[0], Kt = K0 + agg[1], Vt = V0 + agg[2];
-  if (Kt > 0xFFFFFFFFull || Vt > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
-  if (Et > a.entry_cap || Kt > a.key_cap || Vt > a.val_cap) err |= LSMBLK_ERR_CAPACITY;
-  if (b + 1 == a.nblk && l == 0) {  // totals, required sizes and the sentinels (as dec_scan_kernel)
-    if (a.blk_ent) a.blk_ent[a.nblk] = Et;
-    a.stats[0] = Et;
-    a.stats[1] = Kt;
-    a.stats[2] = Vt;
-    if (Et <= a.entry_cap) {
-      a.key_off[Et] = uint32_t(Kt);
-      a.val_off[Et] = uint32_t(Vt);
-    }
-  }
-
-  if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
-    if (composed) {
-      if (!(a.skip & 8)) {
-#pragma unroll
-        for (uint32_t it = 0; it < 2; ++it) {
-          const uint32_t k = 64 * it + l;
-          if (k >= h.n) continue;
-          const uint64_t e = E0 + k;
-          const u32x2 q = *reinterpret_cast<const u32x2*>(L.img + lead + ent[it].epos + 4 + ent[it].s);
-          a.ts[e] = __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
-          a.key_off[e] = uint32_t(K0 + ent[it].kout);
-          a.val_off[e] = uint32_t(V0 + ent[it].vout);
-        }
-      }
-      const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
-      flush_run_shifted(a.keys + (K0 - kb), L.out, kb, uint32_t(K));
-      flush_run_shifted(a.vals + (V0 - vb), L.out + vrun, vb, uint32_t(V));
-    } else if (fast) {
-      dec_fast_outputs(a, L, lead, h, ent, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
-    } else if (big) {
-      DecTables& T = *reinterpret_cast<DecTables*>(L.img);  // large blocks are not staged
-      uint64_t kr = 0, vr = 0;
-      for (uint32_t c0 = 0; c0 < h.n; c0 += kDecMaxE) {
-        const uint32_t cn = min(kDecMaxE, h.n - c0);
-        wave_sync();  // the previous chunk's table reads are done
-        const GlbImg im{R, lead};
-        for (uint32_t c = 0; c < cn; c += 64) {
-          const uint32_t k = c + l;
-          uint32_t off = 0, p = 0, s = 0, vl = 0;
-          if (k < cn) parse_entry(im, h, c0 + k, off, p, s, vl);
-          const uint32_t kl = p + s;
-          const uint32_t ki = wave_incl_scan<uint32_t>(kl), vi = wave_incl_scan<uint32_t>(vl);
-          if (k < cn) {
-            T.epos[k] = uint16_t(off);
-            T.pfx[k] = uint16_t(p);
-            T.sfx[k] = uint16_t(s);
-            T.kout[k] = uint32_t(kr) + ki - kl;
-            T.vout[k] = uint32_t(vr) + vi - vl;
-          }
-          kr += __shfl(ki, 63, 64);
-          vr += __shfl(vi, 63, 64);
-        }
-        if (l == 0) {
-          T.kout[cn] = uint32_t(kr);
-          T.vout[cn] = uint32_t(vr);
-        }
-        wave_sync();
-        dec_big_outputs(a, T, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V));
-      }
-    } else {
-      dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
-    }
-  }
-  raise_err(a.stats, err);
 }
 
-// Block b = kDW * workgroup + wave.  Waiting is only ever for lower-indexed blocks, and
-// workgroups are dispatched in index order (round-robin over the XCDs, in order on each), so
-// every block waited for has been dispatched before the waiter.  (A dispatch ticket per block --
-// one atomic on one word by a million waves -- serialised at ~11 ns per block.)  All waits are
-// bounded (kSpinLimit): a violation reports TIMEOUT instead of hanging.
-__global__ __launch_bounds__(64 * kDW) void decode1_kernel(DecodeArgs a) {
-  __shared__ DecLds lds[kDW];
-  __shared__ Dec1Shared S;
-  const uint32_t w = wave_id();
-  if (threadIdx.x == 0) {
-    S.ready = 0;
-    S.base_ready = 0;
-    S.err = 0;
+__global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
+  __shared__ DecLds lds;
+  const uint64_t j = blockIdx.x;
+  const bool cnt = j < a.nblk, dec = j >= a.lag;
+  if (j % kTile == 0) dbg_trace(a.dbg, j / kTile, 4);                     // the tile's first count starts
+  if (dec && (j - a.lag) % kTile == 0) dbg_trace(a.dbg, (j - a.lag) / kTile, 5);  // its first decoder starts
+  const uint64_t b = j - a.lag;
+  // both blocks' ranges first, then the count's staging loads, then (inside decode_block) the
+  // decode's: the count waits only for its own loads
+  // (one load instruction: lanes 0-1 the count's range, lanes 2-3 the decode's)
+  const uint32_t l = lane_id();
+  uint64_t o = 0;
+  if ((l < 2 && cnt) || (l >= 2 && l < 4 && dec)) o = a.blk_off[(l < 2 ? j : b) + (l & 1)];
+  const uint64_t cs = lane64(o, 0), ce = lane64(o, 1), ds = lane64(o, 2), de = lane64(o, 3);
+  CntPre C;
+  const bool do_cnt = cnt && !(a.skip & 1024);  // (1024: ablation, aggregates 0 without the count)
+  if (do_cnt) C = cnt_issue(a.blocks, a.tail, cs, ce);
+  uint32_t err = 0;
+  BlkCount r{0, 0, 0, false};
+  auto count = [&] {
+    if (!do_cnt) return;
+    r = cnt_finish(C, lds.img);
+    wave_sync();  // the count's image reads are done before the decode stages into it
+  };
+  // (the count's aggregate is published after the decode's staging has landed: a store issued
+  // before the landing's vmcnt(0) would be waited for there)
+  // Tile t's bases are published by workgroup f(t) = 64 t + 63 + lag / 2 - (t & 7), after its own
+  // block's entry parse and before its own decode waits for a base.  By then the tile's counts
+  // have long been published (no waiting on a slow XCD's tile-mates), f(t) < f(t + 1) (the tile
+  // look-back finds its predecessors' aggregates), f(t) is far below the tile's first decoder
+  // (64 t + lag), and the finishers rotate over the XCDs (workgroup j runs on XCD j mod 8).
+  // Measured before: the tile's last-arriving count finishing it (an arrival counter) put every
+  // tile finish on the slowest XCD -- which then stayed `lag` behind, the other XCDs' decoders
+  // waiting (2.8 ms at every lag); the tile's last block finishing it after its own decode
+  // chained the tiles `lag` apart into one serial sequence (2.7 ms).
+  const uint64_t D = a.lag / 2 + 63;
+  const uint64_t ft = j >= D ? (j - D + 8) / kTile : ~0ull;  // the tile workgroup j finishes, if any
+  const bool fin = j >= D && ft * kTile + D - (ft & 7) == j && ft * kTile < a.nblk;
+  auto publish = [&] {
+    if (!cnt || (a.skip & 16384)) return;  // (16384: ablation, no publish)
+    // (a malformed block is reported by its decoder; its aggregate is 0 there too)
+    publish3(a.bagg, j, r.n, r.K, r.V, a.tag, 1, a.poll);
+    if (r.K > 0xFFFFFFFFull || r.V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+  };
+  auto finish = [&] {
+    if (fin && !(a.skip & (8192 | 16384))) lag_tile_finish(a, ft, err);  // (8192: ablation, no tile finish)
+  };
+  if (dec) {
+    decode_block<true>(a, lds, b, ds, de, count, publish, finish);
+  } else {
+    count();
+    publish();
+    finish();
   }
-  __syncthreads();
-  const uint64_t b = uint64_t(blockIdx.x) * kDW + w;
-  if (b < a.nblk) {
-    decode1_block(a, lds[w], S, w, b);
-  } else if (lane_id() == 0) {  // no block: an empty aggregate for the leader
-    S.n[w] = S.k[w] = S.v[w] = 0;
-    __hip_atomic_fetch_or(&S.ready, 1u << w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
+  raise_err(a.stats, err);
 }
 
 // ---------------------------------------------------------------- decode pass 1: count
@@ -1026,56 +1008,13 @@ struct CountArgs {
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void dec_count_staged_kernel(CountArgs a) {
   __shared__ alignas(16) uint8_t img[kDecImg];
   const uint64_t b = blockIdx.x;
-  const uint32_t l = lane_id();
-  const uint64_t start = uni64(a.blk_off[b]), end = uni64(a.blk_off[b + 1]);
-  bool ok = !(end < start + a.tail || end - start > 0x7FFFFFF0ull);
-  const uint32_t len = ok ? uint32_t(end - start) - a.tail : 0u;
-  const uint8_t* bp = a.blocks + start;
-  const uint32_t lead = uni(uint32_t(reinterpret_cast<uintptr_t>(bp) & 15));
-  const rsrc_t R = make_rsrc(bp - lead, lead + len);
-  uint64_t K = 0, V = 0;
-  uint32_t n = 0;
-  bool bad = false;
-  auto count = [&](const auto& im) {
-    const BlockHdr h = parse_hdr(im, len);
-    if (!h.ok) {
-      bad = true;
-      return;
-    }
-    n = h.n;
-    for (uint32_t c = 0; c < h.n; c += 64) {
-      const uint32_t k = c + l;
-      uint32_t off = 0, p = 0, s = 0, vl = 0;
-      if (k < h.n && !parse_entry(im, h, k, off, p, s, vl)) bad = true;
-      K += wave_sum<uint32_t>(p + s);
-      V += wave_sum<uint32_t>(vl);
-    }
-  };
-  if (ok && lead + len + 15 <= kDecImg) {
-    const uint32_t nchunk = (lead + len + 15) >> 4;
-    u32x4 v[5];
-#pragma unroll
-    for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) v[i] = __builtin_amdgcn_raw_buffer_load_b128(R, (l + 64 * i) * 16, 0, kLdAux);
-#pragma unroll
-    for (uint32_t i = 0; i < 5; ++i)
-      if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(img + (l + 64 * i) * 16) = v[i];
-    wave_sync();
-    count(LdsImg{img, lead});
-  } else if (ok) {
-    count(GlbImg{R, lead});
-  }
-  uint32_t err = 0;
-  if (!ok || __ballot(bad)) {
-    err |= LSMBLK_ERR_MALFORMED;
-    n = 0;
-    K = V = 0;
-  }
-  if (l == 0) {
-    a.agg[3 * b] = n;
-    a.agg[3 * b + 1] = uint32_t(K > 0xFFFFFFFFull ? 0xFFFFFFFFull : K);
-    a.agg[3 * b + 2] = uint32_t(V > 0xFFFFFFFFull ? 0xFFFFFFFFull : V);
-    if (K > 0xFFFFFFFFull || V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
+  const BlkCount r = cnt_finish(cnt_issue(a.blocks, a.tail, uni64(a.blk_off[b]), uni64(a.blk_off[b + 1])), img);
+  uint32_t err = r.bad ? LSMBLK_ERR_MALFORMED : 0u;
+  if (lane_id() == 0) {
+    a.agg[3 * b] = r.n;
+    a.agg[3 * b + 1] = uint32_t(r.K > 0xFFFFFFFFull ? 0xFFFFFFFFull : r.K);
+    a.agg[3 * b + 2] = uint32_t(r.V > 0xFFFFFFFFull ? 0xFFFFFFFFull : r.V);
+    if (r.K > 0xFFFFFFFFull || r.V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
   }
   raise_err(a.stats, err);
 }
@@ -2712,6 +2651,9 @@ __global__ __launch_bounds__(256) void filt_write_kernel(FiltArgs a) {
 // ================================================================ host side
 namespace {
 
+// per block 3 aggregate + 3 base granules; per tile 3 aggregate + 3 inclusive granules
+uint64_t lag_words(uint64_t nb) { return 6 * nb + 6 * ((nb + kTile - 1) / kTile + 1); }
+
 int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t segs) {
   int rc;
   uint64_t cap;
@@ -2726,15 +2668,15 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
     if ((rc = grow(&c->tile_pre, &cap, tiles, 3))) return rc;
     c->tile_cap = cap;
   }
-  if (blocks > c->d1_blk_cap) {
-    // one arena: 3 granules per kDW-block tile (aggregate), then 3 per tile (inclusive prefix)
+  if (blocks > c->lag_blk_cap) {
+    // one arena: per block 3 aggregate + 3 base granules, then per tile 3 aggregate + 3 inclusive
     const uint64_t nb = blocks + blocks / 4 + 1024;
     cap = 0;  // (grow frees the old arena)
-    if ((rc = grow(&c->d1_gran, &cap, 6 * ((nb + kDW - 1) / kDW + 1), 1, kStatusFlags))) {
-      c->d1_blk_cap = 0;
+    if ((rc = grow(&c->lag_gran, &cap, lag_words(nb), 1, kStatusFlags))) {
+      c->lag_blk_cap = 0;
       return rc;
     }
-    c->d1_blk_cap = nb;
+    c->lag_blk_cap = nb;
     c->epoch = 0;  // the fresh arena is zeroed; the next call starts a new epoch sequence
   }
   if (segs > c->seg_cap) {
@@ -2766,9 +2708,8 @@ int next_epoch(lsmblk_ctx* c, hipStream_t st) {
       if (hipMemsetAsync(c->seg_agg, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
       if (hipMemsetAsync(c->seg_inc, 0, c->seg_cap * 2 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     }
-    if (c->d1_blk_cap) {
-      const uint64_t words = 6 * ((c->d1_blk_cap + kDW - 1) / kDW + 1);
-      if (hipMemsetAsync(c->d1_gran, 0, words * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    if (c->lag_blk_cap) {
+      if (hipMemsetAsync(c->lag_gran, 0, lag_words(c->lag_blk_cap) * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     }
     c->epoch = 0;
   }
@@ -2838,7 +2779,8 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->vcrc);
   (void)hipFree(c->sws);
   (void)hipFree(c->rws);
-  (void)hipFree(c->d1_gran);
+  (void)hipFree(c->lag_gran);
+  (void)hipFree(c->dbg);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -2851,8 +2793,19 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->poll = value;
   } else if (key == LSMBLK_DEBUG_DECODE_SKIP) {
     c->skip = value;
-  } else if (key == LSMBLK_DEBUG_SINGLE_PASS_DECODE) {
-    c->dec_single_pass = value != 0;
+  } else if (key == LSMBLK_DEBUG_TWO_PASS_DECODE) {
+    c->dec_two_pass = value != 0;
+  } else if (key == LSMBLK_DEBUG_COUNTERS) {
+    if (value && !c->dbg) {
+      DeviceGuard dg(c->device);
+      if (!dg.ok || hipMalloc(reinterpret_cast<void**>(&c->dbg), kDbgWords * 8) != hipSuccess) {
+        c->dbg = nullptr;
+        return LSMBLK_E_NOMEM;
+      }
+    }
+    c->dbg_on = value != 0;
+  } else if (key == LSMBLK_DEBUG_DECODE_LAG && value >= 2 * kTile && value <= (1u << 24)) {
+    c->dec_lag = value;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->ev[0]) {
       DeviceGuard dg(c->device);
@@ -2865,6 +2818,16 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     return LSMBLK_E_INVAL;
   }
   return LSMBLK_OK;
+}
+
+int lsmblk_debug_counters(lsmblk_ctx* c, uint64_t* out, uint32_t n) {
+  if (!c || !out || n > kDbgWords) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (uint32_t i = 0; i < n; ++i) out[i] = 0;
+  if (!c->dbg) return LSMBLK_OK;
+  DeviceGuard dg(c->device);
+  if (!dg.ok || hipDeviceSynchronize() != hipSuccess) return LSMBLK_E_HIP;
+  return hipMemcpy(out, c->dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
 int lsmblk_ctx_kernel_times(lsmblk_ctx* c, float* ms) {
@@ -2948,16 +2911,22 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   a.tail = tail;
   a.blk_ent = blk_ent;
   a.skip = c->skip;
-  a.tagg = a.tinc = nullptr;
+  a.bagg = a.bbase = a.tagg = a.tinc = a.dbg = nullptr;
+  a.lag = 0;
   a.tag = a.poll = 0;
-  if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && c->dec_single_pass) {
-    // single pass: E is read once (decode1_kernel; diagnostic, slower at U: DESIGN.md section 8)
+  if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && !c->dec_two_pass) {
+    // lagged decode: E is read from HBM once, one launch (decode_lag_kernel)
     if ((rc = next_epoch(c, st))) return rc;
-    a.tagg = c->d1_gran;
-    a.tinc = a.tagg + 3 * ((c->d1_blk_cap + kDW - 1) / kDW + 1);
+    a.bagg = c->lag_gran;
+    a.bbase = a.bagg + 3 * c->lag_blk_cap;
+    a.tagg = a.bbase + 3 * c->lag_blk_cap;
+    a.tinc = a.tagg + 3 * ((c->lag_blk_cap + kTile - 1) / kTile + 1);
+    a.lag = c->dec_lag;
+    a.dbg = c->dbg_on ? c->dbg : nullptr;
+    if (a.dbg && hipMemsetAsync(a.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     a.tag = c->epoch;
     a.poll = c->poll;
-    tlaunch(c, decode1_kernel, dim3(uint32_t((nblk + kDW - 1) / kDW)), dim3(64 * kDW), st, 4, 5, a);
+    tlaunch(c, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), st, 4, 5, a);
     if (c->timing) {  // the count and scan slots of lsmblk_ctx_kernel_times read 0
       (void)hipEventRecord(c->ev[0], st);
       (void)hipEventRecord(c->ev[1], st);

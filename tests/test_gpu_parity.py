@@ -618,9 +618,12 @@ def test_verifying_decode_counts_in_the_crc_pass(gen, n, bs):
 
 
 @pytest.mark.parametrize("cfg,n", [("U", 30000), ("Z", 30000), ("M", 4000)])
-def test_single_pass_decode_path(cfg, n):
-    """The single-pass look-back decode (LSMBLK_DEBUG_SINGLE_PASS_DECODE, the A/B alternative to
-    count + scan + decode) gives the oracle's stream and block entry index."""
+@pytest.mark.parametrize("mode", ["two_pass", "lag128", "lag_beyond_batch"])
+def test_decode_modes(cfg, n, mode):
+    """The A/B decode paths give the oracle's stream and block entry index: count + scan + decode
+    (LSMBLK_DEBUG_TWO_PASS_DECODE), and the lagged decode at its smallest lag (128: each tile's
+    finisher, lag / 2 + 63 workgroups after the tile's first count, just ahead of the tile's first
+    decoder) and at a lag beyond the batch (every count before any decode)."""
     from lsm_amd._lib import lib
     kv = O.KV(*synth.GENERATORS[cfg](n, seed=21))
     seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 128 << 10)
@@ -628,12 +631,27 @@ def test_single_pass_decode_path(cfg, n):
     rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
     assert rc == 0
     ctx = batch._ctx(0)
-    lib().lsmblk_debug_set(ctx, 3, 1)
+    if mode == "two_pass":
+        assert lib().lsmblk_debug_set(ctx, 3, 1) == 0
+    else:
+        assert lib().lsmblk_debug_set(ctx, 4, 128 if mode == "lag128" else 1 << 20) == 0
     try:
         for shift in (0, 5):
             db, do = dev_blocks(ref_blocks, ref_off, shift)
             assert_kv_equal(batch.decode_blocks(db, do), ref_kv)
         out, ent = batch.decode_blocks(*dev_blocks(ref_blocks, ref_off), with_blk_ent=True)
-        np.testing.assert_array_equal(ent.cpu().numpy().view(np.uint64)[-1], kv.n)
+        counts = [int.from_bytes(ref_blocks[int(ref_off[i + 1]) - 2:int(ref_off[i + 1])].tobytes(), "big")
+                  for i in range(len(ref_off) - 1)]
+        np.testing.assert_array_equal(ent.cpu().numpy().view(np.uint64), np.concatenate([[0], np.cumsum(counts)]))
     finally:
         lib().lsmblk_debug_set(ctx, 3, 0)
+        lib().lsmblk_debug_set(ctx, 4, 8192)
+
+
+def test_decode_lag_setting_bounds():
+    """Lags below two tiles or above 2^24 blocks are refused."""
+    from lsm_amd._lib import lib
+    ctx = batch._ctx(0)
+    assert lib().lsmblk_debug_set(ctx, 4, 127) != 0
+    assert lib().lsmblk_debug_set(ctx, 4, (1 << 24) + 1) != 0
+    assert lib().lsmblk_debug_set(ctx, 4, 8192) == 0
