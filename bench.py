@@ -77,6 +77,7 @@ def parse(argv=None):
     p.add_argument("--decode-lag", type=int, default=None,
                    help="diagnostics (A/B): blocks the lagged decode counts ahead of its decodes (default 8192)")
     p.add_argument("--ablate-lag", action="store_true", help="diagnostics: the lagged decode's ablation masks")
+    p.add_argument("--trace-plan", action="store_true", help="diagnostics: the plan walk's per-segment trace")
     p.add_argument("--ablate-only", action="store_true", help="diagnostics: time only mask 0 and --ablate")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
@@ -223,6 +224,26 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
         if ev is not None:
             ev[2].record(stream)
 
+    if args.trace_plan and not extra:  # the plan walk's per-segment realtime trace over one encode
+        import ctypes
+        step()
+        torch.cuda.synchronize()
+        check(lib().lsmblk_debug_set(ctx, 5, 1))
+        batch.encode_into(out_kv, seg_t, len(seg) - 1, bs, out_blocks, out_cap, out_off, blk_cap, st_enc)
+        NW = 16 + 8 * 32768
+        w = (ctypes.c_uint64 * NW)()
+        check(lib().lsmblk_debug_counters(ctx, w, NW))
+        check(lib().lsmblk_debug_set(ctx, 5, 0))
+        tr = np.frombuffer(w, dtype=np.uint64)[16:].reshape(-1, 8).astype(np.int64)[:len(seg) - 1]
+        t0 = tr[:, 0].min()
+        q = lambda x: {p: round(float(np.percentile(x, p)), 2) for p in (10, 50, 90, 100)}
+        print(json.dumps({"plan_trace": {
+            "walk_start_us": q((tr[:, 0] - t0) / 100), "walk_us": q((tr[:, 1] - tr[:, 0]) / 100),
+            "walk_wait_frac": q(tr[:, 2] / np.maximum(1, tr[:, 1] - tr[:, 0])),
+            "windows": q(tr[:, 3]), "blocks": q(tr[:, 7]),
+            "helper_us": q((tr[:, 5] - tr[:, 4]) / 100), "helper_wait_frac": q(tr[:, 6] / np.maximum(1, tr[:, 5] - tr[:, 4])),
+            "walk_end_us": q((tr[:, 1] - t0) / 100)}}), flush=True)
+        return None
     if args.ablate is not None and not extra:
         if 16 <= args.ablate < 256:  # encode-side masks: per-kernel times with the mask applied
             res = {}

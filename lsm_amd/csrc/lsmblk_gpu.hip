@@ -1125,6 +1125,7 @@ struct PlanArgs {
   const uint64_t* dn;      // optional: n read from device memory (overrides n)
   const uint32_t* dnseg;   // optional: nseg read from device memory (overrides nseg)
   uint32_t span;           // segments cover [seg_start[0], seg_start[nseg]) of the stream, not all of it
+  uint64_t* dbg;           // optional realtime trace per segment (LSMBLK_DEBUG_COUNTERS)
 };
 
 __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
@@ -1192,14 +1193,17 @@ constexpr uint32_t kChunk = 256;         // entries per producer hand-off (1024 
 // A chunk may overwrite the ring's older half once the walker's window has left it;
 // prod[0] = entries produced (relative to s0), cons[0] = walker's window start (relative).
 __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, uint32_t s1, uint32_t* CR,
-                             uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t& err) {
+                             uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t& err, uint64_t* tr) {
   const uint32_t l = lane_id();
+  uint64_t waited = 0;
+  if (tr && l == 0) tr[4] = __builtin_amdgcn_s_memrealtime();
   const uint32_t klim = K.glead + uni(a.key_off[a.n]);
   for (uint32_t c = s0; c < s1; c += kChunk) {
     const uint32_t cend = s1 - c < kChunk ? s1 : c + kChunk;
     if (c - s0 + kChunk > kRing) {  // ring space: the walker's window must have passed c + kChunk - kRing
       const uint32_t need = c - s0 + kChunk - kRing;
       uint32_t spins = 0;
+      const uint64_t w0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
       while (__hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
         if (++spins > kSpinMax) {
           err |= LSMBLK_ERR_TIMEOUT;
@@ -1207,6 +1211,7 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (tr) waited += __builtin_amdgcn_s_memrealtime() - w0;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 #pragma unroll 1
@@ -1290,6 +1295,10 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (l == 0) __hip_atomic_store(prod, cend - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  if (tr && l == 0) {
+    tr[5] = __builtin_amdgcn_s_memrealtime();
+    tr[6] = waited;
+  }
 }
 
 // (fused: three workgroups of 8 waves per CU, so that up to 3 K segments walk at once)
@@ -1323,8 +1332,9 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     if (s1 < s0) s1 = s0;
   }
   const PlanKeys K = plan_keys(a);
+  uint64_t* const tr = a.dbg && g < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(g) : nullptr;  // (diagnostics)
   if (wv >= 4) {
-    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err);
+    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
     const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
                           (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
     raise_err(a.stats, werr);
@@ -1334,9 +1344,13 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
   // until the window's entries are in and tells the helper where the window starts.
   uint32_t known = 0;  // entries of the ring the producer has finished (relative to s0)
   bool stalled = false;
+  uint64_t waited = 0, windows = 0;
+  if (tr && l == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
   auto need = [&](uint32_t j0, uint32_t wend) {
     __hip_atomic_store(&hand_cons[ww], j0 - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (tr) ++windows;
     if (wend - s0 > known && !stalled) {
+      const uint64_t w0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
       uint32_t spins = 0;
       while ((known = __hip_atomic_load(&hand_prod[ww], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < wend - s0) {
         if (++spins > kSpinMax) {
@@ -1346,6 +1360,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (tr) waited += __builtin_amdgcn_s_memrealtime() - w0;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
   };
@@ -1438,6 +1453,12 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       }
       carry += lane64(incl, 63);
     }
+  }
+  if (tr && l == 0) {
+    tr[1] = __builtin_amdgcn_s_memrealtime();
+    tr[2] = waited;
+    tr[3] = windows;
+    tr[7] = nb;
   }
   // make this wave's record stores visible to its own later loads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -3029,6 +3050,8 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.dn = dn;
   p.dnseg = dnseg;
   p.span = span ? 1u : 0u;
+  p.dbg = c->dbg_on ? c->dbg : nullptr;
+  if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   c->enc_timed = c->timing;
   tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, 6, 7, p);
   // the big-block flags are cleared before emit (the start of emit_kernel to the end of
