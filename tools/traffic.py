@@ -9,7 +9,7 @@ usage: python tools/traffic.py PMC_DIR WORKLOAD BLOCKS OUT_JSON
 import csv, glob, json, os, sys
 from collections import defaultdict
 
-NAMES = {"decode_lag_kernel": "decode", "dec_count_kernel": "dec_count", "dec_count_staged_kernel": "dec_count", "dec_scan_kernel": "dec_scan", "decode_kernel": "decode",
+NAMES = {"decode_lag_kernel": "decode", "dec_count_kernel": "dec_count", "dec_count_staged_kernel": "dec_count", "dec_scan_kernel": "dec_scan", "decode_kernel": "decode_two_pass",
          "plan_adj_kernel": "plan_adj", "plan_walk_kernel": "plan_walk", "emit_kernel": "emit",
          "crc_kernel<false>": "crc32", "crc_kernel<true>": "crc32_count", "agg_tile_kernel": "agg_tile"}
 root, workload, blocks, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
