@@ -245,6 +245,15 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
             "walk_end_us": q((tr[:, 1] - t0) / 100)}}), flush=True)
         return None
     if args.ablate is not None and not extra:
+        if args.ablate >= 65536:  # plan masks: the plan kernel alone (emit not launched)
+            res = {}
+            for mask in (0, 1 << 16, 1 << 17, 3 << 16):
+                check(lib().lsmblk_debug_set(ctx, 1, mask))
+                step()
+                res[mask] = kernel_times(ctx, step, dev, reps=2)["plan"]
+            check(lib().lsmblk_debug_set(ctx, 1, 0))
+            print(json.dumps({"ablation_plan_ms_by_skip_mask": res}), flush=True)
+            return None
         if 16 <= args.ablate < 256:  # encode-side masks: per-kernel times with the mask applied
             res = {}
             for mask in (0, 16, 32, 64, 112, 128, 240):

@@ -593,11 +593,17 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
       // compiler issued, so they over-wait by these (safe: returns are in issue order).  Landed
       // by the explicit vmcnt(0) below, before any store is issued after them.
       const uint32_t o = 16 * l, o4 = o + 4096;
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v[0]) : "v"(o), "s"(R));
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:1024" : "=v"(v[1]) : "v"(o), "s"(R));
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:2048" : "=v"(v[2]) : "v"(o), "s"(R));
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:3072" : "=v"(v[3]) : "v"(o), "s"(R));
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v[4]) : "v"(o4), "s"(R));
+      // (one statement led by s_nop 4: a VALU write of R's SGPRs needs 5 wait states before a VMEM
+      // read of them, which the compiler's hazard pass does not check inside asm)
+      asm volatile(
+          "s_nop 4\n\t"
+          "buffer_load_dwordx4 %0, %5, %7, 0 offen\n\t"
+          "buffer_load_dwordx4 %1, %5, %7, 0 offen offset:1024\n\t"
+          "buffer_load_dwordx4 %2, %5, %7, 0 offen offset:2048\n\t"
+          "buffer_load_dwordx4 %3, %5, %7, 0 offen offset:3072\n\t"
+          "buffer_load_dwordx4 %4, %6, %7, 0 offen"
+          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4])
+          : "v"(o), "v"(o4), "s"(R));
       mid();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1126,6 +1132,8 @@ struct PlanArgs {
   const uint32_t* dnseg;   // optional: nseg read from device memory (overrides nseg)
   uint32_t span;           // segments cover [seg_start[0], seg_start[nseg]) of the stream, not all of it
   uint64_t* dbg;           // optional realtime trace per segment (LSMBLK_DEBUG_COUNTERS)
+  uint32_t skip;           // ablation (timing only, emit not launched): 1 << 16 helpers skip the key
+                           // loads and LCPs, 1 << 17 walkers skip the scans (one block per window)
 };
 
 __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
@@ -1230,10 +1238,11 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
         }
       }
       u32x4 xk[kProdBatch], xp[kProdBatch];
+      const bool nokeys = a.skip & (1u << 16);
 #pragma unroll
       for (uint32_t i = 0; i < kProdBatch; ++i) {
         const uint32_t e = c + 64 * (h + i) + l;
-        if (e < cend && e != s0) {
+        if (e < cend && e != s0 && !nokeys) {
           xk[i] = __builtin_amdgcn_raw_buffer_load_b128(K.gk, K.glead + kp[i], 0, 0);
           xp[i] = __builtin_amdgcn_raw_buffer_load_b128(K.gk, K.glead + pp[i], 0, 0);
         }
@@ -1245,7 +1254,7 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
         const uint32_t kl = kn[i] - kp[i], x = (e - s0) & (kRing - 1);
         if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
         uint32_t al = 0;
-        if (e != s0) {  // as plan_adj_kernel: LCP with the predecessor, bit 31 = out of order
+        if (e != s0 && !nokeys) {  // as plan_adj_kernel: LCP with the predecessor, bit 31 = out of order
           const uint32_t pl = kp[i] - pp[i], m = pl < kl ? pl : kl;
           uint32_t lcp = m, w0 = 0, w1 = 0;
           bool done = false;
@@ -1375,6 +1384,17 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     for (uint32_t j0 = s;; j0 += 64) {
       const uint32_t wend = s1 - j0 < 64 ? s1 : j0 + 64;
       need(j0, wend);
+      if (a.skip & (1u << 17)) {  // ablation: consume the window as one block, no scans
+        const uint32_t x = (j0 + l - s0) & (kRing - 1);
+        const uint32_t rr = j0 + l < s1 ? CR[x] + CA[x] : 0u;
+        if (l == 0) {
+          a.rec_first[s0 + nb] = s;
+          a.sz[s0 + nb] = __builtin_amdgcn_readfirstlane(rr);
+        }
+        ++nb;
+        s = wend;
+        break;
+      }
       const uint32_t e = j0 + l;
       const bool valid = e < s1;
       uint32_t r = 0, al = kAlcpLcp;
@@ -3050,10 +3070,18 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.dn = dn;
   p.dnseg = dnseg;
   p.span = span ? 1u : 0u;
+  p.skip = c->skip;
   p.dbg = c->dbg_on ? c->dbg : nullptr;
   if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   c->enc_timed = c->timing;
   tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, 6, 7, p);
+  if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
+    if (c->timing) {
+      (void)hipEventRecord(c->ev[8], st);
+      (void)hipEventRecord(c->ev[9], st);
+    }
+    return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  }
   // the big-block flags are cleared before emit (the start of emit_kernel to the end of
   // emit_big_kernel is what bench.py's roofline divides by)
   const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;  // blocks <= entries, <= blk_cap

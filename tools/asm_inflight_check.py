@@ -1,0 +1,139 @@
+"""Check, on the gfx950 ISA of one kernel, that no instruction reads or writes the registers of
+inline-asm loads between the loads and an inline-asm `s_waitcnt vmcnt` (CFG reachability).
+usage: python tools/asm_inflight_check.py ISA.s KERNEL_SYMBOL_SUBSTRING"""
+import re
+import sys
+
+
+def main(path, kname):
+    s = open(path).read()
+    name_line = [l for l in s.split('\n') if l.startswith('_') and kname in l and re.match(r'^\S+:', l)][0]
+    name_line = name_line.split(':')[0] + ':'
+
+    start = s.index('\n' + name_line) + 1
+    end = s.index('.Lfunc_end', start)
+    body = s[start:end].split('\n')
+    # basic blocks
+    labels, blocks = {}, []
+    cur = []
+    for k, l in enumerate(body):
+        t = l.strip()
+        m = re.match(r'^(\.LBB\d+_\d+):', t)
+        if m or t.startswith('; %bb.'):
+            if cur:
+                blocks.append(cur)
+            cur = [k]
+            if m:
+                labels[m.group(1)] = len(blocks)
+        else:
+            cur.append(k)
+    blocks.append(cur)
+    blk_of = {}
+    for bi, b in enumerate(blocks):
+        for k in b:
+            blk_of[k] = bi
+
+    def succs(bi):
+        out = []
+        last = None
+        for k in blocks[bi]:
+            t = body[k].strip()
+            if t and not t.startswith(';') and not t.startswith('.'):
+                last = t
+        for k in blocks[bi]:
+            m = re.search(r's_c?branch\w*\s+(\.LBB\d+_\d+)', body[k])
+            if m:
+                out.append(labels[m.group(1)])
+        if not (last and (last.startswith('s_branch') or last.startswith('s_endpgm'))) and bi + 1 < len(blocks):
+            out.append(bi + 1)
+        return out
+
+    def regs_in(t):
+        r = set()
+        for m in re.finditer(r'v\[(\d+):(\d+)\]', t):
+            r |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+        for m in re.finditer(r'\bv(\d+)\b', t):
+            r.add(int(m.group(1)))
+        return r
+
+    asm_loads, asm_waits, asm_any = [], set(), set()
+    inside = False
+    for k, l in enumerate(body):
+        if ';;#ASMSTART' in l:
+            inside = True
+            continue
+        if ';;#ASMEND' in l:
+            inside = False
+            continue
+        if inside:
+            t = l.strip()
+            asm_any.add(k)
+            if t.startswith('buffer_load') or t.startswith('global_load'):
+                asm_loads.append(k)
+            if t.startswith('s_waitcnt') and 'vmcnt' in t:
+                asm_waits.add(k)
+    regs = set()
+    for k in asm_loads:
+        regs |= regs_in(body[k].split(',')[0])
+    bad = 0
+    for k0 in asm_loads:
+        seen = set()
+        stack = [(blk_of[k0], k0 + 1)]
+        while stack:
+            bi, startk = stack.pop()
+            if (bi, startk) in seen:
+                continue
+            seen.add((bi, startk))
+            stop = False
+            for k in blocks[bi]:
+                if k < startk:
+                    continue
+                t = body[k].strip()
+                if k in asm_waits:
+                    stop = True
+                    break
+                if not t or t.startswith(';') or t.startswith('.') or k in asm_any:
+                    continue
+                u = regs_in(t) & regs
+                if u:
+                    bad += 1
+                    if bad <= 20:
+                        print(f"line {k}: {sorted(u)} {t[:100]}  (after asm load line {k0})")
+            if not stop:
+                for sb in succs(bi):
+                    stack.append((sb, blocks[sb][0]))
+    # gfx9 hazard: a VALU write of an SGPR that a VMEM instruction reads needs 5 wait states; the
+    # compiler's hazard recognizer may not look inside inline asm
+    def sregs(t):
+        r = set()
+        for m in re.finditer(r's\[(\d+):(\d+)\]', t):
+            r |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+        for m in re.finditer(r'\bs(\d+)\b', t):
+            r.add(int(m.group(1)))
+        return r
+    for k in sorted(asm_any):
+        t = body[k].strip()
+        if not (t.startswith('buffer_') or t.startswith('global_')):
+            continue
+        used = sregs(t)
+        waits, q = 0, k - 1
+        while q >= 0 and waits < 5:
+            u = body[q].strip()
+            if u.startswith('.LBB') or u.startswith('; %bb'):
+                break
+            if u and not u.startswith(';') and not u.startswith('.'):
+                op = u.split()[0]
+                if op.startswith('v_') and u.split()[1].rstrip(',').startswith('s'):
+                    if sregs(u.split(',')[0]) & used:
+                        bad += 1
+                        print(f"line {k}: VALU SGPR write at line {q} within {waits} wait states: {u[:80]}")
+                m = re.match(r's_nop\s+(\d+)', u)
+                waits += (int(m.group(1)) + 1) if m else 1
+            q -= 1
+    print(f"{len(asm_loads)} asm loads, {len(asm_waits)} asm waits, registers {sorted(regs)}: "
+          f"{'OK' if not bad else str(bad) + ' VIOLATIONS'}")
+    return 1 if bad else 0
+
+
+if __name__ == '__main__':
+    sys.exit(main(sys.argv[1], sys.argv[2]))
