@@ -75,7 +75,7 @@ def parse(argv=None):
     p.add_argument("--decode-two-pass", action="store_true",
                    help="diagnostics (A/B): count + tile scan + decode (three launches) instead of the lagged decode")
     p.add_argument("--decode-lag", type=int, default=None,
-                   help="diagnostics (A/B): blocks the lagged decode counts ahead of its decodes (default 8192)")
+                   help="diagnostics (A/B): blocks the lagged decode counts ahead of its decodes (default 10240)")
     p.add_argument("--ablate-lag", action="store_true", help="diagnostics: the lagged decode's ablation masks")
     p.add_argument("--trace-plan", action="store_true", help="diagnostics: the plan walk's per-segment trace")
     p.add_argument("--ablate-only", action="store_true", help="diagnostics: time only mask 0 and --ablate")

@@ -783,8 +783,8 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 //     64-block tile sums the tile, finds the tile's prefix by a decoupled look-back over tiles and
 //     publishes every block's base (one granule triple per block, read by its decoder);
 //   * the decode's second read of the block comes from the Infinity Cache: between the two reads
-//     the chip reads `lag` further blocks and writes their decoded bytes (~8 KiB each; lag 8192
-//     = 67 MB of the 256 MB cache).
+//     the chip reads `lag` further blocks and writes their decoded bytes (~8 KiB each; lag 10240
+//     = 84 MB of the 256 MB cache; lag 8192 / 10240 / 12288: decode 2.11 / 2.08-2.09 / 2.10 ms).
 // Every wait is on lower-indexed workgroups (dispatch is in index order), bounded by kSpinLimit
 // (then TIMEOUT).  The two-pass path (count, tile scan, decode: three launches) remains for the
 // CRC-verifying read and as the A/B diagnostic.

@@ -645,7 +645,7 @@ def test_decode_modes(cfg, n, mode):
         np.testing.assert_array_equal(ent.cpu().numpy().view(np.uint64), np.concatenate([[0], np.cumsum(counts)]))
     finally:
         lib().lsmblk_debug_set(ctx, 3, 0)
-        lib().lsmblk_debug_set(ctx, 4, 8192)
+        lib().lsmblk_debug_set(ctx, 4, 10240)
 
 
 def test_decode_lag_setting_bounds():
@@ -654,4 +654,4 @@ def test_decode_lag_setting_bounds():
     ctx = batch._ctx(0)
     assert lib().lsmblk_debug_set(ctx, 4, 127) != 0
     assert lib().lsmblk_debug_set(ctx, 4, (1 << 24) + 1) != 0
-    assert lib().lsmblk_debug_set(ctx, 4, 8192) == 0
+    assert lib().lsmblk_debug_set(ctx, 4, 10240) == 0
