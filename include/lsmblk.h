@@ -160,7 +160,9 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
 #define LSMBLK_DEBUG_DECODE_SKIP 1
 #define LSMBLK_DEBUG_KERNEL_TIMING 2 /* 1: dispatch start/stop events on every kernel launch */
 #define LSMBLK_DEBUG_TWO_PASS_DECODE 3 /* 1: count + tile scan + decode (three launches) instead of the lagged decode (A/B) */
-#define LSMBLK_DEBUG_DECODE_LAG 4 /* blocks the lagged decode counts ahead of its decodes (>= 128; default 10240) */
+#define LSMBLK_DEBUG_DECODE_LAG 4 /* blocks the lagged decode counts ahead of its decodes (>= 128; default: 40 MiB of
+                                     blocks at the batch's mean block size, at most 10240); setting it fixes the lag, 0 restores the default */
+#define LSMBLK_DEBUG_DECODE_LAG_BYTES 6 /* the lagged decode's lag in bytes of blocks (default 40 MiB; 0: the lag set by key 4) */
 #define LSMBLK_DEBUG_COUNTERS 5 /* 1: the lagged decode records a realtime trace per tile (lsmblk_debug_counters) */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* The trace of the last lagged decode with LSMBLK_DEBUG_COUNTERS on (n <= 16 + 8 * 32768 words;

@@ -443,6 +443,9 @@ inline void crc_host_tables(CrcTabs& T) {
 
 }  // namespace
 
+constexpr uint32_t kDecLagDefault = 10240;
+constexpr uint64_t kDecLagBytesDefault = 10240ull * 4096;
+
 struct lsmblk_ctx {
   int device = 0;
   std::mutex mu;
@@ -464,7 +467,8 @@ struct lsmblk_ctx {
   uint64_t* lag_gran = nullptr;  // lagged decode granules (uncached): 3 aggregate + 3 base per block,
   uint64_t lag_blk_cap = 0;      //   then 3 aggregate + 3 inclusive per 64-block tile; blocks covered
   bool dec_two_pass = false;     // diagnostics: count + scan + decode instead of the lagged decode (A/B)
-  uint32_t dec_lag = 10240;      // blocks the lagged decode's counts run ahead of its decodes
+  uint32_t dec_lag = kDecLagDefault;  // blocks the lagged decode's counts run ahead of its decodes, at most;
+  uint64_t dec_lag_bytes = kDecLagBytesDefault;  // that many bytes of blocks at the mean block size (0: exactly dec_lag)
   uint64_t* dbg = nullptr;       // debug cycle counters (LSMBLK_DEBUG_COUNTERS), 16 words
   bool dbg_on = false;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing

@@ -52,7 +52,8 @@ struct DecodeArgs {
   uint64_t* bbase;            // 3 per block: the block's output base (entries, key bytes, value bytes)
   uint64_t* tagg;             // 3 per kTile-block tile: the tile's aggregate
   uint64_t* tinc;             // 3 per tile: inclusive prefix through the tile
-  uint64_t lag;               // workgroup j counts block j and decodes block j - lag
+  uint64_t lag;               // workgroup j counts block j and decodes block j - lag (at most)
+  uint64_t lag_bytes;         // nonzero: the lag is lag_bytes of blocks at the batch's mean block size
   uint64_t* dbg;              // optional realtime trace per tile (lsmblk_debug_counters)
   uint32_t tag, poll;
 };
@@ -437,47 +438,109 @@ __device__ __forceinline__ void copy_run_wave(const rsrc_t& RS, uint32_t so, con
 // pieces are numbered consecutively over the lanes (wave scan of the piece counts) and each
 // lane moves pieces lane, lane + 64, ... of that numbering, kBigB loads in flight per lane --
 // so a wave round trip moves 8 KiB whatever the run lengths.  (One run after another cost a
-// round trip per run: ~46 per 64 KiB block of config M.)  A piece finds its run by a binary
-// search over the lanes' first-piece numbers (ds_bpermute); a run's last piece overlaps the one
+// round trip per run: ~46 per 64 KiB block of config M.)  A run's last piece overlaps the one
 // before, so any length >= 16 is covered exactly.
+// A piece finds its run through the wave-private LDS scratch sc (kCopyScratch words): per row of
+// 64 pieces, each run starting in the row marks its slot with its lane + 1, and an inclusive
+// max-scan over the slots (carried from row to row) gives every piece its owner; the owner's
+// {source, destination, length - 16, first piece} is one 16-B LDS read.  (Round 2 searched the
+// lanes' first-piece numbers with 6 dependent ds_bpermutes and read the owner's fields with 4
+// more; the copies are most of M's large-block encode.)
+#ifndef LSMBLK_COPY_PIPE
+#define LSMBLK_COPY_PIPE true
+#endif
+#ifndef LSMBLK_DEC_COPY_PIPE
+#define LSMBLK_DEC_COPY_PIPE false
+#endif
+constexpr uint32_t kCopyScratch = 4 * 64 + 64;
+static_assert(4 * kCopyScratch <= kDecOut, "the decode's large-block path lends its output image");
+
+template <uint32_t B>
+struct CopyBatch {
+  u32x4 q[B];
+  uint32_t dst[B];
+};
+
+// Rows g0 .. g0 + 64 B of the piece numbering: owners, then the pieces' loads.
+template <uint32_t B>
+__device__ __forceinline__ void copy_issue(const rsrc_t& RS, uint32_t g0, uint32_t total, uint32_t np, uint32_t first,
+                                           uint32_t* sc, uint32_t& carry, CopyBatch<B>& c) {
+  const uint32_t l = lane_id();
+  const u32x4* rec = reinterpret_cast<const u32x4*>(sc);
+  uint32_t* mark = sc + 4 * 64;
+  uint32_t own[B];
+#pragma unroll
+  for (uint32_t j = 0; j < B; ++j) {
+    const uint32_t G = g0 + 64 * j;
+    own[j] = 0;
+    if (G < total) {  // wave-uniform
+      mark[l] = 0;
+      wave_sync();
+      if (np != 0 && first - G < 64u) mark[first - G] = l + 1;  // run starts are distinct pieces
+      wave_sync();
+      const uint32_t m = max(wave_incl_max32(mark[l]), carry);
+      carry = __builtin_amdgcn_readlane(m, 63);
+      own[j] = m - 1;
+      wave_sync();  // this row's slot reads are done before the next row clears them
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < B; ++j) {
+    const uint32_t g = g0 + 64 * j + l;
+    c.dst[j] = ~0u;
+    if (g < total) {
+      const u32x4 r = rec[own[j]];
+      const uint32_t off = min(16 * (g - r.w), r.z);
+      c.q[j] = gload16(RS, r.x + off);
+      c.dst[j] = r.y + off;
+    }
+  }
+}
+
+template <uint32_t B>
+__device__ __forceinline__ void copy_store(const rsrc_t& RD, const CopyBatch<B>& c) {
+#pragma unroll
+  for (uint32_t j = 0; j < B; ++j)
+    if (c.dst[j] != ~0u) {
+      const uint32_t v[4] = {c.q[j].x, c.q[j].y, c.q[j].z, c.q[j].w};
+      st16(RD, c.dst[j], v);
+    }
+}
+
+// pipe: the next batch's loads are issued before this batch's stores (kBigB / 2 pieces per lane
+// each), so the wait for a batch's loads never waits for the previous batch's stores (vmcnt
+// counts stores and retires in order).  The register cost is the same; the decode (whose VGPR
+// count sets its occupancy) keeps the plain loop.
+template <bool pipe = false>
 __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, uint32_t so, const rsrc_t& RD,
-                                               uint32_t dof, uint32_t len) {
+                                               uint32_t dof, uint32_t len, uint32_t* sc) {
   const uint32_t l = lane_id();
   const uint32_t np = longrun ? (len + 15) >> 4 : 0u;
   const uint32_t incl = wave_incl_scan32(np);
   const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  if (total == 0) return;
   const uint32_t first = incl - np;  // this lane's first piece number
-  for (uint32_t g0 = 0; g0 < total; g0 += 64 * kBigB) {
-    u32x4 q[kBigB];
-    uint32_t dst[kBigB];
-#pragma unroll
-    for (uint32_t j = 0; j < kBigB; ++j) {
-      const uint32_t g = g0 + 64 * j + l, gg = min(g, total - 1);
-      // owner: the last lane whose first piece number is <= g (a lane after the owner starts
-      // past g; lanes before it without pieces share its number but are not the last).  The
-      // search and the owner reads run on every lane: ds_bpermute reads nothing from a lane
-      // that is masked off, and the owner may be one whose own piece slot is past the end.
-      uint32_t lo = 0;
-#pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1) {
-        const uint32_t f = uint32_t(__shfl(first, int((lo + step) & 63), 64));
-        if (lo + step < 64 && f <= gg) lo += step;
-      }
-      const uint32_t o_so = uint32_t(__shfl(so, int(lo), 64)), o_dof = uint32_t(__shfl(dof, int(lo), 64));
-      const uint32_t o_len = uint32_t(__shfl(len, int(lo), 64)), o_first = uint32_t(__shfl(first, int(lo), 64));
-      const uint32_t off = min(16 * (gg - o_first), o_len - 16);
-      dst[j] = ~0u;
-      if (g < total) {
-        q[j] = gload16(RS, o_so + off);
-        dst[j] = o_dof + off;
-      }
+  wave_sync();                       // the scratch's previous readers are done
+  reinterpret_cast<u32x4*>(sc)[l] = u32x4{so, dof, len - 16, first};  // read only for lanes with a run
+  uint32_t carry = 0;  // owner + 1 of the previous row's last piece
+  if (!pipe) {
+    for (uint32_t g0 = 0; g0 < total; g0 += 64 * kBigB) {
+      CopyBatch<kBigB> c;
+      copy_issue(RS, g0, total, np, first, sc, carry, c);
+      copy_store(RD, c);
     }
-#pragma unroll
-    for (uint32_t j = 0; j < kBigB; ++j)
-      if (dst[j] != ~0u) {
-        const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-        st16(RD, dst[j], v);
-      }
+    return;
+  }
+  constexpr uint32_t H = kBigB / 2, R = 64 * H;
+  CopyBatch<H> c0, c1;
+  copy_issue(RS, 0, total, np, first, sc, carry, c0);
+  for (uint32_t g0 = R;; g0 += 2 * R) {
+    if (g0 < total) copy_issue(RS, g0, total, np, first, sc, carry, c1);
+    copy_store(RD, c0);
+    if (g0 >= total) break;
+    if (g0 + R < total) copy_issue(RS, g0 + R, total, np, first, sc, carry, c0);
+    copy_store(RD, c1);
+    if (g0 + R >= total) break;
   }
 }
 
@@ -526,7 +589,7 @@ __device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecTabl
 // Outputs of the n entries whose tables are in L (block entries Eb - E0 .. + n), large block.
 __device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const rsrc_t& R, uint32_t lead,
                                 const BlockHdr& h, uint32_t n, uint64_t Eb, uint64_t K0, uint64_t V0, uint32_t K,
-                                uint32_t V) {
+                                uint32_t V, uint32_t* sc) {
   const uint32_t l = lane_id();
   const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
   const rsrc_t RK = make_rsrc_exact(a.keys + (K0 - kb), kb + K), RV = make_rsrc_exact(a.vals + (V0 - vb), vb + V);
@@ -543,7 +606,7 @@ __device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const r
       vl = L.vout[k + 1] - L.vout[k];
       if (vl < kCoop) copy_run(R, vsrc, lim, RV, vdst, vl);
     }
-    copy_long_runs(live && vl >= kCoop, R, vsrc, RV, vdst, vl);
+    copy_long_runs<LSMBLK_DEC_COPY_PIPE>(live && vl >= kCoop, R, vsrc, RV, vdst, vl, sc);
   }
 }
 
@@ -746,7 +809,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
     if (fast) {
       dec_fast_outputs(a, L, lead, h, ent, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
     } else if (big && h.n <= kDecMaxE) {
-      dec_big_outputs(a, T, R, lead, h, h.n, E0, K0, V0, uint32_t(K), uint32_t(V));
+      dec_big_outputs(a, T, R, lead, h, h.n, E0, K0, V0, uint32_t(K), uint32_t(V), reinterpret_cast<uint32_t*>(L.out));
     } else if (big) {
       uint64_t kr = 0, vr = 0;
       for (uint32_t c0 = 0; c0 < h.n; c0 += kDecMaxE) {
@@ -754,7 +817,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
         wave_sync();  // the previous chunk's table reads are done
         parse_tables(GlbImg{R, lead}, c0, cn, kr, vr);
         wave_sync();
-        dec_big_outputs(a, T, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V));
+        dec_big_outputs(a, T, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V), reinterpret_cast<uint32_t*>(L.out));
       }
     } else if (fits) {
       dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
@@ -939,20 +1002,40 @@ __device__ void lag_tile_finish(const DecodeArgs& a, uint64_t t, uint32_t& err) 
 __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   __shared__ DecLds lds;
   const uint64_t j = blockIdx.x;
-  const bool cnt = j < a.nblk, dec = j >= a.lag;
-  if (j % kTile == 0) dbg_trace(a.dbg, j / kTile, 4);                     // the tile's first count starts
-  if (dec && (j - a.lag) % kTile == 0) dbg_trace(a.dbg, (j - a.lag) / kTile, 5);  // its first decoder starts
-  const uint64_t b = j - a.lag;
+  const bool cnt = j < a.nblk;
   // both blocks' ranges first, then the count's staging loads, then (inside decode_block) the
   // decode's: the count waits only for its own loads
-  // (one load instruction: lanes 0-1 the count's range, lanes 2-3 the decode's)
+  // (one load instruction: lanes 0-1 the count's range, lanes 2-3 the decode's at the largest lag)
+  // The lag scales with the block size (lag_bytes): the decode re-reads its block's bytes lag
+  // blocks after the count did (the parse of a large block, the whole staged image of a small
+  // one), and those reads should come from the Infinity Cache.  Measured on config M (64 KiB
+  // blocks): decode 2.11 ms at lag 10240 (640 MiB apart, headers re-read from HBM: 6.2 GB
+  // fetched for 4.3 GB of blocks), 2.02 at 640 (40 MiB, as 10240 x 4 KiB) and 2.01 at 320.
   const uint32_t l = lane_id();
   uint64_t o = 0;
-  if ((l < 2 && cnt) || (l >= 2 && l < 4 && dec)) o = a.blk_off[(l < 2 ? j : b) + (l & 1)];
-  const uint64_t cs = lane64(o, 0), ce = lane64(o, 1), ds = lane64(o, 2), de = lane64(o, 3);
+  if ((l < 2 && cnt) || (l >= 2 && l < 4 && j >= a.lag)) o = a.blk_off[(l < 2 ? j : j - a.lag) + (l & 1)];
+  // the batch's first and last offsets: scalar loads (as vector-load lanes they cost U's decode ~1 %)
+  const uint64_t o0 = a.lag_bytes ? a.blk_off[0] : 0, o1 = a.lag_bytes ? a.blk_off[a.nblk] : 0;
+  const uint64_t cs = lane64(o, 0), ce = lane64(o, 1);
   CntPre C;
   const bool do_cnt = cnt && !(a.skip & 1024);  // (1024: ablation, aggregates 0 without the count)
   if (do_cnt) C = cnt_issue(a.blocks, a.tail, cs, ce);
+  uint64_t lag = a.lag;  // (worked out under the count's loads)
+  if (a.lag_bytes) {
+    // lag_bytes / mean block size < lag?  (4 KiB units; products below 2^57; the divide only then)
+    const uint64_t tot = (o1 - o0) >> 12, lb = a.lag_bytes >> 12;
+    if (lb * a.nblk < lag * tot) {
+      const uint64_t want = uint64_t(float(uint32_t(lb)) * (float(uint32_t(a.nblk)) / float(uint32_t(tot))));
+      lag = want < 2 * kTile ? 2 * kTile : want;
+    }
+  }
+  if (j >= a.nblk + lag) return;  // (the grid is sized for the largest lag; no count was issued here)
+  const bool dec = j >= lag;
+  if (j % kTile == 0) dbg_trace(a.dbg, j / kTile, 4);                       // the tile's first count starts
+  if (dec && (j - lag) % kTile == 0) dbg_trace(a.dbg, (j - lag) / kTile, 5);  // its first decoder starts
+  const uint64_t b = j - lag;
+  if (lag != a.lag && dec && l >= 2 && l < 4) o = a.blk_off[b + (l & 1)];  // (wave-uniform branch)
+  const uint64_t ds = lane64(o, 2), de = lane64(o, 3);
   uint32_t err = 0;
   BlkCount r{0, 0, 0, false};
   auto count = [&] {
@@ -971,7 +1054,7 @@ __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   // tile finish on the slowest XCD -- which then stayed `lag` behind, the other XCDs' decoders
   // waiting (2.8 ms at every lag); the tile's last block finishing it after its own decode
   // chained the tiles `lag` apart into one serial sequence (2.7 ms).
-  const uint64_t D = a.lag / 2 + 63;
+  const uint64_t D = lag / 2 + 63;
   const uint64_t ft = j >= D ? (j - D + 8) / kTile : ~0ull;  // the tile workgroup j finishes, if any
   const bool fin = j >= D && ft * kTile + D - (ft & 7) == j && ft * kTile < a.nblk;
   auto publish = [&] {
@@ -1584,7 +1667,8 @@ __device__ __forceinline__ void lds_st_short(uint8_t* p, uint32_t len, const uin
 // first key in 16-B compares; suffix and value as 16-B unaligned buffer loads/stores with
 // batched loads (copy_run); header, ts and value_len as single unaligned stores; the offset
 // slot at data_len + 2k, data_len = size - 2n - 2 known from the plan (checked at the end).
-__device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, uint64_t size, uint32_t& err) {
+__device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, uint64_t size, uint32_t& err,
+                         uint32_t* sc) {
   const uint32_t l = lane_id();
   const uint32_t kg = uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15), vg = uint32_t(reinterpret_cast<uintptr_t>(a.vals) & 15);
   const uint32_t klim = kg + uni(a.key_off[a.n]), vlim = vg + uni(a.val_off[a.n]);  // valid descriptor bytes
@@ -1603,7 +1687,7 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
       kl = a.key_off[s + k + 1] - (kp - kg);
       vp = vg + a.val_off[s + k];
       vl = a.val_off[s + k + 1] - (vp - vg);
-      if (k != 0) {  // builder.rs:62 common_prefix(first_key, key)
+      if (k != 0 && !(a.skip & 128)) {  // builder.rs:62 common_prefix(first_key, key)
         const uint32_t m = fl < kl ? fl : kl;
         p = m;
         for (uint32_t q = 0; q < m; q += 16) {
@@ -1634,6 +1718,7 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
     if (k < n) {
       const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
       vdst = at + 14 + sfx;
+      if (!(a.skip & 16)) {
       // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value
       __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
       copy_run(RK, kp + p, klim, RO, at + 4, sfx);
@@ -1645,8 +1730,9 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
       // builder.rs:71: offsets.push(data.len() as u16), BE
       __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO,
                                             ob + uint32_t(data_len) + 2 * k, 0, 0);
+      }
     }
-    copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl);
+    if (!(a.skip & 32)) copy_long_runs<LSMBLK_COPY_PIPE>(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc);
   }
   if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
   if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
@@ -1968,6 +2054,7 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   const uint64_t lim = nblk < a.blk_cap ? nblk : (a.blk_cap ? a.blk_cap - 1 : 0);
   const uint64_t nw = uint64_t(gridDim.x) * 4;
   const uint32_t l = lane_id();
+  __shared__ alignas(16) uint32_t scratch[4][kCopyScratch];
   uint32_t err = 0;
   for (uint64_t base = blockIdx.x * 4 + wave_id(); base < lim; base += nw * 64) {
     const uint64_t mine = base + nw * l;
@@ -1978,7 +2065,7 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
       const uint64_t bi = base + nw * i;
       const uint32_t s = uni(a.blk_first[bi]), e = uni(a.blk_first[bi + 1]);
       const uint64_t O = uni64(a.blk_off[bi]), size = uni64(a.blk_off[bi + 1]) - O;
-      emit_big(a, s, e - s, O, size, err);
+      emit_big(a, s, e - s, O, size, err, scratch[wave_id()]);
     }
   }
   raise_err(a.stats, err);
@@ -2845,8 +2932,14 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
       }
     }
     c->dbg_on = value != 0;
+  } else if (key == LSMBLK_DEBUG_DECODE_LAG_BYTES) {
+    c->dec_lag_bytes = value;
+  } else if (key == LSMBLK_DEBUG_DECODE_LAG && value == 0) {  // the default
+    c->dec_lag = kDecLagDefault;
+    c->dec_lag_bytes = kDecLagBytesDefault;
   } else if (key == LSMBLK_DEBUG_DECODE_LAG && value >= 2 * kTile && value <= (1u << 24)) {
     c->dec_lag = value;
+    c->dec_lag_bytes = 0;  // exactly this lag (experiments)
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->ev[0]) {
       DeviceGuard dg(c->device);
@@ -2953,7 +3046,7 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   a.blk_ent = blk_ent;
   a.skip = c->skip;
   a.bagg = a.bbase = a.tagg = a.tinc = a.dbg = nullptr;
-  a.lag = 0;
+  a.lag = a.lag_bytes = 0;
   a.tag = a.poll = 0;
   if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && !c->dec_two_pass) {
     // lagged decode: E is read from HBM once, one launch (decode_lag_kernel)
@@ -2963,6 +3056,7 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     a.tagg = a.bbase + 3 * c->lag_blk_cap;
     a.tinc = a.tagg + 3 * ((c->lag_blk_cap + kTile - 1) / kTile + 1);
     a.lag = c->dec_lag;
+    a.lag_bytes = c->dec_lag_bytes;
     a.dbg = c->dbg_on ? c->dbg : nullptr;
     if (a.dbg && hipMemsetAsync(a.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     a.tag = c->epoch;

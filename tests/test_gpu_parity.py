@@ -618,12 +618,14 @@ def test_verifying_decode_counts_in_the_crc_pass(gen, n, bs):
 
 
 @pytest.mark.parametrize("cfg,n", [("U", 30000), ("Z", 30000), ("M", 4000)])
-@pytest.mark.parametrize("mode", ["two_pass", "lag128", "lag_beyond_batch"])
+@pytest.mark.parametrize("mode", ["two_pass", "lag128", "lag_beyond_batch", "lag_bytes"])
 def test_decode_modes(cfg, n, mode):
     """The A/B decode paths give the oracle's stream and block entry index: count + scan + decode
     (LSMBLK_DEBUG_TWO_PASS_DECODE), and the lagged decode at its smallest lag (128: each tile's
     finisher, lag / 2 + 63 workgroups after the tile's first count, just ahead of the tile's first
-    decoder) and at a lag beyond the batch (every count before any decode)."""
+    decoder), at a lag beyond the batch (every count before any decode), and at a lag scaled from
+    bytes below the largest lag (the decode's range loaded a second time: U/Z ~300 blocks, M's
+    large blocks clamped to 128)."""
     from lsm_amd._lib import lib
     kv = O.KV(*synth.GENERATORS[cfg](n, seed=21))
     seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 128 << 10)
@@ -633,6 +635,8 @@ def test_decode_modes(cfg, n, mode):
     ctx = batch._ctx(0)
     if mode == "two_pass":
         assert lib().lsmblk_debug_set(ctx, 3, 1) == 0
+    elif mode == "lag_bytes":
+        assert lib().lsmblk_debug_set(ctx, 6, 300 * 4096) == 0
     else:
         assert lib().lsmblk_debug_set(ctx, 4, 128 if mode == "lag128" else 1 << 20) == 0
     try:
@@ -645,7 +649,7 @@ def test_decode_modes(cfg, n, mode):
         np.testing.assert_array_equal(ent.cpu().numpy().view(np.uint64), np.concatenate([[0], np.cumsum(counts)]))
     finally:
         lib().lsmblk_debug_set(ctx, 3, 0)
-        lib().lsmblk_debug_set(ctx, 4, 10240)
+        lib().lsmblk_debug_set(ctx, 4, 0)
 
 
 def test_decode_lag_setting_bounds():
@@ -655,3 +659,4 @@ def test_decode_lag_setting_bounds():
     assert lib().lsmblk_debug_set(ctx, 4, 127) != 0
     assert lib().lsmblk_debug_set(ctx, 4, (1 << 24) + 1) != 0
     assert lib().lsmblk_debug_set(ctx, 4, 10240) == 0
+    assert lib().lsmblk_debug_set(ctx, 4, 0) == 0  # the default (scaled by the block size)
