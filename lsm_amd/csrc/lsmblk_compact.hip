@@ -981,7 +981,9 @@ __global__ void merge_empty_kernel(uint64_t* mstats, uint32_t* okey_off, uint32_
 //                      chain reaches the target or the end)
 //   rot_f_kernel       F(g) by binary lifting over the levels, then the next key change
 //   rot_chain_kernel   the SST chain 0, F(0), F(F(0)), ... by doubling F (level k appends
-//                      chain elements [2^k, 2^(k+1)) and squares F)
+//                      chain elements [2^k, 2^(k+1)) and squares F), for K levels; then
+//   rot_walk_kernel    one lane: every 2^K-th chain element through F^(2^K), and
+//   rot_fill_kernel    one thread per such anchor: the 2^K - 1 elements after it through F
 //   rot_finish_kernel  sst_start[] and the SST count.
 // The kept stream's versions of a key must be newest first (as MergeIterator yields SST data);
 // then "same as last key" is "same key as the previous kept entry" (DESIGN.md).
@@ -1003,8 +1005,9 @@ struct RotArgs {
   u32x2* JS;                // levels x (n_max + 1): {J_k[s], S_k[s]} side by side, so a doubling
                             // step gathers both with one 8-B load (two 4-B gathers cost two sectors)
   uint32_t levels;          // levels allocated for J / S
-  uint32_t* F0;             // n_max + 1: F, then the doubling ping-pong
-  uint32_t* F1;
+  uint32_t* F0;             // n_max + 1: F (kept for the chain's fill)
+  uint32_t* F1;             // n_max + 1 each: the doubling ping-pong F^(2^k)
+  uint32_t* F2;
   uint32_t* need;           // kRotMaxLevels: level k still has a chain short of target and end
   uint32_t* chain_end;      // [0] set once the SST chain reached the end
   uint32_t* starts;         // sst_cap: SST start entries (the chain), then n
@@ -1407,6 +1410,38 @@ __global__ void rot_chain_check_kernel(RotArgs a, uint32_t k) {
   if (last >= a.sst_cap || a.starts[last] >= n) *a.chain_end = k + 1;
 }
 
+// The chain past its first 2^K elements (K doubling levels done, FK = F^(2^K)): chain element
+// i 2^K for every i, by one lane -- a serial walk of (SSTs / 2^K) dependent loads instead of
+// log2(sst_cap) - K more squarings of F over all n entries (74 us each at config C's 29.5 M).
+// Past the chain's end the anchors are n.
+__global__ void rot_walk_kernel(RotArgs a, uint32_t K, const uint32_t* FK) {
+  if (threadIdx.x || *(volatile uint32_t*)a.chain_end) return;
+  const uint64_t n = rot_n(a);
+  uint32_t x = a.starts[0];
+  for (uint64_t i = 1ull << K; i < a.sst_cap; i += 1ull << K) {
+    x = x < n ? FK[x] : uint32_t(n);
+    a.starts[i] = x;
+  }
+}
+
+// Thread i: chain elements i 2^K + 1 .. (i + 1) 2^K - 1 from anchor i through F.
+__global__ __launch_bounds__(64) void rot_fill_kernel(RotArgs a, uint32_t K) {
+  if (*(volatile uint32_t*)a.chain_end) return;
+  const uint64_t n = rot_n(a);
+  const uint64_t base = (uint64_t(blockIdx.x) * 64 + threadIdx.x) << K;
+  if (base >= a.sst_cap) return;
+  uint32_t x = a.starts[base];
+  for (uint64_t t = base + 1; t < base + (1ull << K) && t < a.sst_cap; ++t) {
+    x = x < n ? a.F0[x] : uint32_t(n);
+    a.starts[t] = x;
+  }
+}
+
+// After the fill every slot of starts[] is a chain element (or n past the end).
+__global__ void rot_filled_kernel(RotArgs a, uint32_t levels) {
+  if (threadIdx.x == 0 && !*(volatile uint32_t*)a.chain_end) *a.chain_end = levels;
+}
+
 __global__ __launch_bounds__(256) void rot_finish_kernel(RotArgs a) {
   const uint64_t n = rot_n(a);
   __shared__ uint32_t s_ns;
@@ -1603,6 +1638,7 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, u
   } else {
     P.r.F0 = cv.take<uint32_t>(N1);
     P.r.F1 = cv.take<uint32_t>(N1);
+    P.r.F2 = cv.take<uint32_t>(N1);
   }
   P.r.need = cv.take<uint32_t>(kRotMaxLevels + 2);
   P.r.chain_end = P.r.need + kRotMaxLevels;
@@ -1631,14 +1667,25 @@ int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
   int rc = rotation_chains(r, st);
   if (rc) return rc;
   const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
+  // K doubling levels (chain elements [0, 2^K), F^(2^K)), then the walk + fill: K = 4 up to
+  // sst_cap 4096 (walk <= 256 loads), growing with the capacity so the walk stays that short.
+  // Config C (1 803 SSTs, sst_cap 4 096): 12 levels, 0.94 ms -> 4 levels + walk + fill.
+  uint32_t lc = 0;  // ceil(log2(sst_cap))
+  while (lc < 32 && (1ull << lc) < r.sst_cap) ++lc;
+  const uint32_t K = lc > 12 ? lc - 8 : 4;
   uint32_t* cur = r.F0;
   uint32_t* nxt = r.F1;
   for (uint32_t k = 0; k < 32 && (1ull << k) < r.sst_cap; ++k) {
+    if (k == K) {
+      hipLaunchKernelGGL(rot_walk_kernel, dim3(1), dim3(64), 0, st, r, K, cur);
+      hipLaunchKernelGGL(rot_fill_kernel, dim3(uint32_t(((r.sst_cap >> K) + 1 + 63) / 64)), dim3(64), 0, st, r, K);
+      hipLaunchKernelGGL(rot_filled_kernel, dim3(1), dim3(64), 0, st, r, lc);
+      break;
+    }
     hipLaunchKernelGGL(rot_chain_kernel, dim3(g), dim3(256), 0, st, r, k, cur, nxt);
     hipLaunchKernelGGL(rot_chain_check_kernel, dim3(1), dim3(64), 0, st, r, k);
-    uint32_t* t = cur;
-    cur = nxt;
-    nxt = t;
+    cur = nxt;                      // F^(2^(k+1))
+    nxt = cur == r.F1 ? r.F2 : r.F1;  // F (F0) is kept for the fill
   }
   hipLaunchKernelGGL(rot_finish_kernel, dim3(1), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;

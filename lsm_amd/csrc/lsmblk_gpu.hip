@@ -446,12 +446,6 @@ __device__ __forceinline__ void copy_run_wave(const rsrc_t& RS, uint32_t so, con
 // {source, destination, length - 16, first piece} is one 16-B LDS read.  (Round 2 searched the
 // lanes' first-piece numbers with 6 dependent ds_bpermutes and read the owner's fields with 4
 // more; the copies are most of M's large-block encode.)
-#ifndef LSMBLK_COPY_PIPE
-#define LSMBLK_COPY_PIPE true
-#endif
-#ifndef LSMBLK_DEC_COPY_PIPE
-#define LSMBLK_DEC_COPY_PIPE false
-#endif
 constexpr uint32_t kCopyScratch = 4 * 64 + 64;
 static_assert(4 * kCopyScratch <= kDecOut, "the decode's large-block path lends its output image");
 
@@ -507,11 +501,6 @@ __device__ __forceinline__ void copy_store(const rsrc_t& RD, const CopyBatch<B>&
     }
 }
 
-// pipe: the next batch's loads are issued before this batch's stores (kBigB / 2 pieces per lane
-// each), so the wait for a batch's loads never waits for the previous batch's stores (vmcnt
-// counts stores and retires in order).  The register cost is the same; the decode (whose VGPR
-// count sets its occupancy) keeps the plain loop.
-template <bool pipe = false>
 __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, uint32_t so, const rsrc_t& RD,
                                                uint32_t dof, uint32_t len, uint32_t* sc) {
   const uint32_t l = lane_id();
@@ -523,24 +512,10 @@ __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, u
   wave_sync();                       // the scratch's previous readers are done
   reinterpret_cast<u32x4*>(sc)[l] = u32x4{so, dof, len - 16, first};  // read only for lanes with a run
   uint32_t carry = 0;  // owner + 1 of the previous row's last piece
-  if (!pipe) {
-    for (uint32_t g0 = 0; g0 < total; g0 += 64 * kBigB) {
-      CopyBatch<kBigB> c;
-      copy_issue(RS, g0, total, np, first, sc, carry, c);
-      copy_store(RD, c);
-    }
-    return;
-  }
-  constexpr uint32_t H = kBigB / 2, R = 64 * H;
-  CopyBatch<H> c0, c1;
-  copy_issue(RS, 0, total, np, first, sc, carry, c0);
-  for (uint32_t g0 = R;; g0 += 2 * R) {
-    if (g0 < total) copy_issue(RS, g0, total, np, first, sc, carry, c1);
-    copy_store(RD, c0);
-    if (g0 >= total) break;
-    if (g0 + R < total) copy_issue(RS, g0 + R, total, np, first, sc, carry, c0);
-    copy_store(RD, c1);
-    if (g0 + R >= total) break;
+  for (uint32_t g0 = 0; g0 < total; g0 += 64 * kBigB) {
+    CopyBatch<kBigB> c;
+    copy_issue(RS, g0, total, np, first, sc, carry, c);
+    copy_store(RD, c);
   }
 }
 
@@ -606,7 +581,7 @@ __device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const r
       vl = L.vout[k + 1] - L.vout[k];
       if (vl < kCoop) copy_run(R, vsrc, lim, RV, vdst, vl);
     }
-    copy_long_runs<LSMBLK_DEC_COPY_PIPE>(live && vl >= kCoop, R, vsrc, RV, vdst, vl, sc);
+    copy_long_runs(live && vl >= kCoop, R, vsrc, RV, vdst, vl, sc);
   }
 }
 
@@ -1732,7 +1707,7 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
                                             ob + uint32_t(data_len) + 2 * k, 0, 0);
       }
     }
-    if (!(a.skip & 32)) copy_long_runs<LSMBLK_COPY_PIPE>(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc);
+    if (!(a.skip & 32)) copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc);
   }
   if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
   if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
