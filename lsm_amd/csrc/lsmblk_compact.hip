@@ -1398,7 +1398,7 @@ __global__ __launch_bounds__(256) void rot_chain_kernel(RotArgs a, uint32_t k, c
     const uint32_t c = a.starts[s];
     a.starts[h + s] = c < n ? cur[c] : uint32_t(n);
   }
-  if (s <= n) nxt[s] = cur[cur[s]];
+  if (nxt && s <= n) nxt[s] = cur[cur[s]];
 }
 
 // After each level: has the last chain element computed so far reached the end?
@@ -1410,16 +1410,18 @@ __global__ void rot_chain_check_kernel(RotArgs a, uint32_t k) {
   if (last >= a.sst_cap || a.starts[last] >= n) *a.chain_end = k + 1;
 }
 
-// The chain past its first 2^K elements (K doubling levels done, FK = F^(2^K)): chain element
-// i 2^K for every i, by one lane -- a serial walk of (SSTs / 2^K) dependent loads instead of
-// log2(sst_cap) - K more squarings of F over all n entries (74 us each at config C's 29.5 M).
-// Past the chain's end the anchors are n.
-__global__ void rot_walk_kernel(RotArgs a, uint32_t K, const uint32_t* FK) {
+// The chain past its first 2^K elements (K doubling levels done, the last without its squaring;
+// FH = F^(2^(K-1))): chain element i 2^K for every i, by one lane -- a serial walk of
+// 2 SSTs / 2^K dependent loads instead of log2(sst_cap) - K + 1 more squarings of F over all n
+// entries (~90 us each at config C's 29.5 M; a load of the walk ~0.3 us).  Past the chain's
+// end the anchors are n.
+__global__ void rot_walk_kernel(RotArgs a, uint32_t K, const uint32_t* FH) {
   if (threadIdx.x || *(volatile uint32_t*)a.chain_end) return;
   const uint64_t n = rot_n(a);
   uint32_t x = a.starts[0];
   for (uint64_t i = 1ull << K; i < a.sst_cap; i += 1ull << K) {
-    x = x < n ? FK[x] : uint32_t(n);
+    x = x < n ? FH[x] : uint32_t(n);
+    x = x < n ? FH[x] : uint32_t(n);
     a.starts[i] = x;
   }
 }
@@ -1667,12 +1669,13 @@ int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
   int rc = rotation_chains(r, st);
   if (rc) return rc;
   const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
-  // K doubling levels (chain elements [0, 2^K), F^(2^K)), then the walk + fill: K = 4 up to
-  // sst_cap 4096 (walk <= 256 loads), growing with the capacity so the walk stays that short.
-  // Config C (1 803 SSTs, sst_cap 4 096): 12 levels, 0.94 ms -> 4 levels + walk + fill.
+  // K doubling levels (chain elements [0, 2^K); the last level does not square F), then the
+  // walk + fill: K = 3 up to sst_cap 4096 (walk <= 1024 loads), growing with the capacity so the
+  // walk stays that short.  Config C (1 803 SSTs, sst_cap 4 096): 12 levels, 0.89 ms ->
+  // 4 levels + walk + fill 0.40 ms -> 3 levels (2 squarings) + walk + fill.
   uint32_t lc = 0;  // ceil(log2(sst_cap))
   while (lc < 32 && (1ull << lc) < r.sst_cap) ++lc;
-  const uint32_t K = lc > 12 ? lc - 8 : 4;
+  const uint32_t K = lc > 12 ? lc - 9 : 3;
   uint32_t* cur = r.F0;
   uint32_t* nxt = r.F1;
   for (uint32_t k = 0; k < 32 && (1ull << k) < r.sst_cap; ++k) {
@@ -1682,8 +1685,11 @@ int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
       hipLaunchKernelGGL(rot_filled_kernel, dim3(1), dim3(64), 0, st, r, lc);
       break;
     }
-    hipLaunchKernelGGL(rot_chain_kernel, dim3(g), dim3(256), 0, st, r, k, cur, nxt);
+    const bool last = k + 1 == K && (2ull << k) < r.sst_cap;  // the walk follows: no squaring
+    hipLaunchKernelGGL(rot_chain_kernel, dim3(last ? uint32_t(((1ull << k) + 255) / 256) : g), dim3(256), 0, st, r,
+                       k, cur, last ? nullptr : nxt);
     hipLaunchKernelGGL(rot_chain_check_kernel, dim3(1), dim3(64), 0, st, r, k);
+    if (last) continue;             // cur stays F^(2^k) = F^(2^(K-1)) for the walk
     cur = nxt;                      // F^(2^(k+1))
     nxt = cur == r.F1 ? r.F2 : r.F1;  // F (F0) is kept for the fill
   }
