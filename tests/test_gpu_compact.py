@@ -230,7 +230,7 @@ def test_sst_rotation_vs_restated_loop(bs, target):
     """lsmblk_sst_rotation_batch == orc_segment_like_compaction (the rotation of compact.rs:278-289
     over the entries handed to SsTableBuilder::add), multi-version keys.  The capacity is n + 2
     (2^15 slots): the SST chain's walk + fill run with K = 6 doubling levels, and target 1 (an SST
-    at every key change, ~6 700 of them) walks ~200 anchors; the bench's C sizes use K = 3."""
+    at every key change, ~6 700 of them) walks ~105 anchors, 2 loads each; the bench's C sizes use K = 3."""
     keys, ko, vals, vo, ts, rs = synth.gen_runs(20000, nrun=4, seed=7, versions=3, tombstone=0.05)
     kv = O.KV(keys, ko, vals, vo, ts)
     src = O.merge_runs(kv, rs)
