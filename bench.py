@@ -70,6 +70,8 @@ def parse(argv=None):
     p.add_argument("--no-pcie", action="store_true", help="skip the H2D+D2H-inclusive rate (DESIGN.md)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher self-test: ranks join a gloo group and report the world, no GPU work")
+    p.add_argument("--dry-run-fail-extra", type=int, default=None,
+                   help="diagnostics: in --dry-run, this rank raises inside compact_dist (the N>1 extra's path)")
     p.add_argument("--dry-run-fail-rank", type=int, default=None,
                    help="launcher self-test: this rank exits with status 3 before joining the group")
     p.add_argument("--decode-two-pass", action="store_true",
@@ -292,12 +294,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
             "plan": 8 * (n + 1) + K + 8 * nblk, "emit": D + E + 16 * (nblk + 1)}
     dom = max(kms, key=lambda k: kms[k])
     achieved = algo[dom] / (kms[dom] * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        tj = json.load(open(tpath))
-        if tj.get("workload") == cfg and tj.get("blocks") == nblk:
-            traffic = tj.get("bytes_per_launch", {}).get(dom)
+    traffic, why = measured_traffic(cfg, dom, default_size=args.blocks is None)
     desc = {"U": "16-B uniform keys, 100-B values", "Z": "Zipf 12-B prefixes, 100-B values",
             "M": "16-B keys, 8 B-4 KiB values"}[cfg]
     result = {
@@ -313,6 +310,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
                    "oracle_checked_blocks": int(checked_all)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     **({"traffic_reason": why} if why else {}),
                      "bytes_per_launch": algo[dom], "launch_ms": round(kms[dom], 4),
                      "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
                      "stage_ms": {"decode": round(dec_ms, 4), "encode": round(enc_ms, 4)},
@@ -524,6 +522,9 @@ def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
     ms = t_max / steps * 1e3
     Dk = s[6] + s[7] + 16 * s[5]
     D = K + V + 16 * n
+    step_bytes = {"decode": E + D, "merge_gather": 2 * D + 4 * n, "encode": Dk + s[1]}
+    roofline = compaction_roofline(ctx, step, dev, E, D, Dk, n, nblk, s, sum(step_bytes.values()), ms,
+                                   default_size=args.blocks is None)
     return {
         "metric": METRIC, "value": round(world * E * steps / t_max / GiB, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
@@ -538,8 +539,36 @@ def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
                    "rccl_world": world, "compaction_bit_exact": bool(ok_all),
                    "oracle_checked_blocks": int(checked_all)},
         "stage_ms": {"decode": round(dec_ms, 4), "compact": round(cmp_ms, 4)},
-        "step_algorithmic_bytes": {"decode": E + D, "merge_gather": 2 * D + 4 * n, "encode": Dk + s[1]},
+        "step_algorithmic_bytes": step_bytes,
+        "roofline": roofline,
     }
+
+
+def compaction_roofline(ctx, step, dev, E, D, Dk, n, nblk, s, step_bytes, ms, default_size=True):
+    """Config C's roofline: every kernel of a step timed from its dispatch events (kernel log), the
+    dominant one priced by its algorithmic bytes and its measured traffic."""
+    prof = kernel_log_profile(ctx, step, dev)
+    per = {k: v[1] for k, v in prof.items()}
+    dom = max(per, key=per.get)
+    kept, merged = s[5], s[4]
+    # algorithmic bytes per step of the kernels that can dominate (DESIGN.md section 5)
+    algo = {"decode_lag_kernel": E + D + 20 * nblk,          # blocks in, decoded stream out
+            "merge_tile_kernel": 24 * n,                      # key_off + 16-B key prefix in, merged rank out
+            "mwrite_kernel": 2 * Dk + 4 * merged,             # kept entries gathered in merged order
+            "mflag_kernel": s[6] + 12 * merged,               # keys + ts + order in, keep flags out
+            "emit_kernel": Dk + s[1], "plan_walk_kernel": 8 * (kept + 1) + s[6] + 8 * s[0]}
+    b = algo.get(dom)
+    achieved = b / (per[dom] * 1e-3) / 1e9 if b else None
+    traffic, why = measured_traffic("C", dom, launches=prof[dom][0], default_size=default_size)
+    top = sorted(per.items(), key=lambda kv: -kv[1])[:10]
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+            **({"traffic_reason": why} if why else {}),
+            "bytes_per_launch": b, "launch_ms": round(per[dom], 4),
+            "kernels_ms": {k: round(v, 4) for k, v in top},
+            "launches_per_step": {k: round(prof[k][0], 2) for k, _ in top},
+            "step_algorithmic_bytes": step_bytes,
+            "step_frac": round(step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def storage_slice(k, WR, nblk_range, nrun, seg_bytes, dev):
@@ -718,6 +747,36 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
     }
 
 
+def extra_or_exit(rank, fn):
+    """An N>1 extra config: a rank whose part raises exits at once with status 1 (no cleanup that
+    could block on its peers), so the launcher -- bench.py's own or torch.distributed.run --
+    tears the job down instead of the peers hanging in a collective with it."""
+    try:
+        return fn()
+    except Exception as e:
+        log(f"[rank {rank}] extra config C failed: {e!r}")
+        sys.stderr.flush()
+        os._exit(1)
+
+
+class _DryShard:
+    """--dry-run-fail-extra: a CPU stand-in for shard.RangeShard whose merge raises on one rank,
+    while the other ranks go on into compact_dist's head all-gather (and block there)."""
+
+    def __init__(self, fail):
+        self.fail, self.dev, self.W = fail, torch.device("cpu"), 2
+
+    def merge(self):
+        if self.fail:
+            raise RuntimeError("dry run: merge failed as asked")
+        return 0
+
+    def head(self):
+        from lsm_amd import shard
+        z = torch.zeros(1, dtype=torch.int64)
+        return shard.Head(0, z, z.clone(), z[:0], torch.zeros(0, dtype=torch.uint8), torch.zeros(0, dtype=torch.uint8))
+
+
 def dry_run(args, rank, world, local):
     """The launcher's contract without a GPU: every rank joins one gloo group; rank 0 reports the
     world size the collective saw and the ranks it heard from."""
@@ -732,6 +791,9 @@ def dry_run(args, rank, world, local):
         dist.all_reduce(t)
         seen = dist.get_world_size()
         mask = int(t.item())
+        if args.dry_run_fail_extra is not None:  # the N>1 extra's failure path, through compact_dist
+            from lsm_amd import shard
+            extra_or_exit(rank, lambda: shard.compact_dist(_DryShard(rank == args.dry_run_fail_extra)))
         dist.destroy_process_group()
     else:
         mask = 1
@@ -744,6 +806,9 @@ def dry_run(args, rank, world, local):
 # ---------------------------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.ablate is not None:  # ablation masks exist only in the diagnostics build (lsm_amd/_build.py)
+        from lsm_amd import _build
+        os.environ.setdefault("LSMBLK_SO_OVERRIDE", _build.DIAG_SO)
     if "RANK" not in os.environ and args.gpus > 1:
         return launch(args)
     rank, world, local = dist_env()
@@ -784,13 +849,12 @@ def main():
         extras["C"] = run_compaction(args, 3, 1, rank, world, local, dev, extra=True)
         result["extra_configs"] = extras
     elif world > 1 and args.config == "U" and not args.no_extras and args.blocks is None:
-        # the compaction-shaped config split by key range over the same N GPUs (one extra line)
+        # the compaction-shaped config split by key range over the same N GPUs (one extra line).
+        # A rank that fails here exits at once, non-zero: its peers, blocked in a collective with
+        # it, are then torn down by the launcher (bench.py's own or torch.distributed.run)
+        # instead of hanging until the driver's time limit.
         torch.cuda.empty_cache()
-        try:
-            c = run_compaction(args, 3, 1, rank, world, local, dev, extra=True)
-        except Exception as e:  # an extra never takes the headline line down
-            log(f"[rank {rank}] extra config C failed: {e!r}")
-            c = {"error": repr(e)}
+        c = extra_or_exit(rank, lambda: run_compaction(args, 3, 1, rank, world, local, dev, extra=True))
         if result is not None:
             result["extra_configs"] = {"C": c}
     ok = True
@@ -976,7 +1040,50 @@ def kernel_times(ctx, step, dev, reps=3, lead=3):
         for i, k in enumerate(KERNELS):
             acc[k].append(buf[i])
     check(lib().lsmblk_debug_set(ctx, 2, 0))
-    return {k: float(np.mean(v)) for k, v in acc.items()}
+    # a kernel the step did not launch reads -1 (the lagged decode has no count / scan launches)
+    return {k: float(np.mean(v)) for k, v in acc.items() if min(v) >= 0}
+
+
+def kernel_log_profile(ctx, step, dev, reps=3, lead=2):
+    """{kernel: (launches, ms)} per step over `reps` back-to-back steps, every launch carrying its
+    dispatch start / stop events (lsmblk_ctx_kernel_log), after `lead` untimed steps."""
+    from lsm_amd._lib import kernel_log
+    for _ in range(lead):
+        step()
+    torch.cuda.synchronize(dev)
+    check(lib().lsmblk_debug_set(ctx, 2, 1))
+    kernel_log(ctx)  # empties the log
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize(dev)
+    log = kernel_log(ctx)
+    check(lib().lsmblk_debug_set(ctx, 2, 0))
+    return {k: (n / reps, ms / reps) for k, (n, ms) in log.items()}
+
+
+def measured_traffic(cfg, kernel, launches=1.0, default_size=True):
+    """(HBM bytes per step of `kernel`, None) from profiles/traffic.json when it was measured at the
+    kernel sources this run executes (tools/traffic.sh stamps it with lsm_amd/_build.py src_sha), else
+    (None, the reason)."""
+    from lsm_amd import _build
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if not default_size:
+        return None, "batch size differs from the traffic passes (default sizes only)"
+    if not os.path.exists(tpath):
+        return None, "no profiles/traffic.json"
+    tj = json.load(open(tpath))
+    sha = _build.src_sha()
+    if tj.get("src_sha256") != sha:
+        return None, (f"profiles/traffic.json was measured at kernel sources {str(tj.get('src_sha256'))[:12]} "
+                      f"(commit {tj.get('commit')}), this run's are {sha[:12]}")
+    c = tj.get("configs", {}).get(cfg)
+    if c is None:
+        return None, f"no config {cfg} pass in profiles/traffic.json"
+    if kernel in c.get("bytes_per_launch", {}):
+        return int(c["bytes_per_launch"][kernel]), None
+    if kernel in c.get("kernels", {}):
+        return int(c["kernels"][kernel]["bytes_per_dispatch"] * launches), None
+    return None, f"kernel {kernel} not in the config {cfg} passes"
 
 
 def ablate(args, ctx, blocks, blk_off, nblk, out_kv, st_dec, n, K, V, stream):

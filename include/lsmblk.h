@@ -175,6 +175,16 @@ int lsmblk_debug_counters(lsmblk_ctx* ctx, uint64_t* out, uint32_t n);
  * the recorded events. */
 #define LSMBLK_KERNELS 5
 int lsmblk_ctx_kernel_times(lsmblk_ctx* ctx, float* ms);
+/* Every kernel launched on this context since the previous call (or since LSMBLK_DEBUG_KERNEL_TIMING
+ * was switched on), summed by kernel name: out[0 .. *n).  The log holds the last 16384 launches;
+ * LSMBLK_E_CAPACITY if more were made (or more than cap distinct kernels).  Waits for the events.
+ * Diagnostics (bench.py's per-kernel roofline of every config); the log is cleared by the call. */
+typedef struct {
+  char name[56];
+  uint32_t launches;
+  float ms;
+} lsmblk_kernel_stat;
+int lsmblk_ctx_kernel_log(lsmblk_ctx* ctx, lsmblk_kernel_stat* out, uint32_t cap, uint32_t* n);
 
 /* Decode nblk blocks (block b = blocks[blk_off[b] .. blk_off[b+1]), blk_off u64[nblk+1])
  * into the SoA stream `out` (outputs must be 16-byte aligned).  Asynchronous: completion

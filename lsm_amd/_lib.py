@@ -46,6 +46,10 @@ class CompactOptsC(ctypes.Structure):
                 ("prefix_off", P), ("block_size", U32), ("merge_mode", U32), ("target_sst_size", U64)]
 
 
+class KernelStatC(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 56), ("launches", U32), ("ms", ctypes.c_float)]
+
+
 class KeyRangeC(ctypes.Structure):
     _fields_ = [("lo", P), ("hi", P), ("lo_len", U32), ("hi_len", U32), ("has_lo", U32), ("has_hi", U32)]
 
@@ -82,6 +86,7 @@ SIGNATURES = [
     ("lsmblk_ctx_reserve", I, [P, U64, U64, U64]),
     ("lsmblk_debug_set", I, [P, I, U32]),
     ("lsmblk_ctx_kernel_times", I, [P, ctypes.POINTER(ctypes.c_float)]),
+    ("lsmblk_ctx_kernel_log", I, [P, ctypes.POINTER(KernelStatC), U32, ctypes.POINTER(U32)]),
     ("lsmblk_debug_counters", I, [P, ctypes.POINTER(ctypes.c_uint64), U32]),
     ("lsmblk_decode_batch", I, [P, P, P, U64, ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_decode_batch_ex", I, [P, P, P, U64, U32, U32, ctypes.POINTER(KVStreamC), P, P, P]),
@@ -133,6 +138,14 @@ def lib():
             raise RuntimeError("liblsmblk.so ABI version mismatch")
         _lib = L
     return _lib
+
+
+def kernel_log(ctx):
+    """{kernel name: (launches, ms)} of every launch on ctx since the previous read (kernel timing on)."""
+    buf = (KernelStatC * 256)()
+    n = U32(0)
+    check(lib().lsmblk_ctx_kernel_log(ctx, buf, 256, ctypes.byref(n)), "lsmblk_ctx_kernel_log")
+    return {buf[i].name.decode(): (int(buf[i].launches), float(buf[i].ms)) for i in range(n.value)}
 
 
 def check(status, what=""):

@@ -60,15 +60,30 @@ def release_contexts(device: int = None):
         keys = [k for k in _ctxs if device is None or k[0] == device]
         for k in keys:
             c = _ctxs.pop(k)
-            with c.lock:
+            with c.lock:  # waits for a call in progress on it (batch wrappers hold the lock)
                 torch.cuda.synchronize(k[0])
                 lib().lsmblk_ctx_destroy(c.h)
+                c.h = None  # a thread that fetched c before the pop takes a fresh context
     return len(keys)
 
 
 def _ctx(device: int, stream=None):
-    """Context handle for `device` and `stream` (default: the device's current stream)."""
+    """Context handle for `device` and `stream` (default: the device's current stream).  For
+    diagnostics calls; the batch wrappers go through _native, which holds the context's lock."""
     return _ctx_for(device, _stream_ptr(stream, device)).h
+
+
+def _native(fn, device: int, stream, *args, what=None, own=None):
+    """One library call on the (device, stream) context (or on `own`, an OwnCtx), with that
+    context's lock held for the whole call, so release_contexts cannot destroy it meanwhile; a
+    context released before the lock was taken is replaced by a fresh one."""
+    if own is not None:
+        return check(getattr(lib(), fn)(own.h, *args), what or fn)
+    while True:
+        c = _ctx_for(device, _stream_ptr(stream, device))
+        with c.lock:
+            if c.h is not None:
+                return check(getattr(lib(), fn)(c.h, *args), what or fn)
 
 
 class OwnCtx:
@@ -218,8 +233,8 @@ def decode_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_cap,
             or out.vals.numel() < val_cap:
         raise ValueError("decode_into: capacities exceed the output tensors")
     c = out._c(entry_cap, key_cap, val_cap)
-    check(lib().lsmblk_decode_batch(_ctx(dev, stream), _ptr(blocks), _ptr(blk_off), nblk, ctypes.byref(c),
-                                    stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_decode_batch")
+    _native("lsmblk_decode_batch", dev, stream, _ptr(blocks), _ptr(blk_off), nblk, ctypes.byref(c),
+            stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_decode_batch")
 
 
 def decode_ex_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_cap, val_cap, tail=0, verify=False,
@@ -237,9 +252,9 @@ def decode_ex_into(blocks, blk_off, nblk, out: KVStream, stats, entry_cap, key_c
             or out.vals.numel() < val_cap:
         raise ValueError("decode_ex_into: capacities exceed the output tensors")
     c = out._c(entry_cap, key_cap, val_cap)
-    check(lib().lsmblk_decode_batch_ex(_ctx(dev, stream), _ptr(blocks), _ptr(blk_off), nblk, tail,
-                                       LSMBLK_DECODE_VERIFY_CRC if verify else 0, ctypes.byref(c), _ptr(blk_ent),
-                                       stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_decode_batch_ex")
+    _native("lsmblk_decode_batch_ex", dev, stream, _ptr(blocks), _ptr(blk_off), nblk, tail,
+            LSMBLK_DECODE_VERIFY_CRC if verify else 0, ctypes.byref(c), _ptr(blk_ent),
+            stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_decode_batch_ex")
 
 
 def decode_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None, tail: int = 0, verify: bool = False,
@@ -292,9 +307,9 @@ def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: in
     _need(blk_off, torch.int64, "blk_off", dev, blk_cap)
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     c = kv._c()
-    check(lib().lsmblk_encode_batch(_ctx(dev, stream), ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
-                                    _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
-                                    _stream_ptr(stream, dev)), "lsmblk_encode_batch")
+    _native("lsmblk_encode_batch", dev, stream, ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
+            _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
+            _stream_ptr(stream, dev), what="lsmblk_encode_batch")
 
 
 def encode_kv(kv: KVStream, seg_start, block_size: int, stream=None):
@@ -325,8 +340,8 @@ def crc32_into(blocks: torch.Tensor, blk_off: torch.Tensor, nblk: int, crc: torc
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     if nblk:
         _need(blocks, torch.uint8, "blocks", dev)
-    check(lib().lsmblk_crc32_batch(_ctx(dev, stream), _ptr(blocks), blk_off.data_ptr(), nblk, tail, _ptr(crc),
-                                   stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_crc32_batch")
+    _native("lsmblk_crc32_batch", dev, stream, _ptr(blocks), blk_off.data_ptr(), nblk, tail, _ptr(crc),
+            stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_crc32_batch")
 
 
 def crc32_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None, tail: int = 0) -> torch.Tensor:
@@ -353,9 +368,8 @@ def segment_blocks_into(seg_start: torch.Tensor, nseg: int, enc_stats: torch.Ten
     _need(seg_start, torch.int32, "seg_start", dev, nseg + 1)
     _need(seg_blk, torch.int32, "seg_blk", dev, nseg + 1)
     _need(enc_stats, torch.int64, "enc_stats", dev, STATS_WORDS)
-    check(lib().lsmblk_encode_segment_blocks(_ctx(dev, stream), seg_start.data_ptr(), nseg, enc_stats.data_ptr(),
-                                             seg_blk.data_ptr(), _stream_ptr(stream, dev)),
-          "lsmblk_encode_segment_blocks")
+    _native("lsmblk_encode_segment_blocks", dev, stream, seg_start.data_ptr(), nseg, enc_stats.data_ptr(),
+            seg_blk.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_encode_segment_blocks")
 
 
 def block_meta_into(blocks, blk_off, nblk, seg_blk, nseg, meta, meta_cap, meta_off, stats, stream=None, tail=0):
@@ -366,9 +380,9 @@ def block_meta_into(blocks, blk_off, nblk, seg_blk, nseg, meta, meta_cap, meta_o
     _need(meta, torch.uint8, "meta", dev, meta_cap)
     _need(meta_off, torch.int64, "meta_off", dev, nseg + 1)
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
-    check(lib().lsmblk_block_meta_batch(_ctx(dev, stream), _ptr(blocks), blk_off.data_ptr(), nblk, tail,
-                                        seg_blk.data_ptr(), nseg, meta.data_ptr(), meta_cap, meta_off.data_ptr(),
-                                        stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_block_meta_batch")
+    _native("lsmblk_block_meta_batch", dev, stream, _ptr(blocks), blk_off.data_ptr(), nblk, tail,
+            seg_blk.data_ptr(), nseg, meta.data_ptr(), meta_cap, meta_off.data_ptr(),
+            stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_block_meta_batch")
 
 
 def block_meta(blocks: torch.Tensor, blk_off: torch.Tensor, seg_blk, stream=None, tail: int = 0):
@@ -445,10 +459,9 @@ def compact_filter(kv: KVStream, watermark: int, bottom_level: bool, prefixes=()
     out = KVStream.empty(n, kb, vb, dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
     ci, co = kv._c(), out._c(n, kb + 16, vb + 16)
-    check(lib().lsmblk_compact_filter_batch(_ctx(dev.index, stream), ctypes.byref(ci), watermark,
-                                            int(bool(bottom_level)), pfx.data_ptr(), pfo.data_ptr(), len(prefixes),
-                                            ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev.index)),
-          "lsmblk_compact_filter_batch")
+    _native("lsmblk_compact_filter_batch", dev.index, stream, ctypes.byref(ci), watermark,
+            int(bool(bottom_level)), pfx.data_ptr(), pfo.data_ptr(), len(prefixes),
+            ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev.index), what="lsmblk_compact_filter_batch")
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:
@@ -468,9 +481,8 @@ def merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, out: KVStream, 
     out.check(dev, "out", 0)
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     ci, co = kv._c(), out._c(*out.caps())
-    check(lib().lsmblk_merge_batch_ex(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun, merge_mode,
-                                      ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev)),
-          "lsmblk_merge_batch_ex")
+    _native("lsmblk_merge_batch_ex", dev, stream, ctypes.byref(ci), run_start.data_ptr(), nrun, merge_mode,
+            ctypes.byref(co), stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_merge_batch_ex")
 
 
 def merge_runs(kv: KVStream, run_start, stream=None, merge_mode=LSMBLK_MERGE_RUNS) -> KVStream:
@@ -501,9 +513,8 @@ def sst_rotation(kv: KVStream, block_size: int, target_sst_size: int, stream=Non
     starts = torch.zeros(cap, dtype=torch.int32, device=dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
     c = kv._c()
-    check(lib().lsmblk_sst_rotation_batch(_ctx(dev.index, stream), ctypes.byref(c), block_size, target_sst_size,
-                                          starts.data_ptr(), cap, stats.data_ptr(), _stream_ptr(stream, dev.index)),
-          "lsmblk_sst_rotation_batch")
+    _native("lsmblk_sst_rotation_batch", dev.index, stream, ctypes.byref(c), block_size, target_sst_size,
+            starts.data_ptr(), cap, stats.data_ptr(), _stream_ptr(stream, dev.index), what="lsmblk_sst_rotation_batch")
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:
@@ -540,10 +551,10 @@ def compact_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, b
     _need(run_start, torch.int32, "run_start", dev, nrun + 1)
     o = _opts_c(opts)
     ci, ck = kv._c(), buf.kept._c(*buf.kept.caps())
-    check(lib().lsmblk_compact_batch(_ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun, ctypes.byref(o),
-                                     ctypes.byref(ck), buf.out.data_ptr(), buf.out_cap, buf.blk_off.data_ptr(),
-                                     buf.blk_cap, buf.sst_start.data_ptr(), buf.sst_blk.data_ptr(), buf.sst_cap,
-                                     buf.stats.data_ptr(), _stream_ptr(stream, dev)), "lsmblk_compact_batch")
+    _native("lsmblk_compact_batch", dev, stream, ctypes.byref(ci), run_start.data_ptr(), nrun, ctypes.byref(o),
+            ctypes.byref(ck), buf.out.data_ptr(), buf.out_cap, buf.blk_off.data_ptr(),
+            buf.blk_cap, buf.sst_start.data_ptr(), buf.sst_blk.data_ptr(), buf.sst_cap,
+            buf.stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_compact_batch")
 
 
 def _opts_c(opts):
@@ -606,10 +617,9 @@ def compact_merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: d
     _need(stats, torch.int64, "stats", dev, 5)
     o = _opts_c(opts)
     ci, ck = kv._c(), kept._c(*kept.caps())
-    check(lib().lsmblk_compact_merge_batch(ctx.h if ctx is not None else _ctx(dev, stream), ctypes.byref(ci), run_start.data_ptr(), nrun,
-                                           ctypes.byref(o), ctypes.byref(key_range) if key_range is not None else None,
-                                           ctypes.byref(ck), stats.data_ptr(), _stream_ptr(stream, dev)),
-          "lsmblk_compact_merge_batch")
+    _native("lsmblk_compact_merge_batch", dev, stream, ctypes.byref(ci), run_start.data_ptr(), nrun,
+            ctypes.byref(o), ctypes.byref(key_range) if key_range is not None else None,
+            ctypes.byref(ck), stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_compact_merge_batch", own=ctx)
 
 
 def shard_prepare(ext: KVStream, n_own: int, last: bool, block_size: int, target_sst_size: int, sst_cap: int,
@@ -617,17 +627,17 @@ def shard_prepare(ext: KVStream, n_own: int, last: bool, block_size: int, target
     dev = _dev_index(ext.key_off)
     ext.check(dev, "ext")
     c = ext._c()
-    check(lib().lsmblk_shard_rotation_prepare(ctx.h if ctx is not None else _ctx(dev, stream), ctypes.byref(c), n_own,
-                                              LSMBLK_SHARD_LAST if last else 0, block_size, target_sst_size, sst_cap,
-                                              _stream_ptr(stream, dev)), "lsmblk_shard_rotation_prepare")
+    _native("lsmblk_shard_rotation_prepare", dev, stream, ctypes.byref(c), n_own,
+            LSMBLK_SHARD_LAST if last else 0, block_size, target_sst_size, sst_cap,
+            _stream_ptr(stream, dev), what="lsmblk_shard_rotation_prepare", own=ctx)
 
 
 def shard_carry(carry_in: torch.Tensor, carry_out: torch.Tensor, stream=None, ctx=None):
     dev = _dev_index(carry_in)
     _need(carry_in, torch.int64, "carry_in", dev, 2)
     _need(carry_out, torch.int64, "carry_out", dev, 2)
-    check(lib().lsmblk_shard_rotation_carry(ctx.h if ctx is not None else _ctx(dev, stream), carry_in.data_ptr(), carry_out.data_ptr(),
-                                            _stream_ptr(stream, dev)), "lsmblk_shard_rotation_carry")
+    _native("lsmblk_shard_rotation_carry", dev, stream, carry_in.data_ptr(), carry_out.data_ptr(),
+            _stream_ptr(stream, dev), what="lsmblk_shard_rotation_carry", own=ctx)
 
 
 def shard_encode_into(ext: KVStream, out, out_cap, blk_off, blk_cap, seg_start, seg_blk, seg_cap, stats,
@@ -640,10 +650,9 @@ def shard_encode_into(ext: KVStream, out, out_cap, blk_off, blk_cap, seg_start, 
     _need(seg_blk, torch.int32, "seg_blk", dev, seg_cap)
     _need(stats, torch.int64, "stats", dev, 8)
     c = ext._c()
-    check(lib().lsmblk_shard_encode_batch(ctx.h if ctx is not None else _ctx(dev, stream), ctypes.byref(c), out.data_ptr(), out_cap,
-                                          blk_off.data_ptr(), blk_cap, seg_start.data_ptr(), seg_blk.data_ptr(),
-                                          seg_cap, stats.data_ptr(), _stream_ptr(stream, dev)),
-          "lsmblk_shard_encode_batch")
+    _native("lsmblk_shard_encode_batch", dev, stream, ctypes.byref(c), out.data_ptr(), out_cap,
+            blk_off.data_ptr(), blk_cap, seg_start.data_ptr(), seg_blk.data_ptr(),
+            seg_cap, stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_shard_encode_batch", own=ctx)
 
 
 def seek_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, q_blk, qkeys, tail: int = 0, stream=None):
@@ -660,9 +669,9 @@ def seek_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, q_blk, qkeys, tail:
     qo, qb = _u32_table(ko, dev), _u32_table(np.asarray(q_blk, np.uint32), dev)
     idx = torch.zeros(max(len(qkeys), 1), dtype=torch.int32, device=dev)
     stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
-    check(lib().lsmblk_seek_batch(_ctx(dev.index, stream), _ptr(blocks), blk_off.data_ptr(), nblk, tail,
-                                  qk.data_ptr(), qo.data_ptr(), qb.data_ptr(), len(qkeys), idx.data_ptr(),
-                                  stats.data_ptr(), _stream_ptr(stream, dev.index)), "lsmblk_seek_batch")
+    _native("lsmblk_seek_batch", dev.index, stream, _ptr(blocks), blk_off.data_ptr(), nblk, tail,
+            qk.data_ptr(), qo.data_ptr(), qb.data_ptr(), len(qkeys), idx.data_ptr(),
+            stats.data_ptr(), _stream_ptr(stream, dev.index), what="lsmblk_seek_batch")
     torch.cuda.synchronize(dev)
     st = _status(stats)
     if st:

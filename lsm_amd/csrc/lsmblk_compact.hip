@@ -1543,18 +1543,18 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   m.two = two;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (n == 0) {
-    hipLaunchKernelGGL(merge_empty_kernel, dim3(1), dim3(64), 0, st, m.mstats, out->key_off, out->val_off,
+    LSM_LAUNCH(merge_empty_kernel, dim3(1), dim3(64), 0, st, m.mstats, out->key_off, out->val_off,
                        out->entry_cap, stats);
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
   if (hipMemsetAsync(m.mstats, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t nc = m.nc_max;
-  hipLaunchKernelGGL(cand_rank_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
+  LSM_LAUNCH(cand_rank_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   const uint64_t nb = (uint64_t(nc) + 1) * nrun;
-  hipLaunchKernelGGL(bounds_kernel, dim3(uint32_t((nb + 255) / 256)), dim3(256), 0, st, m);
-  hipLaunchKernelGGL(merge_tile_kernel, dim3(nc), dim3(kMTT), 0, st, m);
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, m);
-  hipLaunchKernelGGL(perm_kernel, dim3(nc), dim3(64), 0, st, m);
+  LSM_LAUNCH(bounds_kernel, dim3(uint32_t((nb + 255) / 256)), dim3(256), 0, st, m);
+  LSM_LAUNCH(merge_tile_kernel, dim3(nc), dim3(kMTT), 0, st, m);
+  LSM_LAUNCH(tile_scan_kernel, dim3(1), dim3(1024), 0, st, m);
+  LSM_LAUNCH(perm_kernel, dim3(nc), dim3(64), 0, st, m);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   GatherArgs g;
   g.keys = in->keys;
@@ -1588,10 +1588,10 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   g.two = two;
   g.ksame = two && rules ? P.ksame : nullptr;
   const uint32_t gt = uint32_t((n + kGTile - 1) / kGTile);
-  if (two && rules) hipLaunchKernelGGL(mgroup_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, g);
-  hipLaunchKernelGGL(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
-  hipLaunchKernelGGL(mscan_kernel, dim3(1), dim3(1024), 0, st, g);
-  hipLaunchKernelGGL(mwrite_kernel, dim3(gt), dim3(256), 0, st, g);
+  if (two && rules) LSM_LAUNCH(mgroup_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, g);
+  LSM_LAUNCH(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
+  LSM_LAUNCH(mscan_kernel, dim3(1), dim3(1024), 0, st, g);
+  LSM_LAUNCH(mwrite_kernel, dim3(gt), dim3(256), 0, st, g);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1655,11 +1655,11 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, u
 int rotation_chains(const RotArgs& r, hipStream_t st) {
   if (hipMemsetAsync(r.need, 0, (kRotMaxLevels + 2) * sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
-  hipLaunchKernelGGL(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
-  hipLaunchKernelGGL(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
+  LSM_LAUNCH(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
+  LSM_LAUNCH(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
   const uint32_t gd = uint32_t((r.n_max + 1 + 256 * kRotPer - 1) / (256 * kRotPer));
-  for (uint32_t k = 1; k < r.levels; ++k) hipLaunchKernelGGL(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
-  hipLaunchKernelGGL(rot_f_kernel, dim3(uint32_t((r.n_max + 1 + 511) / 512)), dim3(256), 0, st, r);
+  for (uint32_t k = 1; k < r.levels; ++k) LSM_LAUNCH(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
+  LSM_LAUNCH(rot_f_kernel, dim3(uint32_t((r.n_max + 1 + 511) / 512)), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1672,28 +1672,32 @@ int rotation_locked(lsmblk_ctx* c, RotArgs r, hipStream_t st) {
   // K doubling levels (chain elements [0, 2^K); the last level does not square F), then the
   // walk + fill: K = 3 up to sst_cap 4096 (walk <= 1024 loads), growing with the capacity so the
   // walk stays that short.  Config C (1 803 SSTs, sst_cap 4 096): 12 levels, 0.89 ms ->
-  // 4 levels + walk + fill 0.40 ms -> 3 levels (2 squarings) + walk + fill.
+  // 4 levels + walk + fill 0.40 ms -> 3 levels (2 squarings) + walk + fill.  The fill follows
+  // 2^K - 1 elements through F one after another per thread, so K stays <= kRotFillMax: a larger
+  // capacity (sst_cap > 2^17) takes every doubling level instead (ceil(log2 sst_cap) squarings,
+  // no walk, no fill) -- never a chain of serial loads that grows with the capacity.
   uint32_t lc = 0;  // ceil(log2(sst_cap))
   while (lc < 32 && (1ull << lc) < r.sst_cap) ++lc;
-  const uint32_t K = lc > 12 ? lc - 9 : 3;
+  constexpr uint32_t kRotFillMax = 8;
+  const uint32_t K = lc <= 12 ? 3u : (lc - 9 <= kRotFillMax ? lc - 9 : 32u);  // 32: doubling to the end
   uint32_t* cur = r.F0;
   uint32_t* nxt = r.F1;
   for (uint32_t k = 0; k < 32 && (1ull << k) < r.sst_cap; ++k) {
     if (k == K) {
-      hipLaunchKernelGGL(rot_walk_kernel, dim3(1), dim3(64), 0, st, r, K, cur);
-      hipLaunchKernelGGL(rot_fill_kernel, dim3(uint32_t(((r.sst_cap >> K) + 1 + 63) / 64)), dim3(64), 0, st, r, K);
-      hipLaunchKernelGGL(rot_filled_kernel, dim3(1), dim3(64), 0, st, r, lc);
+      LSM_LAUNCH(rot_walk_kernel, dim3(1), dim3(64), 0, st, r, K, cur);
+      LSM_LAUNCH(rot_fill_kernel, dim3(uint32_t(((r.sst_cap >> K) + 1 + 63) / 64)), dim3(64), 0, st, r, K);
+      LSM_LAUNCH(rot_filled_kernel, dim3(1), dim3(64), 0, st, r, lc);
       break;
     }
     const bool last = k + 1 == K && (2ull << k) < r.sst_cap;  // the walk follows: no squaring
-    hipLaunchKernelGGL(rot_chain_kernel, dim3(last ? uint32_t(((1ull << k) + 255) / 256) : g), dim3(256), 0, st, r,
+    LSM_LAUNCH(rot_chain_kernel, dim3(last ? uint32_t(((1ull << k) + 255) / 256) : g), dim3(256), 0, st, r,
                        k, cur, last ? nullptr : nxt);
-    hipLaunchKernelGGL(rot_chain_check_kernel, dim3(1), dim3(64), 0, st, r, k);
+    LSM_LAUNCH(rot_chain_check_kernel, dim3(1), dim3(64), 0, st, r, k);
     if (last) continue;             // cur stays F^(2^k) = F^(2^(K-1)) for the walk
     cur = nxt;                      // F^(2^(k+1))
     nxt = cur == r.F1 ? r.F2 : r.F1;  // F (F0) is kept for the fill
   }
-  hipLaunchKernelGGL(rot_finish_kernel, dim3(1), dim3(256), 0, st, r);
+  LSM_LAUNCH(rot_finish_kernel, dim3(1), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1762,7 +1766,7 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const 
   if (range && ((range->has_lo && range->lo_len && !range->lo) || (range->has_hi && range->hi_len && !range->hi)))
     return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(stats + 4, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
@@ -1770,7 +1774,7 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const 
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
                                 o->nprefix, range, kept, stats, st, &MP, 0)))
     return rc;
-  if (in->n) hipLaunchKernelGGL(copy_u64_kernel, dim3(1), dim3(64), 0, st, stats + 4, MP.m.mstats);
+  if (in->n) LSM_LAUNCH(copy_u64_kernel, dim3(1), dim3(64), 0, st, stats + 4, MP.m.mstats);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1780,7 +1784,7 @@ int lsmblk_shard_rotation_prepare(lsmblk_ctx* c, const lsmblk_kv_stream* ext, ui
   if (block_size == 0 || target_sst_size == 0 || sst_cap == 0 || n_own > ext->n || ext->n >= 0xFFFFFFF0ull)
     return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   c->shard_ready = false;
@@ -1795,10 +1799,10 @@ int lsmblk_shard_rotation_prepare(lsmblk_ctx* c, const lsmblk_kv_stream* ext, ui
   c->shard_flags = flags;
   c->shard_sst_cap = sst_cap;
   const RotArgs r = shard_args(c, ext);
-  hipLaunchKernelGGL(set_u64_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(r.dn), uint64_t(ext->n));
+  LSM_LAUNCH(set_u64_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(r.dn), uint64_t(ext->n));
   if ((rc = rotation_chains(r, st))) return rc;
   const uint32_t gr = uint32_t((ext->n + 1 + 255) / 256);
-  for (uint32_t k = 1; k < fl; ++k) hipLaunchKernelGGL(rot_flev_kernel, dim3(gr), dim3(256), 0, st, r, k);
+  for (uint32_t k = 1; k < fl; ++k) LSM_LAUNCH(rot_flev_kernel, dim3(gr), dim3(256), 0, st, r, k);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   c->shard_ready = true;
   return LSMBLK_OK;
@@ -1808,10 +1812,10 @@ int lsmblk_shard_rotation_carry(lsmblk_ctx* c, const uint64_t* carry_in, uint64_
   if (!c || !carry_in || !carry_out) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->shard_ready) return LSMBLK_E_INVAL;
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   const RotArgs r = shard_args(c, nullptr);
-  hipLaunchKernelGGL(shard_carry_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), r, carry_in,
+  LSM_LAUNCH(shard_carry_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), r, carry_in,
                      carry_out);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -1824,20 +1828,20 @@ int lsmblk_shard_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* ext, uint8_
   if (seg_cap < 2 || blk_cap == 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->shard_ready || ext->n != c->shard_n) return LSMBLK_E_INVAL;
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const RotArgs r = shard_args(c, ext);
   uint64_t* est = r.sstate + 8;
   if (hipMemsetAsync(stats, 0, LSMBLK_COMPACT_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  hipLaunchKernelGGL(shard_seg_kernel, dim3((seg_cap + 255) / 256), dim3(256), 0, st, r, seg_start, seg_cap, r.nsst);
+  LSM_LAUNCH(shard_seg_kernel, dim3((seg_cap + 255) / 256), dim3(256), 0, st, r, seg_start, seg_cap, r.nsst);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   int rc = lsmblk_impl::encode_locked(c, ext, nullptr, seg_start, r.nsst, seg_cap - 1, c->shard_block_size, out,
                                       out_cap, blk_off, blk_cap, est, st, true);
   if (rc) return rc;
   if ((rc = lsmblk_impl::segment_blocks_locked(c, seg_start, seg_cap - 1, est, seg_blk, st))) return rc;
-  hipLaunchKernelGGL(shard_stats_kernel, dim3(1), dim3(64), 0, st, stats, est, r.sstate);
+  LSM_LAUNCH(shard_stats_kernel, dim3(1), dim3(64), 0, st, stats, est, r.sstate);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1846,7 +1850,7 @@ int lsmblk_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t
   int rc = check_merge_args(c, in, run_start, nrun, out, stats);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, nullptr, out, stats,
                              reinterpret_cast<hipStream_t>(stream), nullptr, 0);
@@ -1858,7 +1862,7 @@ int lsmblk_merge_batch_ex(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint3
   if (rc) return rc;
   if (merge_mode != LSMBLK_MERGE_RUNS && merge_mode != LSMBLK_MERGE_TWO_LEVEL) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   return merge_gather_locked(c, in, run_start, nrun, 0, 0, 0, nullptr, nullptr, 0, nullptr, out, stats,
                              reinterpret_cast<hipStream_t>(stream), nullptr, merge_mode == LSMBLK_MERGE_TWO_LEVEL);
@@ -1870,7 +1874,7 @@ int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_
   if (!c || !in || !sst_start || !stats || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
   if (block_size == 0 || target_sst_size == 0 || sst_cap == 0 || in->n >= 0xFFFFFFF0ull) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   RotPlan P = plan_rot(nullptr, 0, in->n, target_sst_size);
@@ -1878,7 +1882,7 @@ int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_
   if (rc) return rc;
   P = plan_rot(c->cws, 0, in->n, target_sst_size);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  hipLaunchKernelGGL(set_u64_kernel, dim3(1), dim3(64), 0, st, P.dn, uint64_t(in->n));
+  LSM_LAUNCH(set_u64_kernel, dim3(1), dim3(64), 0, st, P.dn, uint64_t(in->n));
   RotArgs r = P.r;
   r.keys = in->keys;
   r.key_off = in->key_off;
@@ -1904,7 +1908,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return LSMBLK_E_INVAL;
   const uint32_t two = o->merge_mode == LSMBLK_MERGE_TWO_LEVEL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const uint64_t n = in->n;
@@ -1923,7 +1927,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
                                 o->nprefix, nullptr, kept, fst, st, &MP, two)))
     return rc;
   R = plan_rot(c->cws, M.bytes, n, o->target_sst_size);
-  hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
+  LSM_LAUNCH(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
   RotArgs r = R.r;
   r.keys = kept->keys;
   r.key_off = kept->key_off;
@@ -1941,7 +1945,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
                                        blk_off, blk_cap, est, st)))
     return rc;
   if ((rc = lsmblk_impl::segment_blocks_locked(c, sst_start, sst_cap - 1, est, sst_blk, st))) return rc;
-  hipLaunchKernelGGL(compact_stats_kernel, dim3(1), dim3(64), 0, st, stats, fst, rst, est, MP.m.mstats);
+  LSM_LAUNCH(compact_stats_kernel, dim3(1), dim3(64), 0, st, stats, fst, rst, est, MP.m.mstats);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 

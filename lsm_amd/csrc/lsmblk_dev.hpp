@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <vector>
 
 #include "lsmblk.h"
 
@@ -20,6 +21,13 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr uint32_t kSpinLimit = 1u << 22;  // look-back bound (~seconds); never reached when correct
+
+// Diagnostics build (lsm_amd/_build.py builds liblsmblk_diag.so with -DLSMBLK_DIAG_BUILD=1 next to the
+// product liblsmblk.so with 0): only there do the kernels honour the ablation masks of
+// LSMBLK_DEBUG_DECODE_SKIP, which make outputs wrong for timing experiments.  In the product
+// library the masks fold to 0 at compile time and lsmblk_debug_set refuses the key.
+constexpr bool kDiag = LSMBLK_DIAG_BUILD != 0;
+__device__ __forceinline__ uint32_t diag_mask(uint32_t skip) { return kDiag ? skip : 0u; }
 
 // ---------------------------------------------------------------- wave primitives
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -473,10 +481,19 @@ struct lsmblk_ctx {
   bool dbg_on = false;
   uint32_t epoch = 0;            // 1..16383; 0 = status arrays need clearing
   uint32_t poll = 0;             // look-back poll protocol (see gload)
-  uint32_t skip = 0;             // decode ablation mask (timing experiments only)
-  bool timing = false;           // record HIP events around every kernel (diagnostics)
-  hipEvent_t ev[10] = {};        // start / stop: count 0 1, scan 2 3, decode 4 5, plan 6 7, emit 8 9
-  bool dec_timed = false, enc_timed = false;
+  uint32_t skip = 0;             // ablation mask (diagnostics builds only: kDiag)
+  bool timing = false;           // dispatch start / stop events on every kernel launch (diagnostics)
+  // kernel log (timing on): a ring of launches with their dispatch events; slot = the
+  // lsmblk_ctx_kernel_times entry the launch counts towards (-1: none)
+  struct KLog {
+    const char* name;
+    int slot;
+    hipEvent_t e0, e1;
+  };
+  std::vector<KLog> klog;        // kKLogCap entries once timing is first switched on
+  uint64_t klog_n = 0;           // launches logged since the last lsmblk_ctx_kernel_log
+  uint64_t klog_total = 0;       // launches logged since timing was switched on
+  uint64_t dec_log0 = 0, dec_log1 = 0, enc_log0 = 0, enc_log1 = 0;  // klog_total range of the last decode / encode
   // BlockMeta sections (lsmblk_block_meta_batch)
   uint32_t* meta_rec = nullptr;     // nblk
   uint64_t* meta_pos = nullptr;     // nblk + 1
@@ -537,23 +554,74 @@ int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per, unsigned flags = 0) 
 }
 }  // namespace
 
+// The context whose ABI call is running on this thread (set by DeviceGuard under the context's
+// lock): every kernel launch of the call goes through lsm_launch, which logs it when the
+// context's kernel timing is on.
+inline thread_local lsmblk_ctx* tl_launch_ctx = nullptr;
+constexpr uint32_t kKLogCap = 16384;
+
 namespace {
 // Make `dev` current for one ABI call and restore the caller's device afterwards: the library
 // never changes which device the calling thread's later allocations land on.
 struct DeviceGuard {
   int prev = -1;
   bool ok = false;
-  explicit DeviceGuard(int dev) {
+  lsmblk_ctx* prev_ctx = nullptr;
+  explicit DeviceGuard(int dev, lsmblk_ctx* c = nullptr) {
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+    prev_ctx = tl_launch_ctx;
+    tl_launch_ctx = c;
   }
   ~DeviceGuard() {
+    tl_launch_ctx = prev_ctx;
     if (prev >= 0) (void)hipSetDevice(prev);
   }
   DeviceGuard(const DeviceGuard&) = delete;
   DeviceGuard& operator=(const DeviceGuard&) = delete;
 };
+
+// The next kernel-log entry of c (events created on first use of a ring slot), nullptr when
+// events cannot be created (the launch then runs untimed).
+inline lsmblk_ctx::KLog* klog_next(lsmblk_ctx* c, const char* name, int slot) {
+  if (c->klog.size() != kKLogCap) c->klog.assign(kKLogCap, lsmblk_ctx::KLog{nullptr, -1, nullptr, nullptr});
+  lsmblk_ctx::KLog& e = c->klog[c->klog_total % kKLogCap];
+  if (!e.e0 && hipEventCreate(&e.e0) != hipSuccess) return nullptr;
+  if (!e.e1 && hipEventCreate(&e.e1) != hipSuccess) return nullptr;
+  e.name = name;
+  e.slot = slot;
+  ++c->klog_n;
+  ++c->klog_total;
+  return &e;
+}
+
+// The launches of one ABI call (kernel log indices [*a, *b)), for lsmblk_ctx_kernel_times.
+struct KLogRange {
+  lsmblk_ctx* c;
+  uint64_t* b;
+  KLogRange(lsmblk_ctx* c_, uint64_t* a_, uint64_t* b_) : c(c_), b(b_) { *a_ = *b_ = c->klog_total; }
+  ~KLogRange() { *b = c->klog_total; }
+  KLogRange(const KLogRange&) = delete;
+  KLogRange& operator=(const KLogRange&) = delete;
+};
+
+// Every kernel launch of the library: with the running call's context timing on, the dispatch
+// itself fills the log entry's start / stop events (hipExtLaunchKernelGGL) -- the kernel's own
+// begin and end, as rocprofv3 reports them (event markers recorded between launches added ~8 %).
+template <typename K, typename... Args>
+inline void lsm_launch(const char* name, int slot, K kern, dim3 grid, dim3 block, uint32_t shmem, hipStream_t st,
+                       Args... args) {
+  lsmblk_ctx* c = tl_launch_ctx;
+  lsmblk_ctx::KLog* e = c && c->timing ? klog_next(c, name, slot) : nullptr;
+  if (e)
+    hipExtLaunchKernelGGL(kern, grid, block, shmem, st, e->e0, e->e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kern, grid, block, shmem, st, args...);
+}
 }  // namespace
+#define LSM_LAUNCH(kern, grid, block, shmem, st, ...) lsm_launch(#kern, -1, kern, grid, block, shmem, st, __VA_ARGS__)
+#define LSM_LAUNCH_SLOT(slot, kern, grid, block, shmem, st, ...) \
+  lsm_launch(#kern, slot, kern, grid, block, shmem, st, __VA_ARGS__)
 
 // Internal entry points shared between translation units (called with ctx->mu held).
 namespace lsmblk_impl {

@@ -601,7 +601,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
   uint32_t cn = 0, ck = 0, cv = 0;
   uint64_t tp0 = 0, tp1 = 0, tp2 = 0, gb = 0;
   if constexpr (lagm) {
-    if (l < 3 && !(a.skip & 4096)) gb = gload(a.bbase + 3 * b + l, 0);  // (4096: ablation)
+    if (l < 3 && !(diag_mask(a.skip) & 4096)) gb = gload(a.bbase + 3 * b + l, 0);  // (4096: ablation)
   } else {
     if (l < jb) {
       const uint64_t q = tb * kTile + l;
@@ -662,7 +662,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
     post();
     h = parse_hdr(GlbImg{R, lead}, len);
   }
-  if (a.skip & 256) return;  // ablation: staging only
+  if (diag_mask(a.skip) & 256) return;  // ablation: staging only
   if (!h.ok) err |= LSMBLK_ERR_MALFORMED;
   const bool fast = fits && h.n <= kDecMaxE;
   // large block: entry tables in LDS, bytes HBM -> HBM; more than kDecMaxE entries are taken
@@ -732,7 +732,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
       V += wave_sum<uint64_t>(vl);
     }
   }
-  if (a.skip & 512) return;  // ablation: staging + entry tables only
+  if (diag_mask(a.skip) & 512) return;  // ablation: staging + entry tables only
   if (__ballot(bad)) err |= LSMBLK_ERR_MALFORMED;
   uint64_t agg[3] = {h.n, K, V};
   if (err) agg[0] = agg[1] = agg[2] = 0;
@@ -745,7 +745,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
     const uint64_t want = (uint64_t(a.tag) << 2) | 2;
     uint32_t spins = 0;
     if (b % kTile == 0) dbg_trace(a.dbg, b / kTile, 2);
-    while (!(a.skip & 2048) && __ballot(l < 3 && (gb & 0xFFFF) != want)) {  // (2048: ablation, no wait)
+    while (!(diag_mask(a.skip) & 2048) && __ballot(l < 3 && (gb & 0xFFFF) != want)) {  // (2048: ablation, no wait)
       if (++spins > kSpinLimit) {
         err |= LSMBLK_ERR_TIMEOUT;
         break;
@@ -782,7 +782,7 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
 
   if (!(err & (LSMBLK_ERR_MALFORMED | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_OVERFLOW | LSMBLK_ERR_CAPACITY)) && h.n) {
     if (fast) {
-      dec_fast_outputs(a, L, lead, h, ent, E0, K0, V0, uint32_t(K), uint32_t(V), a.skip);
+      dec_fast_outputs(a, L, lead, h, ent, E0, K0, V0, uint32_t(K), uint32_t(V), diag_mask(a.skip));
     } else if (big && h.n <= kDecMaxE) {
       dec_big_outputs(a, T, R, lead, h, h.n, E0, K0, V0, uint32_t(K), uint32_t(V), reinterpret_cast<uint32_t*>(L.out));
     } else if (big) {
@@ -993,7 +993,7 @@ __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   const uint64_t o0 = a.lag_bytes ? a.blk_off[0] : 0, o1 = a.lag_bytes ? a.blk_off[a.nblk] : 0;
   const uint64_t cs = lane64(o, 0), ce = lane64(o, 1);
   CntPre C;
-  const bool do_cnt = cnt && !(a.skip & 1024);  // (1024: ablation, aggregates 0 without the count)
+  const bool do_cnt = cnt && !(diag_mask(a.skip) & 1024);  // (1024: ablation, aggregates 0 without the count)
   if (do_cnt) C = cnt_issue(a.blocks, a.tail, cs, ce);
   uint64_t lag = a.lag;  // (worked out under the count's loads)
   if (a.lag_bytes) {
@@ -1033,13 +1033,13 @@ __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   const uint64_t ft = j >= D ? (j - D + 8) / kTile : ~0ull;  // the tile workgroup j finishes, if any
   const bool fin = j >= D && ft * kTile + D - (ft & 7) == j && ft * kTile < a.nblk;
   auto publish = [&] {
-    if (!cnt || (a.skip & 16384)) return;  // (16384: ablation, no publish)
+    if (!cnt || (diag_mask(a.skip) & 16384)) return;  // (16384: ablation, no publish)
     // (a malformed block is reported by its decoder; its aggregate is 0 there too)
     publish3(a.bagg, j, r.n, r.K, r.V, a.tag, 1, a.poll);
     if (r.K > 0xFFFFFFFFull || r.V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
   };
   auto finish = [&] {
-    if (fin && !(a.skip & (8192 | 16384))) lag_tile_finish(a, ft, err);  // (8192: ablation, no tile finish)
+    if (fin && !(diag_mask(a.skip) & (8192 | 16384))) lag_tile_finish(a, ft, err);  // (8192: ablation, no tile finish)
   };
   if (dec) {
     decode_block<true>(a, lds, b, ds, de, count, publish, finish);
@@ -1296,7 +1296,7 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
         }
       }
       u32x4 xk[kProdBatch], xp[kProdBatch];
-      const bool nokeys = a.skip & (1u << 16);
+      const bool nokeys = diag_mask(a.skip) & (1u << 16);
 #pragma unroll
       for (uint32_t i = 0; i < kProdBatch; ++i) {
         const uint32_t e = c + 64 * (h + i) + l;
@@ -1442,7 +1442,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     for (uint32_t j0 = s;; j0 += 64) {
       const uint32_t wend = s1 - j0 < 64 ? s1 : j0 + 64;
       need(j0, wend);
-      if (a.skip & (1u << 17)) {  // ablation: consume the window as one block, no scans
+      if (diag_mask(a.skip) & (1u << 17)) {  // ablation: consume the window as one block, no scans
         const uint32_t x = (j0 + l - s0) & (kRing - 1);
         const uint32_t rr = j0 + l < s1 ? CR[x] + CA[x] : 0u;
         if (l == 0) {
@@ -1662,7 +1662,7 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
       kl = a.key_off[s + k + 1] - (kp - kg);
       vp = vg + a.val_off[s + k];
       vl = a.val_off[s + k + 1] - (vp - vg);
-      if (k != 0 && !(a.skip & 128)) {  // builder.rs:62 common_prefix(first_key, key)
+      if (k != 0 && !(diag_mask(a.skip) & 128)) {  // builder.rs:62 common_prefix(first_key, key)
         const uint32_t m = fl < kl ? fl : kl;
         p = m;
         for (uint32_t q = 0; q < m; q += 16) {
@@ -1693,7 +1693,7 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
     if (k < n) {
       const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
       vdst = at + 14 + sfx;
-      if (!(a.skip & 16)) {
+      if (!(diag_mask(a.skip) & 16)) {
       // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value
       __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
       copy_run(RK, kp + p, klim, RO, at + 4, sfx);
@@ -1707,7 +1707,7 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
                                             ob + uint32_t(data_len) + 2 * k, 0, 0);
       }
     }
-    if (!(a.skip & 32)) copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc);
+    if (!(diag_mask(a.skip) & 32)) copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc);
   }
   if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
   if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
@@ -1875,7 +1875,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         kl = ko1 - ko0;
         vp = vo0 - vb0;
         vl = vo1 - vo0;
-        if (k != 0 && !(a.skip & 128)) {
+        if (k != 0 && !(diag_mask(a.skip) & 128)) {
           const uint32_t m = fl < kl ? fl : kl;
           p = m;
           bool done = false;
@@ -1949,7 +1949,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     // record), so a chunk's source lies below the chunk's end: walking batches of chunks from
     // the top, with all of a batch's reads before its writes, never overwrites a source still
     // unread.
-    if (!(a.skip & 32)) {
+    if (!(diag_mask(a.skip) & 32)) {
       const int32_t top = int32_t((ncs + 63) & ~63u);
       for (int32_t c0 = top; c0 > 0; c0 -= int32_t(64 * kEB)) {
         uint32_t src[kEB];
@@ -1970,7 +1970,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     wave_sync();
     // Phase 3, entry lanes: header, key suffix, ts, value_len, and the value bytes of the
     // partial edge chunks (from the registers captured in phase 1).
-    if (!(a.skip & 16)) {
+    if (!(diag_mask(a.skip) & 16)) {
 #pragma unroll
       for (uint32_t it = 0; it < 2; ++it) {
         const uint32_t k = 64 * it + l;
@@ -2013,7 +2013,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
     // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
-    if (!(a.skip & 64) && O + size <= a.out_cap) flush_run<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
+    if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
     wave_sync();
     if (!has_next) break;
     cur = nxt;
@@ -2824,19 +2824,6 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 }  // namespace lsmblk_impl
 
-// Kernel launch for the host half.  With kernel timing on (lsmblk_debug_set), the launch carries
-// start / stop events filled in by the dispatch itself (hipExtLaunchKernelGGL) -- the kernel's own
-// begin and end, as rocprofv3 reports them; event markers recorded between launches added ~8 % to
-// the per-kernel times.  e0 / e1: context event indices, -1 for none.
-template <typename K, typename... Args>
-static void tlaunch(lsmblk_ctx* c, K kern, dim3 grid, dim3 block, hipStream_t st, int e0, int e1, Args... args) {
-  if (c->timing)
-    hipExtLaunchKernelGGL(kern, grid, block, 0, st, e0 >= 0 ? c->ev[e0] : nullptr, e1 >= 0 ? c->ev[e1] : nullptr, 0,
-                          args...);
-  else
-    hipLaunchKernelGGL(kern, grid, block, 0, st, args...);
-}
-
 extern "C" {
 
 int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
@@ -2858,7 +2845,7 @@ int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
 
 void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   if (!c) return;
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   (void)hipDeviceSynchronize();
   (void)hipFree(c->counters);
   (void)hipFree(c->dec_agg);
@@ -2884,8 +2871,10 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->rws);
   (void)hipFree(c->lag_gran);
   (void)hipFree(c->dbg);
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->klog) {
+    if (e.e0) (void)hipEventDestroy(e.e0);
+    if (e.e1) (void)hipEventDestroy(e.e1);
+  }
   delete c;
 }
 
@@ -2894,13 +2883,13 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
   std::lock_guard<std::mutex> g(c->mu);
   if (key == LSMBLK_DEBUG_POLL_MODE && value <= 2) {
     c->poll = value;
-  } else if (key == LSMBLK_DEBUG_DECODE_SKIP) {
+  } else if (key == LSMBLK_DEBUG_DECODE_SKIP && kDiag) {  // ablation masks: diagnostics builds only
     c->skip = value;
   } else if (key == LSMBLK_DEBUG_TWO_PASS_DECODE) {
     c->dec_two_pass = value != 0;
   } else if (key == LSMBLK_DEBUG_COUNTERS) {
     if (value && !c->dbg) {
-      DeviceGuard dg(c->device);
+      DeviceGuard dg(c->device, c);
       if (!dg.ok || hipMalloc(reinterpret_cast<void**>(&c->dbg), kDbgWords * 8) != hipSuccess) {
         c->dbg = nullptr;
         return LSMBLK_E_NOMEM;
@@ -2916,12 +2905,7 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->dec_lag = value;
     c->dec_lag_bytes = 0;  // exactly this lag (experiments)
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
-    if (value && !c->ev[0]) {
-      DeviceGuard dg(c->device);
-      if (!dg.ok) return LSMBLK_E_HIP;
-      for (auto& e : c->ev)
-        if (hipEventCreate(&e) != hipSuccess) return LSMBLK_E_HIP;
-    }
+    if (value && !c->timing) c->klog_n = 0;  // the log restarts with the timing
     c->timing = value != 0;
   } else {
     return LSMBLK_E_INVAL;
@@ -2934,7 +2918,7 @@ int lsmblk_debug_counters(lsmblk_ctx* c, uint64_t* out, uint32_t n) {
   std::lock_guard<std::mutex> g(c->mu);
   for (uint32_t i = 0; i < n; ++i) out[i] = 0;
   if (!c->dbg) return LSMBLK_OK;
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok || hipDeviceSynchronize() != hipSuccess) return LSMBLK_E_HIP;
   return hipMemcpy(out, c->dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -2942,18 +2926,52 @@ int lsmblk_debug_counters(lsmblk_ctx* c, uint64_t* out, uint32_t n) {
 int lsmblk_ctx_kernel_times(lsmblk_ctx* c, float* ms) {
   if (!c || !ms) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  for (int i = 0; i < LSMBLK_KERNELS; ++i) ms[i] = -1.f;
-  if (!c->ev[0]) return LSMBLK_OK;
-  auto span = [&](int a, int b, float* out) -> int {
-    if (hipEventSynchronize(c->ev[b]) != hipSuccess) return LSMBLK_E_HIP;
-    return hipEventElapsedTime(out, c->ev[a], c->ev[b]) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  for (int i = 0; i < LSMBLK_KERNELS; ++i) ms[i] = -1.f;  // a kernel the last call did not launch
+  if (c->klog.empty()) return LSMBLK_OK;
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  // the last decode's and the last encode's launches (while still in the ring), summed by slot
+  auto add = [&](uint64_t i0, uint64_t i1) -> int {
+    if (c->klog_total - i0 > kKLogCap) return LSMBLK_OK;  // overwritten since
+    for (uint64_t i = i0; i < i1; ++i) {
+      const lsmblk_ctx::KLog& e = c->klog[i % kKLogCap];
+      if (e.slot < 0 || e.slot >= LSMBLK_KERNELS) continue;
+      float t = 0.f;
+      if (hipEventSynchronize(e.e1) != hipSuccess || hipEventElapsedTime(&t, e.e0, e.e1) != hipSuccess)
+        return LSMBLK_E_HIP;
+      ms[e.slot] = (ms[e.slot] < 0.f ? 0.f : ms[e.slot]) + t;
+    }
+    return LSMBLK_OK;
   };
-  int rc = LSMBLK_OK;
-  if (c->dec_timed) {
-    if ((rc = span(0, 1, &ms[0])) || (rc = span(2, 3, &ms[1])) || (rc = span(4, 5, &ms[2]))) return rc;
-  }
-  if (c->enc_timed) {
-    if ((rc = span(6, 7, &ms[3])) || (rc = span(8, 9, &ms[4]))) return rc;
+  const int rc = add(c->dec_log0, c->dec_log1);
+  return rc ? rc : add(c->enc_log0, c->enc_log1);
+}
+
+int lsmblk_ctx_kernel_log(lsmblk_ctx* c, lsmblk_kernel_stat* out, uint32_t cap, uint32_t* n) {
+  if (!c || !n || (cap && !out)) return LSMBLK_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  *n = 0;
+  const uint64_t cnt = c->klog_n;
+  c->klog_n = 0;
+  if (cnt == 0) return LSMBLK_OK;
+  if (cnt > kKLogCap) return LSMBLK_E_CAPACITY;  // the ring was overwritten: read it more often
+  DeviceGuard dg(c->device);
+  if (!dg.ok) return LSMBLK_E_HIP;
+  for (uint64_t i = c->klog_total - cnt; i < c->klog_total; ++i) {
+    const lsmblk_ctx::KLog& e = c->klog[i % kKLogCap];
+    float t = 0.f;
+    if (hipEventSynchronize(e.e1) != hipSuccess || hipEventElapsedTime(&t, e.e0, e.e1) != hipSuccess)
+      return LSMBLK_E_HIP;
+    uint32_t k = 0;
+    while (k < *n && strncmp(out[k].name, e.name, sizeof(out[k].name) - 1) != 0) ++k;
+    if (k == *n) {
+      if (k == cap) return LSMBLK_E_CAPACITY;
+      memset(&out[k], 0, sizeof(out[k]));
+      strncpy(out[k].name, e.name, sizeof(out[k].name) - 1);
+      ++*n;
+    }
+    out[k].launches += 1;
+    out[k].ms += t;
   }
   return LSMBLK_OK;
 }
@@ -2961,7 +2979,7 @@ int lsmblk_ctx_kernel_times(lsmblk_ctx* c, float* ms) {
 int lsmblk_ctx_reserve(lsmblk_ctx* c, uint64_t max_blocks, uint64_t max_entries, uint64_t max_segments) {
   if (!c) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   return reserve_locked(c, max_blocks, max_entries, max_segments);
 }
@@ -2979,14 +2997,14 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   if (nblk > 0x7FFFFFFFull || tail > 16) return LSMBLK_E_INVAL;  // one workgroup (or wave) per block
   if ((flags & LSMBLK_DECODE_VERIFY_CRC) && tail != 4) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc = reserve_locked(c, nblk, 0, 0);
   if (rc) return rc;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nblk == 0) {
-    hipLaunchKernelGGL(finish_empty_decode, dim3(1), dim3(64), 0, st, out->key_off, out->val_off, out->entry_cap);
+    LSM_LAUNCH(finish_empty_decode, dim3(1), dim3(64), 0, st, out->key_off, out->val_off, out->entry_cap);
     if (blk_ent && hipMemsetAsync(blk_ent, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
@@ -3001,7 +3019,7 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   }
   const uint64_t ntiles = (nblk + kTile - 1) / kTile;
-  c->dec_timed = c->timing;
+  const KLogRange lr(c, &c->dec_log0, &c->dec_log1);
   DecodeArgs a;
   a.blocks = blocks;
   a.blk_off = blk_off;
@@ -3030,30 +3048,26 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     a.bbase = a.bagg + 3 * c->lag_blk_cap;
     a.tagg = a.bbase + 3 * c->lag_blk_cap;
     a.tinc = a.tagg + 3 * ((c->lag_blk_cap + kTile - 1) / kTile + 1);
-    a.lag = c->dec_lag;
+    // a batch shorter than the lag needs no more workgroups than blocks of lag: any lag >= 2 kTile
+    // keeps the finisher schedule (decode_lag_kernel) deadlock-free, and lag >= nblk counts every
+    // block before the first decode (one 4 KiB block launched 10 241 workgroups)
+    a.lag = std::max<uint64_t>(2 * kTile, std::min<uint64_t>(c->dec_lag, nblk));
     a.lag_bytes = c->dec_lag_bytes;
     a.dbg = c->dbg_on ? c->dbg : nullptr;
     if (a.dbg && hipMemsetAsync(a.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     a.tag = c->epoch;
     a.poll = c->poll;
-    tlaunch(c, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), st, 4, 5, a);
-    if (c->timing) {  // the count and scan slots of lsmblk_ctx_kernel_times read 0
-      (void)hipEventRecord(c->ev[0], st);
-      (void)hipEventRecord(c->ev[1], st);
-      (void)hipEventRecord(c->ev[2], st);
-      (void)hipEventRecord(c->ev[3], st);
-    }
+    LSM_LAUNCH_SLOT(2, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
   if (flags & LSMBLK_DECODE_VERIFY_CRC) {
-    if (c->timing) (void)hipEventRecord(c->ev[0], st);
     // one pass over E: the CRC of every block and its (entries, key bytes, value bytes), in
     // place of the count pass's second read of E
     if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st, c->dec_agg)))
       return rc;
-    hipLaunchKernelGGL(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
+    LSM_LAUNCH(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
                        c->vcrc, c->meta_cstats, stats);
-    tlaunch(c, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), st, -1, 1, (const uint32_t*)c->dec_agg, nblk,
+    LSM_LAUNCH_SLOT(0, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), 0, st, (const uint32_t*)c->dec_agg, nblk,
             c->tile_sum);
   } else {
     CountArgs ca;
@@ -3064,8 +3078,8 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     ca.tile_sum = c->tile_sum;
     ca.stats = stats;
     ca.tail = tail;
-    tlaunch(c, dec_count_staged_kernel, dim3(uint32_t(nblk)), dim3(64), st, 0, -1, ca);
-    tlaunch(c, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), st, -1, 1, (const uint32_t*)c->dec_agg,
+    LSM_LAUNCH_SLOT(0, dec_count_staged_kernel, dim3(uint32_t(nblk)), dim3(64), 0, st, ca);
+    LSM_LAUNCH_SLOT(0, agg_tile_kernel, dim3(uint32_t((ntiles + 3) / 4)), dim3(256), 0, st, (const uint32_t*)c->dec_agg,
             nblk, c->tile_sum);
   }
   ScanArgs sa;
@@ -3080,8 +3094,8 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   sa.stats = stats;
   sa.blk_ent = blk_ent;
   sa.nblk = nblk;
-  tlaunch(c, dec_scan_kernel, dim3(1), dim3(1024), st, 2, 3, sa);
-  tlaunch(c, decode_kernel, dim3(uint32_t(nblk)), dim3(64), st, 4, 5, a);
+  LSM_LAUNCH_SLOT(1, dec_scan_kernel, dim3(1), dim3(1024), 0, st, sa);
+  LSM_LAUNCH_SLOT(2, decode_kernel, dim3(uint32_t(nblk)), dim3(64), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -3092,7 +3106,7 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   if (in->n >= 0xFFFFFFFFull || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
   if (block_size == 0) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   return lsmblk_impl::encode_locked(c, in, nullptr, seg_start, nullptr, nseg, block_size, out, out_cap, blk_off,
                                     blk_cap, stats, reinterpret_cast<hipStream_t>(stream));
@@ -3104,6 +3118,7 @@ namespace lsmblk_impl {
 int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
                   const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
                   uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span) {
+  const KLogRange lr(c, &c->enc_log0, &c->enc_log1);
   // in->n (and nseg) are upper bounds when dn (dnseg) point at the device-side values
   int rc = reserve_locked(c, 0, in->n, nseg);
   if (rc) return rc;
@@ -3142,13 +3157,8 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.skip = c->skip;
   p.dbg = c->dbg_on ? c->dbg : nullptr;
   if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  c->enc_timed = c->timing;
-  tlaunch(c, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), st, 6, 7, p);
+  LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), 0, st, p);
   if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
-    if (c->timing) {
-      (void)hipEventRecord(c->ev[8], st);
-      (void)hipEventRecord(c->ev[9], st);
-    }
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
   // the big-block flags are cleared before emit (the start of emit_kernel to the end of
@@ -3178,14 +3188,14 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
-  tlaunch(c, emit_kernel, dim3(grid), dim3(256), st, 8, -1, e);
-  tlaunch(c, emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), st, -1, 9, e);
+  LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), 0, st, e);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
 int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
                           uint32_t* seg_blk, hipStream_t st) {
-  hipLaunchKernelGGL(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg_max) + 256) / 256)), dim3(256), 0, st,
+  LSM_LAUNCH(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg_max) + 256) / 256)), dim3(256), 0, st,
                      c->blk_first, enc_stats, seg_start, nseg_max, seg_blk);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -3197,7 +3207,7 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
                        uint32_t* crc, uint64_t* stats, void* stream) {
   if (!c || !blk_off || !stats || (nblk && !crc)) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   int rc = lsmblk_impl::ensure_crc_tabs(c);
   if (rc) return rc;
@@ -3211,11 +3221,11 @@ int lsmblk_encode_segment_blocks(lsmblk_ctx* c, const uint32_t* seg_start, uint3
                                  uint32_t* seg_blk, void* stream) {
   if (!c || !seg_start || !enc_stats || !seg_blk) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   if (!c->blk_first) return LSMBLK_E_INVAL;  // no encode ran on this context
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg) + 256) / 256)), dim3(256), 0, st,
+  LSM_LAUNCH(seg_blocks_kernel, dim3(uint32_t((uint64_t(nseg) + 256) / 256)), dim3(256), 0, st,
                      c->blk_first, enc_stats, seg_start, nseg, seg_blk);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -3226,7 +3236,7 @@ int lsmblk_block_meta_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t
   if (!c || !blk_off || !seg_blk || !meta_off || !stats || !meta || meta_cap < 16) return LSMBLK_E_INVAL;
   if (nseg == 0 || nblk >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   return lsmblk_impl::block_meta_locked(c, blocks, blk_off, nblk, tail, seg_blk, nseg, meta, meta_cap, meta_off,
                                         stats, reinterpret_cast<hipStream_t>(stream));
@@ -3273,15 +3283,15 @@ int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_
   a.crc_stats = c->meta_cstats;
   a.stats = stats;
   const uint32_t sg = uint32_t((uint64_t(nseg) + 255) / 256);
-  if (ntiles) hipLaunchKernelGGL(meta_size_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(meta_scan_kernel, dim3(1), dim3(1024), 0, st, a);
-  if (ntiles) hipLaunchKernelGGL(meta_write_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(meta_seg_kernel, dim3(sg), dim3(256), 0, st, a);
+  if (ntiles) LSM_LAUNCH(meta_size_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  LSM_LAUNCH(meta_scan_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (ntiles) LSM_LAUNCH(meta_write_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  LSM_LAUNCH(meta_seg_kernel, dim3(sg), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   // section CRC over [meta_off[s] + 4, meta_off[s+1] - 4): blocks = meta + 4, tail = 8
   if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if ((rc = lsmblk_impl::launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st))) return rc;
-  hipLaunchKernelGGL(meta_crc_put_kernel, dim3(sg), dim3(256), 0, st, a);
+  LSM_LAUNCH(meta_crc_put_kernel, dim3(sg), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 }  // namespace lsmblk_impl
@@ -3295,7 +3305,7 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
   if (nprefix && (!prefixes || !prefix_off)) return LSMBLK_E_INVAL;
   if (in->n >= 0xFFFFFFFFull) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   const uint64_t n = in->n, ntiles = (n + kFiltTile - 1) / kFiltTile;
   int rc;
@@ -3327,9 +3337,9 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
   a.tile_sum = c->filt_tile;
   a.tile_pre = c->filt_tile + 3 * c->filt_tile_cap;
   a.stats = stats;
-  if (ntiles) hipLaunchKernelGGL(filt_flag_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(filt_scan_kernel, dim3(1), dim3(1024), 0, st, a);
-  if (ntiles) hipLaunchKernelGGL(filt_write_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  if (ntiles) LSM_LAUNCH(filt_flag_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
+  LSM_LAUNCH(filt_scan_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (ntiles) LSM_LAUNCH(filt_write_kernel, dim3(uint32_t(ntiles)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -3367,8 +3377,8 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
     per_cu = 3;
   const uint64_t want = (nblk + 3) / 4, cap = uint64_t(cus > 0 ? cus : 256) * uint64_t(per_cu);
   const dim3 grid(uint32_t(want < cap ? want : cap));
-  if (agg) hipLaunchKernelGGL(crc_kernel<true>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(crc_kernel<false>, grid, dim3(256), 0, st, a);
+  if (agg) LSM_LAUNCH(crc_kernel<true>, grid, dim3(256), 0, st, a);
+  else LSM_LAUNCH(crc_kernel<false>, grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 }  // namespace lsmblk_impl lsmblk_impl

@@ -499,13 +499,13 @@ int lsmblk_seek_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_
                       uint64_t* stats, void* stream) {
   if (!c || !blk_off || !stats || (nq && (!qkey_off || !q_blk || !idx)) || tail > 16) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nq == 0) return LSMBLK_OK;
   SeekArgs a{blocks, blk_off, nblk, tail, qkeys, qkey_off, q_blk, nq, idx, stats};
-  hipLaunchKernelGGL(seek_kernel, dim3(uint32_t((nq + 255) / 256)), dim3(256), 0, st, a);
+  LSM_LAUNCH(seek_kernel, dim3(uint32_t((nq + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -533,7 +533,7 @@ int lsmblk_sst_files_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   if (!c || !blk_off || !sst_blk || !sst_ent || !kv || !kv->key_off || !file_off || !stats) return LSMBLK_E_INVAL;
   if (nsst == 0 || nblk >= 0xFFFFFFFFull || (files_cap && !files)) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  DeviceGuard dg(c->device);
+  DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;
@@ -600,10 +600,10 @@ int lsmblk_sst_files_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   a.stats = stats;
   a.mstats = w.st + 4;
   a.cstats = w.st;
-  hipLaunchKernelGGL(sst_layout_kernel, dim3(1), dim3(1024), 0, st, a);
-  if (nblk) hipLaunchKernelGGL(sst_data_kernel, dim3(uint32_t((nblk + 3) / 4)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(sst_meta_kernel, dim3((nsst + 3) / 4), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(sst_bloom_kernel, dim3(nsst), dim3(256), 0, st, a);
+  LSM_LAUNCH(sst_layout_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (nblk) LSM_LAUNCH(sst_data_kernel, dim3(uint32_t((nblk + 3) / 4)), dim3(256), 0, st, a);
+  LSM_LAUNCH(sst_meta_kernel, dim3((nsst + 3) / 4), dim3(256), 0, st, a);
+  LSM_LAUNCH(sst_bloom_kernel, dim3(nsst), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 

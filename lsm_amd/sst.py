@@ -96,10 +96,10 @@ def sst_files(blocks, blk_off, sst_blk, sst_ent, kv: batch.KVStream, stream=None
     for _ in range(2):
         files = batch._aligned_empty(cap, dev)
         c = kv._c()
-        check(lib().lsmblk_sst_files_batch(batch._ctx(dev.index, stream), batch._ptr(blocks), blk_off.data_ptr(), nblk,
-                                           sst_blk.data_ptr(), sst_ent.data_ptr(), nsst, ctypes.byref(c),
-                                           files.data_ptr(), cap, file_off.data_ptr(), stats.data_ptr(),
-                                           batch._stream_ptr(stream, dev.index)), "lsmblk_sst_files_batch")
+        batch._native("lsmblk_sst_files_batch", dev.index, stream, batch._ptr(blocks), blk_off.data_ptr(), nblk,
+                      sst_blk.data_ptr(), sst_ent.data_ptr(), nsst, ctypes.byref(c),
+                      files.data_ptr(), cap, file_off.data_ptr(), stats.data_ptr(),
+                      batch._stream_ptr(stream, dev.index))
         torch.cuda.synchronize(dev)
         st = batch._status(stats)
         if st == -3:

@@ -113,3 +113,24 @@ def test_bench_launcher_fails_fast_when_a_rank_dies(world, fail):
     assert r.returncode != 0 and r.stdout.strip() == "", (r.returncode, r.stdout)
     assert f"rank {fail} exited with status 3" in r.stderr
     assert dt < 60, dt
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("world,fail", [(2, 1), (3, 0)])
+def test_bench_extra_failure_inside_compact_dist_ends_the_job(world, fail):
+    """A rank that raises inside shard.compact_dist during the N>1 extra config exits at once
+    (extra_or_exit) while its peers block in the head all-gather: the launcher tears the job down
+    and returns non-zero within seconds, printing no bench line."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run",
+                        "--dry-run-fail-extra", str(fail)], capture_output=True, text=True, timeout=100, env=env)
+    dt = time.time() - t0
+    assert r.returncode != 0 and r.stdout.strip() == "", (r.returncode, r.stdout)
+    assert f"[rank {fail}] extra config C failed" in r.stderr and "merge failed as asked" in r.stderr
+    assert f"rank {fail} exited with status 1" in r.stderr
+    assert dt < 60, dt

@@ -240,6 +240,26 @@ def test_sst_rotation_vs_restated_loop(bs, target):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("versions", [1, 3])
+def test_sst_rotation_large_capacity_long_chain(versions):
+    """A capacity far above the SST count's (n + 2 = 2^18: more than 2^17, so every doubling level
+    runs and no walk / fill does) with a long chain (target 1: an SST at every key change, ~10^5):
+    bit-exact, and bounded in time -- the fill's serial loads never grow with the capacity (ADVICE
+    round 3: K = lc - 9 made each fill thread follow ~sst_cap / 512 elements)."""
+    import time
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(200000 // versions, nrun=2, seed=17, versions=versions)
+    kv = O.KV(keys, ko, vals, vo, ts)
+    kept = O.gather(kv, O.merge_runs(kv, rs))
+    want = O.segment_like_compaction(kept, 4096, 1)
+    d = to_dev(kept)
+    batch.sst_rotation(d, 4096, 1)
+    t0 = time.perf_counter()
+    got = batch.sst_rotation(d, 4096, 1)
+    dt = time.perf_counter() - t0
+    np.testing.assert_array_equal(got, want)
+    assert len(want) > 50000 and dt < 0.5, (len(want), dt)
+
+
 def test_sst_rotation_unsorted_and_long_keys():
     rng = np.random.default_rng(9)
     base = bytes(rng.integers(0, 256, 80, dtype=np.uint8))

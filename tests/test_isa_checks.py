@@ -16,13 +16,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
+def _isa(tmp_path, src):
+    out = tmp_path / (src + ".s")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include", "-DLSMBLK_DIAG_BUILD=0",
+                    "--offload-device-only", "-S", "-o", str(out), os.path.join(ROOT, "lsm_amd", "csrc", src)],
+                   check=True, capture_output=True, cwd=str(tmp_path))
+    return out
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 def test_inline_asm_loads_are_landed_before_use(tmp_path):
-    out = tmp_path / "lsmblk_gpu.s"
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include", "--offload-device-only",
-                    "-S", "-o", str(out), os.path.join(ROOT, "lsm_amd", "csrc", "lsmblk_gpu.hip")],
-                   check=True, capture_output=True, cwd=str(tmp_path))
+    out = _isa(tmp_path, "lsmblk_gpu.hip")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asm_inflight_check.py"), str(out),
                         "decode_lag_kernel"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "asm loads" in r.stdout and "OK" in r.stdout, r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_every_inline_asm_site_is_checked(tmp_path):
+    """Every function with inline asm in the product sources passes the checks, and every asm
+    instruction is of a kind the checker covers (a new kind of site fails until classified)."""
+    paths = [str(_isa(tmp_path, f)) for f in ("lsmblk_gpu.hip", "lsmblk_compact.hip", "lsmblk_sst.hip")]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asm_inflight_check.py"), "--all", *paths],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    # decode_lag_kernel (staging loads), the crc / bloom kernels (SDWA), plan / merge-tile waits
+    for k in ("decode_lag_kernel", "crc_kernel", "plan_walk_kernel", "merge_tile_kernel", "sst_bloom_kernel"):
+        assert k in r.stdout, r.stdout

@@ -1,12 +1,35 @@
-"""Check, on the gfx950 ISA of one kernel, that no instruction reads or writes the registers of
-inline-asm loads between the loads and an inline-asm `s_waitcnt vmcnt` (CFG reachability).
-usage: python tools/asm_inflight_check.py ISA.s KERNEL_SYMBOL_SUBSTRING"""
+"""Checks on the gfx950 ISA of the inline-asm sites of a kernel (or of every kernel with --all):
+  * no instruction reads or writes the registers of inline-asm loads between the loads and an
+    inline-asm `s_waitcnt vmcnt` (CFG reachability): the waitcnt pass does not see asm loads;
+  * no VALU write of an SGPR that an inline-asm vector-memory instruction reads comes within 5 wait
+    states of it (the compiler's hazard recognizer does not look inside inline asm);
+  * every inline-asm instruction is of a kind these checks cover (vector loads, `s_waitcnt`,
+    `s_nop`, VALU SDWA ops on VGPRs): a new kind of asm site fails until it is classified.
+usage: python tools/asm_inflight_check.py ISA.s KERNEL_SYMBOL_SUBSTRING
+       python tools/asm_inflight_check.py --all ISA.s [ISA.s ...]"""
 import re
 import sys
 
+# inline-asm instruction kinds the checks below cover
+KNOWN = ("buffer_load", "global_load", "s_waitcnt", "s_nop", "v_and_b32_sdwa")
+
+
+def kernels_with_asm(s):
+    """Symbols of the functions in an ISA file that contain inline asm."""
+    out = []
+    for m in re.finditer(r'^(_\S+):\s*;\s*@', s, flags=re.M):
+        start = m.end()
+        end = s.index('.Lfunc_end', start)
+        if ';;#ASMSTART' in s[start:end]:
+            out.append(m.group(1))
+    return out
+
 
 def main(path, kname):
-    s = open(path).read()
+    return check(open(path).read(), kname)
+
+
+def check(s, kname):
     name_line = [l for l in s.split('\n') if l.startswith('_') and kname in l and re.match(r'^\S+:', l)][0]
     name_line = name_line.split(':')[0] + ':'
 
@@ -56,7 +79,7 @@ def main(path, kname):
             r.add(int(m.group(1)))
         return r
 
-    asm_loads, asm_waits, asm_any = [], set(), set()
+    asm_loads, asm_waits, asm_any, unknown = [], set(), set(), []
     inside = False
     for k, l in enumerate(body):
         if ';;#ASMSTART' in l:
@@ -68,6 +91,9 @@ def main(path, kname):
         if inside:
             t = l.strip()
             asm_any.add(k)
+            if t and not t.startswith(';') and not t.startswith('.') and not t.startswith(KNOWN):
+                print(f"line {k}: unclassified inline-asm instruction: {t[:80]}")
+                unknown.append(k)
             if t.startswith('buffer_load') or t.startswith('global_load'):
                 asm_loads.append(k)
             if t.startswith('s_waitcnt') and 'vmcnt' in t:
@@ -75,7 +101,7 @@ def main(path, kname):
     regs = set()
     for k in asm_loads:
         regs |= regs_in(body[k].split(',')[0])
-    bad = 0
+    bad = len(unknown)
     for k0 in asm_loads:
         seen = set()
         stack = [(blk_of[k0], k0 + 1)]
@@ -130,10 +156,23 @@ def main(path, kname):
                 m = re.match(r's_nop\s+(\d+)', u)
                 waits += (int(m.group(1)) + 1) if m else 1
             q -= 1
-    print(f"{len(asm_loads)} asm loads, {len(asm_waits)} asm waits, registers {sorted(regs)}: "
-          f"{'OK' if not bad else str(bad) + ' VIOLATIONS'}")
+    print(f"{kname[:60]}: {len(asm_any)} asm lines, {len(asm_loads)} asm loads, {len(asm_waits)} asm waits, "
+          f"registers {sorted(regs)}: {'OK' if not bad else str(bad) + ' VIOLATIONS'}")
     return 1 if bad else 0
 
 
+def check_all(paths):
+    rc, n = 0, 0
+    for p in paths:
+        s = open(p).read()
+        for k in kernels_with_asm(s):
+            rc |= check(s, k)
+            n += 1
+    print(f"{n} functions with inline asm checked: {'OK' if rc == 0 else 'VIOLATIONS'}")
+    return rc
+
+
 if __name__ == '__main__':
+    if sys.argv[1] == '--all':
+        sys.exit(check_all(sys.argv[2:]))
     sys.exit(main(sys.argv[1], sys.argv[2]))

@@ -8,7 +8,8 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STRUCTS = {"lsmblk_builder": "LsmblkBuilder", "lsmblk_block": "LsmblkBlock", "lsmblk_iter": "LsmblkIter",
            "lsmblk_ctx": "LsmblkCtx", "lsmblk_kv_stream": "LsmblkKvStream", "lsmblk_compact_opts": "LsmblkCompactOpts",
-           "lsmblk_key_range": "LsmblkKeyRange", "lsmblk_memtable": "LsmblkMemtable"}
+           "lsmblk_key_range": "LsmblkKeyRange", "lsmblk_memtable": "LsmblkMemtable",
+           "lsmblk_kernel_stat": "LsmblkKernelStat"}
 SCALARS = {"int": "c_int", "uint32_t": "u32", "uint64_t": "u64", "size_t": "usize", "uint8_t": "u8",
            "uint16_t": "u16", "float": "f32", "char": "c_char", "void": "c_void", "int32_t": "i32"}
 

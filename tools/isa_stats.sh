@@ -1,6 +1,6 @@
 #!/bin/bash
 # Resource usage (VGPRs, LDS, spills) of the hot kernels from the gfx950 ISA of lsmblk_gpu.hip.
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I/root/repo/include --offload-device-only -S \
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I/root/repo/include -DLSMBLK_DIAG_BUILD=0 --offload-device-only -S \
   -o /tmp/lsmblk_gpu.s /root/repo/lsm_amd/csrc/lsmblk_gpu.hip 2>/dev/null || exit 1
 python3 - "$@" <<'PY'
 import re, sys

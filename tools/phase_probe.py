@@ -8,6 +8,9 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the ablation masks exist only in the diagnostics build
+os.environ.setdefault("LSMBLK_SO_OVERRIDE", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                         "lsm_amd", "liblsmblk_diag.so"))
 
 import torch  # noqa: E402
 
