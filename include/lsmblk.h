@@ -376,12 +376,30 @@ typedef struct {
 uint64_t lsmblk_shard_halo_entries(uint32_t block_size);
 
 /* lsmblk_compact_batch's merge + rules + gather, restricted to keys in *range (NULL: all keys;
- * opts->merge_mode must be LSMBLK_MERGE_RUNS):
+ * opts->merge_mode must be LSMBLK_MERGE_RUNS here; both modes: lsmblk_compact_merge_batch_ex):
  * kept receives this range's entries handed to SsTableBuilder::add.  stats: [0] kept entries [1] key
  * bytes [2] value bytes [3] error flags [4] merged entries.  Asynchronous. */
 int lsmblk_compact_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                                const lsmblk_compact_opts* opts, const lsmblk_key_range* range,
                                const lsmblk_kv_stream* kept, uint64_t* stats, void* stream);
+
+/* The same in either merge mode.  LSMBLK_MERGE_TWO_LEVEL (TwoMergeIterator as written, run nrun-1 = b):
+ * the stream ends at b's last key kb over the WHOLE compaction (two_merge_iterator.rs:32-42,60-66), so
+ * each range says where kb lies (the caller all-gathers every range's local b-run end):
+ *   LSMBLK_TWO_END_IN_RANGE  kb is in this range (or range is NULL): b's local last key is kb;
+ *   LSMBLK_TWO_END_ABOVE     the range lies wholly below kb: no cut-off in it;
+ *   LSMBLK_TWO_END_BELOW     kb lies below the range, or b is empty everywhere: no a-entry survives;
+ * and kept_same (device u8[kept->entry_cap]) receives every kept entry's same_as_last_key of the
+ * compact_generate_sst loop (src/compact.rs:279; with the two-level order it is not "same key as the
+ * previous kept entry"), which the rotation needs: lsmblk_shard_rotation_prepare_ex.  LSMBLK_MERGE_RUNS:
+ * two_end is ignored and kept_same may be NULL. */
+#define LSMBLK_TWO_END_IN_RANGE 0u
+#define LSMBLK_TWO_END_ABOVE 1u
+#define LSMBLK_TWO_END_BELOW 2u
+int lsmblk_compact_merge_batch_ex(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start,
+                                  uint32_t nrun, const lsmblk_compact_opts* opts, const lsmblk_key_range* range,
+                                  uint32_t two_end, const lsmblk_kv_stream* kept, uint8_t* kept_same, uint64_t* stats,
+                                  void* stream);
 
 /* Rotation state of one range over `ext` = its n_own kept entries followed by the halo (ext->n
  * entries in all).  flags: LSMBLK_SHARD_LAST when ext ends where the whole compaction's stream ends
@@ -391,6 +409,12 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, cons
 #define LSMBLK_SHARD_LAST 1u
 int lsmblk_shard_rotation_prepare(lsmblk_ctx* ctx, const lsmblk_kv_stream* ext, uint64_t n_own, uint32_t flags,
                                   uint32_t block_size, uint64_t target_sst_size, uint32_t sst_cap, void* stream);
+/* The same with ext_same (device u8[ext->n], two-level merges): every ext entry's same_as_last_key,
+ * the range's own from lsmblk_compact_merge_batch_ex's kept_same, the halo's from the ranks that
+ * own it.  NULL: "same key as the previous entry" (LSMBLK_MERGE_RUNS). */
+int lsmblk_shard_rotation_prepare_ex(lsmblk_ctx* ctx, const lsmblk_kv_stream* ext, const uint8_t* ext_same,
+                                     uint64_t n_own, uint32_t flags, uint32_t block_size, uint64_t target_sst_size,
+                                     uint32_t sst_cap, void* stream);
 
 /* carry_in (device u64[2]) -> carry_out (device u64[2]) for the next rank.  Asynchronous. */
 int lsmblk_shard_rotation_carry(lsmblk_ctx* ctx, const uint64_t* carry_in, uint64_t* carry_out, void* stream);

@@ -27,6 +27,9 @@ LSMBLK_DECODE_VERIFY_CRC = 1
 LSMBLK_SHARD_LAST = 1
 LSMBLK_MERGE_RUNS = 0
 LSMBLK_MERGE_TWO_LEVEL = 1
+LSMBLK_TWO_END_IN_RANGE = 0
+LSMBLK_TWO_END_ABOVE = 1
+LSMBLK_TWO_END_BELOW = 2
 
 
 class LsmBlkError(RuntimeError):
@@ -104,7 +107,10 @@ SIGNATURES = [
     ("lsmblk_shard_halo_entries", U64, [U32]),
     ("lsmblk_compact_merge_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
                                        ctypes.POINTER(KeyRangeC), ctypes.POINTER(KVStreamC), P, P]),
+    ("lsmblk_compact_merge_batch_ex", I, [P, ctypes.POINTER(KVStreamC), P, U32, ctypes.POINTER(CompactOptsC),
+                                          ctypes.POINTER(KeyRangeC), U32, ctypes.POINTER(KVStreamC), P, P, P]),
     ("lsmblk_shard_rotation_prepare", I, [P, ctypes.POINTER(KVStreamC), U64, U32, U32, U64, U32, P]),
+    ("lsmblk_shard_rotation_prepare_ex", I, [P, ctypes.POINTER(KVStreamC), P, U64, U32, U32, U64, U32, P]),
     ("lsmblk_shard_rotation_carry", I, [P, P, P, P]),
     ("lsmblk_shard_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U64, P, U64, P, P, U32, P, P]),
     ("lsmblk_memtable_new", P, []),

@@ -607,9 +607,11 @@ def key_range_c(lo, hi):
 
 
 def compact_merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: dict, key_range, kept: KVStream,
-                       stats, stream=None, ctx=None):
-    """Asynchronous lsmblk_compact_merge_batch: merge + rules restricted to key_range (a KeyRangeC
-    or None) into preallocated `kept`.  stats: int64[5] device."""
+                       stats, stream=None, ctx=None, two_end=0, kept_same=None):
+    """Asynchronous lsmblk_compact_merge_batch_ex: merge + rules restricted to key_range (a KeyRangeC
+    or None) into preallocated `kept`.  stats: int64[5] device.  Two-level merges (opts merge_mode):
+    two_end (LSMBLK_TWO_END_*) and kept_same (uint8 device tensor, the loop's same_as_last_key per
+    kept entry) as include/lsmblk.h describes."""
     dev = _dev_index(run_start)
     kv.check(dev, "kv")
     _need(run_start, torch.int32, "run_start", dev, nrun + 1)
@@ -617,19 +619,26 @@ def compact_merge_into(kv: KVStream, run_start: torch.Tensor, nrun: int, opts: d
     _need(stats, torch.int64, "stats", dev, 5)
     o = _opts_c(opts)
     ci, ck = kv._c(), kept._c(*kept.caps())
-    _native("lsmblk_compact_merge_batch", dev, stream, ctypes.byref(ci), run_start.data_ptr(), nrun,
-            ctypes.byref(o), ctypes.byref(key_range) if key_range is not None else None,
-            ctypes.byref(ck), stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_compact_merge_batch", own=ctx)
+    if kept_same is not None:
+        _need(kept_same, torch.uint8, "kept_same", dev, kept.caps()[0])
+    _native("lsmblk_compact_merge_batch_ex", dev, stream, ctypes.byref(ci), run_start.data_ptr(), nrun,
+            ctypes.byref(o), ctypes.byref(key_range) if key_range is not None else None, two_end,
+            ctypes.byref(ck), _ptr(kept_same), stats.data_ptr(), _stream_ptr(stream, dev),
+            what="lsmblk_compact_merge_batch_ex", own=ctx)
 
 
 def shard_prepare(ext: KVStream, n_own: int, last: bool, block_size: int, target_sst_size: int, sst_cap: int,
-                  stream=None, ctx=None):
+                  stream=None, ctx=None, ext_same=None):
+    """lsmblk_shard_rotation_prepare_ex; ext_same (uint8 device tensor, two-level merges): every ext
+    entry's same_as_last_key."""
     dev = _dev_index(ext.key_off)
     ext.check(dev, "ext")
+    if ext_same is not None:
+        _need(ext_same, torch.uint8, "ext_same", dev, ext.n)
     c = ext._c()
-    _native("lsmblk_shard_rotation_prepare", dev, stream, ctypes.byref(c), n_own,
+    _native("lsmblk_shard_rotation_prepare_ex", dev, stream, ctypes.byref(c), _ptr(ext_same), n_own,
             LSMBLK_SHARD_LAST if last else 0, block_size, target_sst_size, sst_cap,
-            _stream_ptr(stream, dev), what="lsmblk_shard_rotation_prepare", own=ctx)
+            _stream_ptr(stream, dev), what="lsmblk_shard_rotation_prepare_ex", own=ctx)
 
 
 def shard_carry(carry_in: torch.Tensor, carry_out: torch.Tensor, stream=None, ctx=None):

@@ -106,6 +106,7 @@ struct MergeArgs {
   uint32_t* perm;           // n: merged position -> input index
   uint64_t* mstats;         // [0] merged entries [1] candidates (tiles) [3] error flags
   uint32_t two;             // LSMBLK_MERGE_TWO_LEVEL: TwoMergeIterator(runs 0..nrun-2, run nrun-1)
+  uint32_t two_end;         // two-level, key-range shard: LSMBLK_TWO_END_* (where b's last key lies)
 };
 
 // LSMBLK_MERGE_TWO_LEVEL: the reference's compact() input, TwoMergeIterator(a = MergeIterator(upper
@@ -276,17 +277,22 @@ __device__ __forceinline__ int kcmp16(const MergeArgs& a, const GKeys& G, const 
   return key_cmp(G, a.key_off[xg] + 16, xl - 16, a.key_off[yg] + 16, yl - 16);
 }
 
-// Two-level mode: b's last key, where the reference's stream ends.
+// Two-level mode: b's last key, where the reference's stream ends.  In a key-range shard
+// (lsmblk_compact_merge_batch_ex) the end is that of the WHOLE compaction's b: in this range
+// (b's local last key, as for the whole stream), above it (no cut-off here: inf), or below it /
+// b empty (nothing of a survives: !nonempty).
 struct TwoEnd {
   u32x4 k16;
   uint32_t len, g, pos;
-  bool nonempty;
+  bool nonempty, inf;
 };
 __device__ __forceinline__ TwoEnd two_end(const MergeArgs& a, const GKeys& G) {
   TwoEnd t{};
   const uint32_t e0 = a.run_start[a.nrun - 1], e1 = a.run_start[a.nrun];
-  t.nonempty = e1 > e0;
-  if (t.nonempty) {
+  t.nonempty = e1 > e0 && a.two_end != LSMBLK_TWO_END_BELOW;
+  t.inf = a.two_end == LSMBLK_TWO_END_ABOVE;
+  if (a.two_end == LSMBLK_TWO_END_ABOVE) t.nonempty = true;  // b's keys lie beyond this range
+  if (t.nonempty && !t.inf) {
     t.g = e1 - 1;
     t.pos = a.key_off[t.g];
     t.len = a.key_off[t.g + 1] - t.pos;
@@ -335,7 +341,7 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
     uint32_t sv = !held;
     if (a.two) {
       if (r == B) sv = held ? ((u - H.tb[B]) - bound(B, x, xl, g, false)) & 1u : 1u;  // skip_b
-      else sv = sv && te.nonempty && kcmp16(a, G, x, xl, g, te.k16, te.len, te.g) < 0;
+      else sv = sv && te.nonempty && (te.inf || kcmp16(a, G, x, xl, g, te.k16, te.len, te.g) < 0);
     }
     L.surv[u] = uint8_t(sv);
   }
@@ -432,7 +438,7 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
     uint32_t sv = !held;
     if (a.two) {
       if (r == B) sv = held ? (k - bound(B, xp, xl, false)) & 1u : 1u;  // skip_b
-      else sv = sv && te.nonempty && key_cmp(G, xp, xl, te.pos, te.len) < 0;
+      else sv = sv && te.nonempty && (te.inf || key_cmp(G, xp, xl, te.pos, te.len) < 0);
     }
     stv(a.mrank + H.lo[r] + k, sv);
   }
@@ -1527,7 +1533,8 @@ int ensure_ws(lsmblk_ctx* c, uint64_t bytes) {
 int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                         uint32_t rules, uint64_t wm, int bottom, const uint8_t* pfx, const uint32_t* pfx_off,
                         uint32_t npfx, const lsmblk_key_range* range, const lsmblk_kv_stream* out, uint64_t* stats,
-                        hipStream_t st, MergePlan* plan_out, uint32_t two) {
+                        hipStream_t st, MergePlan* plan_out, uint32_t two, uint32_t two_end = LSMBLK_TWO_END_IN_RANGE,
+                        uint8_t* ksame_out = nullptr) {
   const uint64_t n = in->n;
   MergePlan P = plan_merge(nullptr, n, nrun);
   int rc = ensure_ws(c, P.bytes);
@@ -1541,6 +1548,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   m.run_start = run_start;
   m.nrun = nrun;
   m.two = two;
+  m.two_end = two_end;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (n == 0) {
     LSM_LAUNCH(merge_empty_kernel, dim3(1), dim3(64), 0, st, m.mstats, out->key_off, out->val_off,
@@ -1586,7 +1594,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   g.merr = m.mstats + 3;
   g.range = range ? *range : lsmblk_key_range{};
   g.two = two;
-  g.ksame = two && rules ? P.ksame : nullptr;
+  g.ksame = two && rules ? (ksame_out ? ksame_out : P.ksame) : nullptr;
   const uint32_t gt = uint32_t((n + kGTile - 1) / kGTile);
   if (two && rules) LSM_LAUNCH(mgroup_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, g);
   LSM_LAUNCH(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
@@ -1759,10 +1767,20 @@ uint64_t lsmblk_shard_halo_entries(uint32_t block_size) { return uint64_t(block_
 int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                                const lsmblk_compact_opts* o, const lsmblk_key_range* range,
                                const lsmblk_kv_stream* kept, uint64_t* stats, void* stream) {
+  if (o && o->merge_mode != LSMBLK_MERGE_RUNS) return LSMBLK_E_INVAL;  // two-level: the _ex form
+  return lsmblk_compact_merge_batch_ex(c, in, run_start, nrun, o, range, LSMBLK_TWO_END_IN_RANGE, kept, nullptr, stats,
+                                       stream);
+}
+
+int lsmblk_compact_merge_batch_ex(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
+                                  const lsmblk_compact_opts* o, const lsmblk_key_range* range, uint32_t two_end,
+                                  const lsmblk_kv_stream* kept, uint8_t* kept_same, uint64_t* stats, void* stream) {
   int rc = check_merge_args(c, in, run_start, nrun, kept, stats);
   if (rc) return rc;
   if (!o || (o->nprefix && (!o->prefixes || !o->prefix_off))) return LSMBLK_E_INVAL;
-  if (o->merge_mode != LSMBLK_MERGE_RUNS) return LSMBLK_E_INVAL;  // key ranges: run-priority merge only
+  if (o->merge_mode != LSMBLK_MERGE_RUNS && o->merge_mode != LSMBLK_MERGE_TWO_LEVEL) return LSMBLK_E_INVAL;
+  const uint32_t two = o->merge_mode == LSMBLK_MERGE_TWO_LEVEL;
+  if (two_end > LSMBLK_TWO_END_BELOW || (two && !kept_same)) return LSMBLK_E_INVAL;
   if (range && ((range->has_lo && range->lo_len && !range->lo) || (range->has_hi && range->hi_len && !range->hi)))
     return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1772,7 +1790,7 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const 
   if (hipMemsetAsync(stats + 4, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
   MergePlan MP{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
-                                o->nprefix, range, kept, stats, st, &MP, 0)))
+                                o->nprefix, range, kept, stats, st, &MP, two, two_end, two ? kept_same : nullptr)))
     return rc;
   if (in->n) LSM_LAUNCH(copy_u64_kernel, dim3(1), dim3(64), 0, st, stats + 4, MP.m.mstats);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
@@ -1780,6 +1798,12 @@ int lsmblk_compact_merge_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const 
 
 int lsmblk_shard_rotation_prepare(lsmblk_ctx* c, const lsmblk_kv_stream* ext, uint64_t n_own, uint32_t flags,
                                   uint32_t block_size, uint64_t target_sst_size, uint32_t sst_cap, void* stream) {
+  return lsmblk_shard_rotation_prepare_ex(c, ext, nullptr, n_own, flags, block_size, target_sst_size, sst_cap, stream);
+}
+
+int lsmblk_shard_rotation_prepare_ex(lsmblk_ctx* c, const lsmblk_kv_stream* ext, const uint8_t* ext_same, uint64_t n_own,
+                                     uint32_t flags, uint32_t block_size, uint64_t target_sst_size, uint32_t sst_cap,
+                                     void* stream) {
   if (!c || !ext || !ext->key_off || !ext->val_off) return LSMBLK_E_INVAL;
   if (block_size == 0 || target_sst_size == 0 || sst_cap == 0 || n_own > ext->n || ext->n >= 0xFFFFFFF0ull)
     return LSMBLK_E_INVAL;
@@ -1798,7 +1822,8 @@ int lsmblk_shard_rotation_prepare(lsmblk_ctx* c, const lsmblk_kv_stream* ext, ui
   c->shard_block_size = block_size;
   c->shard_flags = flags;
   c->shard_sst_cap = sst_cap;
-  const RotArgs r = shard_args(c, ext);
+  RotArgs r = shard_args(c, ext);
+  r.ksame = ext_same;  // two-level: the loop's same_as_last_key (baked into alcp by rot_adj)
   LSM_LAUNCH(set_u64_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(r.dn), uint64_t(ext->n));
   if ((rc = rotation_chains(r, st))) return rc;
   const uint32_t gr = uint32_t((ext->n + 1 + 255) / 256);

@@ -32,7 +32,8 @@ import torch
 import torch.distributed as dist
 
 from . import batch
-from ._lib import LsmBlkError, lib
+from ._lib import (LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LSMBLK_TWO_END_ABOVE, LSMBLK_TWO_END_BELOW,
+                   LSMBLK_TWO_END_IN_RANGE, LsmBlkError, lib)
 
 
 def block_ranges(nblk: int, world: int):
@@ -136,10 +137,12 @@ def halo_entries(block_size: int) -> int:
 
 class Head:
     """The first h <= W kept entries of a range (of n in all): relative offsets int64[h+1], ts
-    int64[h], key / value bytes -- tensors on the exchange's device."""
+    int64[h], key / value bytes, and (two-level merges) the loop's same_as_last_key uint8[h] --
+    tensors on the exchange's device."""
 
-    def __init__(self, n, ko, vo, ts, keys, vals):
+    def __init__(self, n, ko, vo, ts, keys, vals, ks=None):
         self.n, self.ko, self.vo, self.ts, self.keys, self.vals = n, ko, vo, ts, keys, vals
+        self.ks = ks if ks is not None else torch.zeros(ts.numel(), dtype=torch.uint8, device=ts.device)
 
     @property
     def h(self):
@@ -147,13 +150,14 @@ class Head:
 
     def to(self, device):
         return Head(self.n, self.ko.to(device), self.vo.to(device), self.ts.to(device), self.keys.to(device),
-                    self.vals.to(device))
+                    self.vals.to(device), self.ks.to(device))
 
 
 def assemble_halo(heads, g: int, W: int):
     """Rank g's halo: the first W entries after its range, from the heads of the ranks after it
     (a short range contributes all of its entries and the next one continues).  Returns (keys,
-    ko, vals, vo, ts, last): `last` when the halo reaches the end of the whole stream."""
+    ko, vals, vo, ts, last, ks): `last` when the halo reaches the end of the whole stream, ks the
+    entries' same_as_last_key (two-level merges)."""
     need, parts, taken, remaining = W, [], 0, sum(h.n for h in heads[g + 1:])
     for hd in heads[g + 1:]:
         if need == 0:
@@ -175,7 +179,18 @@ def assemble_halo(heads, g: int, W: int):
         vbase += int(hd.vo[t])
     cat = (lambda xs, dt: torch.cat(xs) if xs else torch.zeros(0, dtype=dt, device=dev))
     return (cat(kb, torch.uint8), torch.cat(ko), cat(vb, torch.uint8), torch.cat(vo),
-            cat([hd.ts[:t] for hd, t in parts], torch.int64), taken == remaining)
+            cat([hd.ts[:t] for hd, t in parts], torch.int64), taken == remaining,
+            cat([hd.ks[:t] for hd, t in parts], torch.uint8))
+
+
+def two_end_mode(kb, lo, hi):
+    """Where b's last key kb (None: b empty everywhere) lies relative to the range [lo, hi): the
+    LSMBLK_TWO_END_* of lsmblk_compact_merge_batch_ex (two-level merges)."""
+    if kb is None or (lo is not None and kb < lo):
+        return LSMBLK_TWO_END_BELOW
+    if hi is not None and kb >= hi:
+        return LSMBLK_TWO_END_ABOVE
+    return LSMBLK_TWO_END_IN_RANGE
 
 
 def _u32_as_i32(x: torch.Tensor) -> torch.Tensor:
@@ -198,6 +213,9 @@ class RangeShard:
         self.kv, self.opts = kv, opts
         self.stream = stream if stream is not None else torch.cuda.current_stream(self.dev)
         self.ctx = batch.OwnCtx(self.dev.index)
+        self.two = opts.get("merge_mode", LSMBLK_MERGE_RUNS) == LSMBLK_MERGE_TWO_LEVEL
+        self.lo, self.hi = (bytes(lo) if lo is not None else None), (bytes(hi) if hi is not None else None)
+        self.two_end = LSMBLK_TWO_END_IN_RANGE  # two-level: set from the whole compaction's b end (set_b_end)
         self.rs = batch._u32_table(run_start, self.dev)
         self.nrun = self.rs.numel() - 1
         self.bs, self.target = opts["block_size"], opts["target_sst_size"]
@@ -220,14 +238,30 @@ class RangeShard:
         return torch.frombuffer(bytearray(bytes(b) or b"\0"), dtype=torch.uint8)[:len(b)].to(self.dev)
 
     def _grow_kept(self, n, kb, vb, keep=0):
-        old = self.kept
+        old, old_ks = self.kept, getattr(self, "ks", None)
         self.kept = batch.KVStream.empty(n, kb, vb, self.dev)
+        self.ks = torch.zeros(n + 1, dtype=torch.uint8, device=self.dev)  # same_as_last_key (two-level)
+        if old_ks is not None and keep:
+            self.ks[:keep].copy_(old_ks[:keep])
         if old is not None and keep:  # the first `keep` entries survive a regrow
             self.kept.keys[:self.Kk].copy_(old.keys[:self.Kk])
             self.kept.vals[:self.Vk].copy_(old.vals[:self.Vk])
             self.kept.key_off[:keep + 1].copy_(old.key_off[:keep + 1])
             self.kept.val_off[:keep + 1].copy_(old.val_off[:keep + 1])
             self.kept.ts[:keep].copy_(old.ts[:keep])
+
+    # -- phase 0 (two-level merges): where the whole compaction's b ends
+    def b_end(self):
+        """The last key of this range's input b run (run nrun - 1), or None if it holds none: the
+        maximum over the ranges is b's last key over the whole compaction."""
+        a, b = int(self.rs[self.nrun - 1].item()) & 0xFFFFFFFF, int(self.rs[self.nrun].item()) & 0xFFFFFFFF
+        if b <= a:
+            return None
+        k0, k1 = [int(x) & 0xFFFFFFFF for x in self.kv.key_off[b - 1:b + 1].cpu().tolist()]
+        return bytes(self.kv.keys[k0:k1].cpu().numpy())
+
+    def set_b_end(self, kb):
+        self.two_end = two_end_mode(kb, self.lo, self.hi)
 
     # -- phase 1: merge + rules + range
     def merge(self):
@@ -238,7 +272,7 @@ class RangeShard:
         k = self.kept
         k.n = 0
         batch.compact_merge_into(self.kv, self.rs, self.nrun, self.opts, self.range_c, k, self.mstats, self.stream,
-                                 ctx=self.ctx)
+                                 ctx=self.ctx, two_end=self.two_end, kept_same=self.ks if self.two else None)
         torch.cuda.synchronize(self.dev)
         s = self.mstats.cpu().tolist()
         st = lib().lsmblk_stats_status(s[3] & 0xFFFFFFFFFFFFFFFF)
@@ -260,15 +294,16 @@ class RangeShard:
         ko = self.kept.key_off[:h + 1].to(torch.int64) & 0xFFFFFFFF
         vo = self.kept.val_off[:h + 1].to(torch.int64) & 0xFFFFFFFF
         kb, vb = (int(ko[h]), int(vo[h])) if h else (0, 0)
-        return Head(self.m, ko, vo, self.kept.ts[:h].clone(), self.kept.keys[:kb].clone(), self.kept.vals[:vb].clone())
+        return Head(self.m, ko, vo, self.kept.ts[:h].clone(), self.kept.keys[:kb].clone(), self.kept.vals[:vb].clone(),
+                    self.ks[:h].clone())
 
-    def set_halo(self, keys, ko, vals, vo, ts, last: bool):
+    def set_halo(self, keys, ko, vals, vo, ts, last: bool, ks=None):
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))  # the halo was assembled there
         with torch.cuda.stream(self.stream):
-            self._set_halo(keys, ko, vals, vo, ts, last)
+            self._set_halo(keys, ko, vals, vo, ts, last, ks)
         self.stream.synchronize()  # the halo tensors may be freed by the caller right after
 
-    def _set_halo(self, keys, ko, vals, vo, ts, last: bool):
+    def _set_halo(self, keys, ko, vals, vo, ts, last: bool, ks=None):
         m, h = self.m, ts.numel()
         Kh, Vh = keys.numel(), vals.numel()
         ecap, kcap, vcap = self.kept.caps()
@@ -283,6 +318,8 @@ class RangeShard:
             k.key_off[m + 1:m + 1 + h].copy_(_u32_as_i32(ko[1:].to(self.dev) + self.Kk))
             k.val_off[m + 1:m + 1 + h].copy_(_u32_as_i32(vo[1:].to(self.dev) + self.Vk))
             k.ts[m:m + h].copy_(ts.to(self.dev))
+            if ks is not None:
+                self.ks[m:m + h].copy_(ks.to(self.dev))
         self.h, self.Kh, self.Vh, self.last = h, Kh, Vh, bool(last)
         self.ext = batch.KVStream(k.keys, k.key_off, k.vals, k.val_off, k.ts, m + h)
 
@@ -290,7 +327,8 @@ class RangeShard:
     def prepare(self):
         n = self.m + self.h
         self.sst_cap = (self.Kk + self.Vk + self.Kh + self.Vh + 22 * n) // self.target + 3
-        batch.shard_prepare(self.ext, self.m, self.last, self.bs, self.target, self.sst_cap, self.stream, ctx=self.ctx)
+        batch.shard_prepare(self.ext, self.m, self.last, self.bs, self.target, self.sst_cap, self.stream, ctx=self.ctx,
+                            ext_same=self.ks if self.two else None)
 
     # -- phase 4: carry
     def carry(self, carry_in: torch.Tensor) -> torch.Tensor:
@@ -351,11 +389,16 @@ def sst_starts(results, bases):
 def compact_local(shards):
     """Every range of the compaction in this process (in key order), e.g. several ranges on one
     GPU: the same phases and messages as compact_dist, passed in memory."""
+    if shards and shards[0].two:  # two-level: b's last key over the whole compaction
+        ends = [e for e in (s.b_end() for s in shards) if e is not None]
+        for s in shards:
+            s.set_b_end(max(ends) if ends else None)
     for s in shards:
         s.merge()
     heads = [s.head() for s in shards]
     for g, s in enumerate(shards):
-        s.set_halo(*assemble_halo(heads, g, s.W))
+        h = assemble_halo(heads, g, s.W)
+        s.set_halo(*h[:6], ks=h[6])
     for s in shards:
         s.prepare()
     c = torch.zeros(2, dtype=torch.int64, device=shards[0].dev) if shards else None
@@ -386,17 +429,42 @@ def _allgather_heads(head: Head, group=None):
         return out
     buf = torch.cat([pad(head.ko, H + 1).view(torch.uint8), pad(head.vo, H + 1).view(torch.uint8),
                      pad(head.ts, max(H, 1)).view(torch.uint8), pad(head.keys, max(KB, 1)),
-                     pad(head.vals, max(VB, 1))])
+                     pad(head.vals, max(VB, 1)), pad(head.ks, max(H, 1))])
     bufs = [torch.zeros_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf, group=group)
     heads = []
     o1 = 8 * (H + 1)
     o2, o3 = 2 * o1, 2 * o1 + 8 * max(H, 1)
     o4 = o3 + max(KB, 1)
+    o5 = o4 + max(VB, 1)
     for (n, h, kb, vb), b in zip(metas, bufs):
         heads.append(Head(n, b[:o1].view(torch.int64)[:h + 1], b[o1:o2].view(torch.int64)[:h + 1],
-                          b[o2:o3].view(torch.int64)[:h], b[o3:o3 + kb], b[o4:o4 + vb]))
+                          b[o2:o3].view(torch.int64)[:h], b[o3:o3 + kb], b[o4:o4 + vb], b[o5:o5 + h]))
     return heads
+
+
+def _allgather_bytes(items, cdev, group=None):
+    """All-gather every rank's list of byte strings (or None), in rank order: lengths, then one
+    padded byte buffer (exact keys, unlike the sampled splitter exchange)."""
+    world = dist.get_world_size(group)
+    lens = torch.tensor([-1 if x is None else len(x) for x in items], dtype=torch.int64, device=cdev)
+    all_lens = [torch.zeros_like(lens) for _ in range(world)]
+    dist.all_gather(all_lens, lens, group=group)
+    all_lens = [x.cpu().tolist() for x in all_lens]
+    L = max([max(0, v) for ls in all_lens for v in ls] + [1])
+    buf = torch.zeros(len(items) * L, dtype=torch.uint8)
+    for i, x in enumerate(items):
+        if x:
+            buf[i * L:i * L + len(x)] = torch.frombuffer(bytearray(x), dtype=torch.uint8)
+    buf = buf.to(cdev)
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
+    out = []
+    for ls, b in zip(all_lens, bufs):
+        b = b.cpu()
+        for i, v in enumerate(ls):
+            out.append(None if v < 0 else bytes(b[i * L:i * L + v].numpy()))
+    return out
 
 
 def compact_dist(shard, group=None):
@@ -424,6 +492,10 @@ def _compact_dist(shards, group):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     R = len(shards)
     cdev = comm_device(shards[0].dev, group)
+    if getattr(shards[0], "two", False):  # two-level: b's last key over the whole compaction
+        ends = [e for e in _allgather_bytes([s.b_end() for s in shards], cdev, group) if e is not None]
+        for s in shards:
+            s.set_b_end(max(ends) if ends else None)
     for s in shards:
         s.merge()
     # one all-gather per local range index: heads[r * R + i] = rank r's range i
@@ -431,7 +503,7 @@ def _compact_dist(shards, group):
     heads = [per[i][r] for r in range(world) for i in range(R)]
     for i, s in enumerate(shards):
         halo = assemble_halo(heads, rank * R + i, s.W)
-        s.set_halo(*[x.to(s.dev) for x in halo[:5]], halo[5])
+        s.set_halo(*[x.to(s.dev) for x in halo[:5]], halo[5], ks=halo[6].to(s.dev))
         s.prepare()
     cin = torch.zeros(2, dtype=torch.int64, device=cdev)
     if rank > 0:

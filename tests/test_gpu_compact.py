@@ -213,15 +213,28 @@ def test_two_level_synthetic_and_big_tiles():
     assert gpu_merge_mode(big, LSMBLK_MERGE_RUNS) == pyref.merge_runs_rule(big)
 
 
-def test_two_level_mode_rejected_for_key_ranges():
+def test_two_level_key_range_argument_errors():
+    """Key ranges take the two-level merge through lsmblk_compact_merge_batch_ex only, with the
+    kept entries' same_as_last_key output and a valid b-end mode (tests/test_gpu_shard.py runs it)."""
+    from lsm_amd._lib import lib
     kv, rs = kv_runs([kvs([("a", "1")]), kvs([("b", "2")])])
     d = to_dev(kv)
     opts = batch.compact_opts(0, False, (), 4096, 1 << 20, merge_mode=TWO)
     kept = batch.KVStream.empty(d.n, 16, 16, torch.device("cuda"))
     stats = torch.zeros(5, dtype=torch.int64, device="cuda")
-    with pytest.raises(LsmBlkError) as e:
-        batch.compact_merge_into(d, batch._u32_table(rs, "cuda"), 2, opts, None, kept, stats)
+    rs_t = batch._u32_table(rs, "cuda")
+    with pytest.raises(LsmBlkError) as e:  # no kept_same
+        batch.compact_merge_into(d, rs_t, 2, opts, None, kept, stats)
     assert e.value.status == LSMBLK_E_INVAL
+    ks = torch.zeros(d.n + 1, dtype=torch.uint8, device="cuda")
+    with pytest.raises(LsmBlkError) as e:  # no such b-end mode
+        batch.compact_merge_into(d, rs_t, 2, opts, None, kept, stats, two_end=3, kept_same=ks)
+    assert e.value.status == LSMBLK_E_INVAL
+    import ctypes
+    ci, ck, o = d._c(), kept._c(*kept.caps()), batch._opts_c(opts)
+    assert lib().lsmblk_compact_merge_batch(batch._ctx(0), ctypes.byref(ci), rs_t.data_ptr(), 2, ctypes.byref(o),
+                                            None, ctypes.byref(ck), stats.data_ptr(), None) == LSMBLK_E_INVAL
+    torch.cuda.synchronize()
 
 
 # ---------------------------------------------------------------- SST rotation
@@ -242,22 +255,22 @@ def test_sst_rotation_vs_restated_loop(bs, target):
 
 @pytest.mark.parametrize("versions", [1, 3])
 def test_sst_rotation_large_capacity_long_chain(versions):
-    """A capacity far above the SST count's (n + 2 = 2^18: more than 2^17, so every doubling level
-    runs and no walk / fill does) with a long chain (target 1: an SST at every key change, ~10^5):
-    bit-exact, and bounded in time -- the fill's serial loads never grow with the capacity (ADVICE
-    round 3: K = lc - 9 made each fill thread follow ~sst_cap / 512 elements)."""
+    """A capacity far above 2^17 (n + 2 ~ 2^18, so every doubling level runs and no walk / fill
+    does) with a long chain (64-B blocks and target 1: one entry per block and an SST at every key
+    change, 10^4 - 10^5 of them): bit-exact, and bounded in time -- the fill's serial loads never grow
+    with the capacity (K = lc - 9 made each fill thread follow ~sst_cap / 512 elements)."""
     import time
     keys, ko, vals, vo, ts, rs = synth.gen_runs(200000 // versions, nrun=2, seed=17, versions=versions)
     kv = O.KV(keys, ko, vals, vo, ts)
     kept = O.gather(kv, O.merge_runs(kv, rs))
-    want = O.segment_like_compaction(kept, 4096, 1)
+    want = O.segment_like_compaction(kept, 64, 1)
     d = to_dev(kept)
-    batch.sst_rotation(d, 4096, 1)
+    batch.sst_rotation(d, 64, 1)
     t0 = time.perf_counter()
-    got = batch.sst_rotation(d, 4096, 1)
+    got = batch.sst_rotation(d, 64, 1)
     dt = time.perf_counter() - t0
     np.testing.assert_array_equal(got, want)
-    assert len(want) > 50000 and dt < 0.5, (len(want), dt)
+    assert kept.n + 2 > (1 << 17) and len(want) > 20000 and dt < 0.5, (kept.n, len(want), dt)
 
 
 def test_sst_rotation_unsorted_and_long_keys():

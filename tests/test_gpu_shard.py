@@ -197,3 +197,70 @@ def test_ranges_on_distinct_streams_compact_dist_single_rank():
         check_against_single_stream(kv, rs, res, 0, False, bs, target)
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- two-level merge (TwoMergeIterator) by key range
+from lsm_amd._lib import LSMBLK_MERGE_TWO_LEVEL as TWO  # noqa: E402
+
+
+def two_level_input(seed, nkeys, b_frac, versions=3):
+    """Multi-version upper runs and a lower level b (the last run) that ends b_frac of the way
+    through the key space (0: b empty): upper keys beyond b's last key are lost by the reference's
+    TwoMergeIterator, and ranges above that key get nothing of a."""
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(nkeys, nrun=4, seed=seed, versions=versions, tombstone=0.1)
+    kv = O.KV(keys, ko, vals, vo, ts)
+    ents = kv.entries()
+    runs = [ents[rs[r]:rs[r + 1]] for r in range(4)]
+    runs[-1] = runs[-1][:int(len(runs[-1]) * b_frac)]
+    flat = [e for r in runs for e in r]
+    rs2 = np.concatenate([[0], np.cumsum([len(r) for r in runs])]).astype(np.uint32)
+    return O.KV.from_entries(flat), rs2
+
+
+@pytest.mark.parametrize("seed,b_frac,bottom", [(0, 0.6, True), (1, 1.0, False), (2, 0.25, True), (3, 0.0, False)])
+def test_two_level_sharded_compaction_equals_single_stream(seed, b_frac, bottom):
+    """LSMBLK_MERGE_TWO_LEVEL by key range (lsmblk_compact_merge_batch_ex + the kept entries'
+    same_as_last_key carried through the halo into lsmblk_shard_rotation_prepare_ex): the ranges'
+    blocks and SST starts equal the single-stream two-level compaction (lsmblk_compact_batch, which
+    tests/test_gpu_compact.py pins to the line-by-line iterator) -- splitters below, at and above b's
+    last key, ranges wholly past it, and an empty b."""
+    rng = np.random.default_rng(70 + seed)
+    kv, rs = two_level_input(500 + seed, 5000, b_frac)
+    d = to_dev(kv)
+    bs, target = [(4096, 24 << 10), (1024, 6 << 10), (512, 3000), (4096, 1 << 20)][seed]
+    wm = int(kv.ts.max()) // 2
+    single = batch.compact_runs(d, rs, wm, bottom, block_size=bs, target_sst_size=target, merge_mode=TWO)
+    want_blocks = single["blocks"].cpu().numpy().tobytes()
+    want_starts = single["sst_start"].cpu().numpy().view(np.uint32).astype(np.int64)[:-1].tolist()
+    opts = batch.compact_opts(wm, bottom, block_size=bs, target_sst_size=target, merge_mode=TWO)
+    b_last = kv.entry(int(rs[-1]) - 1)[0] if rs[-1] > rs[-2] else None
+    for k in (1, 4, 9):
+        sp = pick_splitters(kv, rng, k)
+        if b_last is not None:
+            sp = sorted(set(sp) | {b_last})  # a range starting exactly at b's last key
+        res, _ = run_ranges(d, rs, opts, sp)
+        assert b"".join(r["blocks"].cpu().numpy().tobytes() for r in res) == want_blocks
+        bases = np.concatenate([[0], np.cumsum([r["m"] for r in res])]).tolist()
+        assert bases[-1] == single["stats"][5]
+        assert shard.sst_starts(res, bases) == want_starts
+        for a, b in zip(res, res[1:]):
+            assert a["carry_out"] == b["carry_in"]
+    if b_frac == 0.0:
+        assert want_blocks == b""
+
+
+def test_two_level_sharded_small_vs_iterator():
+    """A small two-level case through the ranges against compact_generate_sst over the reference's
+    TwoMergeIterator restated line by line (oracle/pyref.py): b's second, fourth, ... versions of a
+    shared key, upper keys past b's end dropped, a tombstone at the bottom level."""
+    from oracle import pyref
+    a = [(b"a", 9, b"A9"), (b"c", 8, b"C8"), (b"k", 9, b"K9"), (b"m", 7, b""), (b"x", 6, b"X6"), (b"z", 5, b"Z5")]
+    b = [(b"c", 5, b"c5"), (b"c", 4, b"c4"), (b"c", 3, b"c3"), (b"k", 2, b"k2"), (b"m", 1, b"m1"), (b"q", 1, b"q1")]
+    runs = [a, b]
+    want = pyref.compact_generate_sst(pyref.two_merge_iter(runs), 0, True, (), 64, 100)
+    kv = O.KV.from_entries(a + b)
+    rs = np.array([0, len(a), len(a) + len(b)], np.uint32)
+    opts = batch.compact_opts(0, True, block_size=64, target_sst_size=100, merge_mode=TWO)
+    for sp in ([b"d"], [b"k", b"q"], [b"m\x00", b"r"], [b"q"]):
+        res, _ = run_ranges(to_dev(kv), rs, opts, sp)
+        assert b"".join(r["blocks"].cpu().numpy().tobytes() for r in res) == b"".join(blk for sst, _ in want for blk in sst)

@@ -55,7 +55,7 @@ class OracleShard:
                           t(k.ts[:h].view(np.int64), np.int64), t(k.keys[:k.key_off[h]], np.uint8),
                           t(k.vals[:k.val_off[h]], np.uint8))
 
-    def set_halo(self, keys, ko, vals, vo, ts, last):
+    def set_halo(self, keys, ko, vals, vo, ts, last, ks=None):
         O, k = self.O, self.kept
         self.ext = O.KV(np.concatenate([k.keys[:k.key_off[-1]], keys.numpy()]),
                         np.concatenate([k.key_off, ko.numpy()[1:] + k.key_off[-1]]).astype(np.uint32),
@@ -136,18 +136,32 @@ def test_gloo_sharded_compaction_equals_single_stream(world, R):
 
 
 def test_assemble_halo_spans_short_ranges():
-    """A range shorter than the halo contributes all its entries and the next range continues."""
+    """A range shorter than the halo contributes all its entries and the next range continues;
+    the entries' same_as_last_key bytes (two-level merges) travel with them."""
     def head(n, h, base):
         return shard.Head(n, torch.arange(h + 1, dtype=torch.int64) * 2, torch.arange(h + 1, dtype=torch.int64),
                           torch.arange(base, base + h, dtype=torch.int64),
-                          torch.arange(2 * h, dtype=torch.uint8), torch.arange(h, dtype=torch.uint8))
+                          torch.arange(2 * h, dtype=torch.uint8), torch.arange(h, dtype=torch.uint8),
+                          (torch.arange(h, dtype=torch.uint8) + base // 100) % 2)
     heads = [head(100, 5, 0), head(2, 2, 100), head(0, 0, 200), head(50, 5, 300)]
-    keys, ko, vals, vo, ts, last = shard.assemble_halo(heads, 0, 5)
+    keys, ko, vals, vo, ts, last, ks = shard.assemble_halo(heads, 0, 5)
     assert ts.tolist() == [100, 101, 300, 301, 302] and not last
     assert ko.tolist() == [0, 2, 4, 6, 8, 10] and keys.numel() == 10 and vals.numel() == 5
-    keys, ko, vals, vo, ts, last = shard.assemble_halo(heads, 1, 5)
+    assert ks.tolist() == [1, 0, 1, 0, 1]
+    keys, ko, vals, vo, ts, last, ks = shard.assemble_halo(heads, 1, 5)
     assert ts.tolist() == [300, 301, 302, 303, 304] and not last
-    assert shard.assemble_halo(heads, 3, 5)[-1] is True           # the last range
+    assert shard.assemble_halo(heads, 3, 5)[5] is True           # the last range
     heads[3] = head(3, 3, 300)
     assert shard.assemble_halo(heads, 0, 9)[4].tolist() == [100, 101, 300, 301, 302]
-    assert shard.assemble_halo(heads, 0, 9)[-1] is True           # the halo reached the stream's end
+    assert shard.assemble_halo(heads, 0, 9)[5] is True           # the halo reached the stream's end
+
+
+def test_two_end_mode():
+    """Where b's last key lies relative to a range (two-level merges, include/lsmblk.h)."""
+    from lsm_amd._lib import LSMBLK_TWO_END_ABOVE as A, LSMBLK_TWO_END_BELOW as B, LSMBLK_TWO_END_IN_RANGE as I
+    assert shard.two_end_mode(None, None, None) == B                 # b empty everywhere
+    assert shard.two_end_mode(b"m", None, None) == I
+    assert shard.two_end_mode(b"m", b"a", b"m") == A                 # hi exclusive: kb above the range
+    assert shard.two_end_mode(b"m", b"m", b"z") == I
+    assert shard.two_end_mode(b"m", b"m\x00", None) == B
+    assert shard.two_end_mode(b"m", None, b"c") == A
