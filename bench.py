@@ -806,7 +806,7 @@ def dry_run(args, rank, world, local):
 # ---------------------------------------------------------------------------------------------
 def main():
     args = parse()
-    if args.ablate is not None:  # ablation masks exist only in the diagnostics build (lsm_amd/_build.py)
+    if args.ablate is not None or args.trace_plan:  # ablation masks and traces: the diagnostics build only
         from lsm_amd import _build
         os.environ.setdefault("LSMBLK_SO_OVERRIDE", _build.DIAG_SO)
     if "RANK" not in os.environ and args.gpus > 1:

@@ -33,14 +33,17 @@
 
 namespace {
 
-constexpr uint32_t kMS = 128;  // every kMS-th entry of a run is a merge candidate
+#ifndef LSMBLK_MERGE_SPACING
+#define LSMBLK_MERGE_SPACING 128
+#endif
+constexpr uint32_t kMS = LSMBLK_MERGE_SPACING;  // every kMS-th entry of a run is a merge candidate
 constexpr uint32_t kMaxRuns = 64;   // runs per merge (one lane per run in the tile kernels)
 // Tile entries with LDS tables (larger tiles: the one-wave global path).  Tile sizes are about
 // exponential with mean kMS (the gaps between consecutive candidates of all runs), so the limit
 // trades the global path's share against residency: merge_tile on config C took 5.3 / 3.1 / 2.8 /
 // 2.8 / 3.5 / 6.9 ms at 256 / 384 / 512 / 640 / 1024 / 2048.
-constexpr uint32_t kMTE = 512;
-constexpr uint32_t kMTT = 128;      // threads per tile workgroup
+constexpr uint32_t kMTE = 4 * kMS;
+constexpr uint32_t kMTT = kMS;      // threads per tile workgroup
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------- key access
@@ -187,9 +190,9 @@ __global__ __launch_bounds__(256) void bounds_kernel(MergeArgs a) {
   const uint32_t NC = uint32_t(a.mstats[1]);
   const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   const uint32_t t = uint32_t(i / a.nrun), r = uint32_t(i % a.nrun);
-  if (t > NC) return;
+  if (t > a.nc_max || r >= a.nrun) return;
   uint32_t* out = a.bounds + uint64_t(t) * a.nrun + r;  // tile-major: a tile's bounds share a line
-  if (t == NC) {
+  if (t >= NC) {  // (rows past the last tile too: the tile kernels see those tiles empty)
     *out = s_rs[r + 1];
     return;
   }
@@ -301,17 +304,56 @@ __device__ __forceinline__ TwoEnd two_end(const MergeArgs& a, const GKeys& G) {
   return t;
 }
 
-// LDS fast path: 128 threads per tile; every key's first 16 bytes in LDS.
-__device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
-  TileHdr& H = L.h;
-  const uint32_t tid = threadIdx.x, l = lane_id(), w = tid >> 6, nrun = a.nrun, total = H.total;
-  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
-  for (uint32_t u = tid; u < total; u += kMTT) {
-    const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
+// Every tile entry's first 16 key bytes and length into LDS.
+__device__ __forceinline__ void load_tile_keys(const MergeArgs& a, MTileLds& L, const GKeys& G) {
+  const TileHdr& H = L.h;
+  for (uint32_t u = threadIdx.x; u < H.total; u += kMTT) {
+    const uint32_t r = find_run(H.tb, a.nrun, u), g = H.lo[r] + u - H.tb[r];
     const uint32_t p = a.key_off[g], len = a.key_off[g + 1] - p;
     L.kw[u] = key16(G, p, len);
     L.klen[u] = len;
   }
+}
+
+// Survivor prefix over the tile (L.sp, H.nsurv, H.rsp, H.rsv) from L.surv.
+__device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLds& L) {
+  TileHdr& H = L.h;
+  const uint32_t tid = threadIdx.x, l = lane_id(), w = tid >> 6, nrun = a.nrun, total = H.total;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < total; c0 += kMTT) {
+    const uint32_t u = c0 + tid;
+    const uint32_t sv = u < total ? L.surv[u] : 0u;
+    const uint32_t inc = wave_incl_scan32(sv);
+    if (l == 63) H.wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < kMTT / 64; ++x) {
+      before += x < w ? H.wsum[x] : 0u;
+      tot += H.wsum[x];
+    }
+    if (u < total) L.sp[u] = uint16_t(carry + before + inc - sv);
+    carry += tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    L.sp[total] = uint16_t(carry);
+    H.nsurv = carry;
+  }
+  __syncthreads();
+  if (tid < nrun) {
+    H.rsp[tid] = L.sp[H.tb[tid]];
+    H.rsv[tid] = L.sp[H.tb[tid + 1]] - L.sp[H.tb[tid]];
+  }
+  __syncthreads();
+}
+
+// LDS fast path: 128 threads per tile; every key's first 16 bytes in LDS.
+__device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
+  TileHdr& H = L.h;
+  const uint32_t tid = threadIdx.x, nrun = a.nrun, total = H.total;
+  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
+  load_tile_keys(a, L, G);
   __syncthreads();
   // first index of run r2's sub-range whose key is >= (x, xl) (> with upper)
   auto bound = [&](uint32_t r2, const u32x4& x, uint32_t xl, uint32_t xg, bool upper) -> uint32_t {
@@ -346,29 +388,7 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
     L.surv[u] = uint8_t(sv);
   }
   __syncthreads();
-  // survivor prefix over the tile
-  uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < total; c0 += kMTT) {
-    const uint32_t u = c0 + tid;
-    const uint32_t sv = u < total ? L.surv[u] : 0u;
-    const uint32_t inc = wave_incl_scan32(sv);
-    if (l == 63) H.wsum[w] = inc;
-    __syncthreads();
-    const uint32_t before = w ? H.wsum[0] : 0u, tot = H.wsum[0] + H.wsum[1];
-    if (u < total) L.sp[u] = uint16_t(carry + before + inc - sv);
-    carry += tot;
-    __syncthreads();
-  }
-  if (tid == 0) {
-    L.sp[total] = uint16_t(carry);
-    H.nsurv = carry;
-  }
-  __syncthreads();
-  if (tid < nrun) {
-    H.rsp[tid] = L.sp[H.tb[tid]];
-    H.rsv[tid] = L.sp[H.tb[tid + 1]] - L.sp[H.tb[tid]];
-  }
-  __syncthreads();
+  tile_survivor_prefix(a, L);
   // phase B: merged rank inside the tile = survivors with a smaller key in every other run +
   // survivors before this entry in its own run (its group's earlier versions included)
   for (uint32_t u = tid; u < total; u += kMTT) {
@@ -387,7 +407,7 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
     }
     a.mrank[g] = rank;
   }
-  if (tid == 0) a.tcnt[t] = carry;
+  if (tid == 0) a.tcnt[t] = H.nsurv;
 }
 
 // Global path (a tile of more than kMTE entries: many versions of one key, or many runs), one
@@ -489,8 +509,7 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
 
 __global__ __launch_bounds__(kMTT) void merge_tile_kernel(MergeArgs a) {
   __shared__ MTileLds L;
-  const uint32_t t = blockIdx.x;
-  if (t >= uni(uint32_t(a.mstats[1]))) return;
+  const uint32_t t = blockIdx.x;  // (tiles past the candidate count are empty: bounds_kernel)
   if (threadIdx.x < 64) tile_ranges(a, L.h, t);
   __syncthreads();
   const uint32_t total = L.h.total;
@@ -884,14 +903,7 @@ __device__ __forceinline__ void lds_put(uint8_t* dst, const uint8_t* src, uint32
 // LDS image [lo, lo + len) -> global bytes at gdst_aligned + lo (lo < 16): aligned 16-B stores,
 // only the two edge chunks byte-masked.
 __device__ __forceinline__ void flush_img(uint8_t* gdst_aligned, const uint8_t* img, uint32_t lo, uint32_t len) {
-  const uint32_t end = lo + len, nc = (end + 15) >> 4;
-  for (uint32_t c = threadIdx.x; c < nc; c += blockDim.x) {
-    const u32x4 q = *reinterpret_cast<const u32x4*>(img + 16 * c);
-    const uint32_t v[4] = {q.x, q.y, q.z, q.w};
-    const uint32_t a0 = 16 * c < lo ? lo - 16 * c : 0u;
-    const uint32_t a1 = min(end - 16 * c, 16u);
-    store_chunk(gdst_aligned + 16 * c, v, a0, a1);
-  }
+  flush_chunks<1>(gdst_aligned, img, lo, len, threadIdx.x, blockDim.x);
 }
 
 constexpr uint32_t kGKImg = 6144;   // LDS image of a round's keys
@@ -901,57 +913,107 @@ constexpr uint32_t kGVImg = 28672;  // LDS image of a round's values
 // kept keys and values form one contiguous output range each: lanes copy their entry's bytes
 // into LDS images of those ranges, which are then flushed with aligned, coalesced 16-B stores
 // (rounds whose ranges exceed the images copy lane by lane straight to global memory).
+// The tile's four rounds load their entry metadata (keep -> perm -> offsets, ts) up front, so the
+// tile waits out those two dependent round trips once instead of once per round: rounds that
+// each waited keep -> perm -> offsets -> bytes held the kernel at about half the HBM rate.
 __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
   if (a.stats[3]) return;
   const uint64_t N = *a.nm;
-  __shared__ uint64_t ws[4][3];
+  constexpr uint32_t R = kGTile / 256;
+  __shared__ uint64_t ws[R][4][3];
   __shared__ __attribute__((aligned(16))) uint8_t kimg[kGKImg + 32], vimg[kGVImg + 32];
   const uint32_t w = wave_id();
+  const uint64_t j0 = uint64_t(blockIdx.x) * kGTile;
+  if (j0 >= N) return;
+  const uint32_t nr = uint32_t(min<uint64_t>(R, (N - j0 + 255) / 256));  // rounds holding entries
+  uint32_t kf[R], ix[R], kso[R], kl[R], vso[R], vl[R];
+  uint64_t tsv[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint64_t j = j0 + 256 * r + threadIdx.x;
+    kf[r] = j < N ? a.keep[j] : 0u;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) ix[r] = (kf[r] & 1u) ? a.perm[j0 + 256 * r + threadIdx.x] : 0u;
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const bool k = kf[r] & 1u;
+    const uint32_t i = ix[r];
+    kso[r] = k ? a.key_off[i] : 0u;
+    kl[r] = k ? a.key_off[i + 1] : 0u;
+    vso[r] = k ? a.val_off[i] : 0u;
+    vl[r] = k ? a.val_off[i + 1] : 0u;
+    tsv[r] = k ? a.ts[i] : 0ull;
+  }
+  uint64_t o[R], ko[R], vo[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const bool k = kf[r] & 1u;
+    kl[r] -= kso[r];
+    vl[r] -= vso[r];
+    const uint32_t ic = wave_incl_scan32(k ? 1u : 0u);
+    const uint64_t ik = wave_incl_scan<uint64_t>(kl[r]), iv = wave_incl_scan<uint64_t>(vl[r]);
+    if (lane_id() == 63) ws[r][w][0] = ic, ws[r][w][1] = ik, ws[r][w][2] = iv;
+    o[r] = ic - 1;
+    ko[r] = ik - kl[r];
+    vo[r] = iv - vl[r];
+  }
+  __syncthreads();
   uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)], a.tile_pre[3 * uint64_t(blockIdx.x) + 1],
                        a.tile_pre[3 * uint64_t(blockIdx.x) + 2]};
-  for (uint32_t sub = 0; sub < kGTile / 256; ++sub) {
-    const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + threadIdx.x;
-    if (uint64_t(blockIdx.x) * kGTile + sub * 256 >= N) break;  // uniform
-    const uint32_t kf = j < N ? a.keep[j] : 0u;
-    const bool k = kf & 1u;
-    const uint32_t i = k ? a.perm[j] : 0u;
-    const uint32_t kl = k ? a.key_off[i + 1] - a.key_off[i] : 0u;
-    const uint32_t vl = k ? a.val_off[i + 1] - a.val_off[i] : 0u;
-    const uint32_t ic = wave_incl_scan32(k ? 1u : 0u);
-    const uint64_t ik = wave_incl_scan<uint64_t>(kl), iv = wave_incl_scan<uint64_t>(vl);
-    if (lane_id() == 63) ws[w][0] = ic, ws[w][1] = ik, ws[w][2] = iv;
-    __syncthreads();
-    uint64_t o = carry[0] + ic - 1, ko = carry[1] + ik - kl, vo = carry[2] + iv - vl;
-    for (uint32_t q = 0; q < w; ++q) o += ws[q][0], ko += ws[q][1], vo += ws[q][2];
-    const uint64_t K0 = carry[1], V0 = carry[2];
+  uint64_t K0[R + 1], V0[R + 1];
 #pragma unroll
-    for (uint32_t q = 0; q < 3; ++q) carry[q] += ws[0][q] + ws[1][q] + ws[2][q] + ws[3][q];
-    const uint64_t K1 = carry[1], V1 = carry[2];
-    __syncthreads();  // ws is rewritten by the next round
-    if (k) {
-      a.okey_off[o] = uint32_t(ko);
-      a.oval_off[o] = uint32_t(vo);
-      a.ots[o] = a.ts[i];
-      if (a.ksame) a.ksame[o] = uint8_t(kf >> 1);
+  for (uint32_t r = 0; r < R; ++r) {
+    uint64_t b[3] = {carry[0], carry[1], carry[2]};
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      if (q < w) b[0] += ws[r][q][0], b[1] += ws[r][q][1], b[2] += ws[r][q][2];
     }
-    const uint32_t kb = uint32_t(K0 & 15), vb = uint32_t(V0 & 15);
-    const bool staged = K1 - K0 + kb <= kGKImg && V1 - V0 + vb <= kGVImg;
+    o[r] += b[0];
+    ko[r] += b[1];
+    vo[r] += b[2];
+    K0[r] = carry[1];
+    V0[r] = carry[2];
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) carry[q] += ws[r][0][q] + ws[r][1][q] + ws[r][2][q] + ws[r][3][q];
+    if (kf[r] & 1u) {
+      a.okey_off[o[r]] = uint32_t(ko[r]);
+      a.oval_off[o[r]] = uint32_t(vo[r]);
+      a.ots[o[r]] = tsv[r];
+      if (a.ksame) a.ksame[o[r]] = uint8_t(kf[r] >> 1);
+    }
+  }
+  K0[R] = carry[1];
+  V0[R] = carry[2];
+  // the copy rounds, not unrolled (each round's copy loop holds 8 x 16 B of loads per lane):
+  // round r's values sit in slot 0, the slots shifting down after every round
+#pragma unroll 1
+  for (uint32_t r = 0; r < nr; ++r) {
+    const bool k = kf[0] & 1u;
+    const uint32_t kb = uint32_t(K0[0] & 15), vb = uint32_t(V0[0] & 15);
+    const bool staged = K0[1] - K0[0] + kb <= kGKImg && V0[1] - V0[0] + vb <= kGVImg;
     if (staged) {
       // runs of 16 B or more by the whole wave, packed; shorter ones lane by lane
-      const uint32_t kso = k ? a.key_off[i] : 0u, vso = k ? a.val_off[i] : 0u;
-      const uint32_t kd = kb + uint32_t(ko - K0), vd = vb + uint32_t(vo - V0);
-      if (k && kl < 16) lds_put(kimg + kd, a.keys + kso, kl);
-      if (k && vl < 16) lds_put(vimg + vd, a.vals + vso, vl);
-      wave_copy_packed(k && kl >= 16, a.keys, kso, kimg, kd, kl);
-      wave_copy_packed(k && vl >= 16, a.vals, vso, vimg, vd, vl);
+      const uint32_t kd = kb + uint32_t(ko[0] - K0[0]), vd = vb + uint32_t(vo[0] - V0[0]);
+      if (k && kl[0] < 16) lds_put(kimg + kd, a.keys + kso[0], kl[0]);
+      if (k && vl[0] < 16) lds_put(vimg + vd, a.vals + vso[0], vl[0]);
+      wave_copy_packed(k && kl[0] >= 16, a.keys, kso[0], kimg, kd, kl[0]);
+      wave_copy_packed(k && vl[0] >= 16, a.vals, vso[0], vimg, vd, vl[0]);
       __syncthreads();
-      flush_img(a.okeys + (K0 - kb), kimg, kb, uint32_t(K1 - K0));
-      flush_img(a.ovals + (V0 - vb), vimg, vb, uint32_t(V1 - V0));
+      flush_img(a.okeys + (K0[0] - kb), kimg, kb, uint32_t(K0[1] - K0[0]));
+      flush_img(a.ovals + (V0[0] - vb), vimg, vb, uint32_t(V0[1] - V0[0]));
       __syncthreads();
     } else if (k) {
-      lane_copy(a.okeys + ko, a.keys + a.key_off[i], kl);
-      lane_copy(a.ovals + vo, a.vals + a.val_off[i], vl);
+      lane_copy(a.okeys + ko[0], a.keys + kso[0], kl[0]);
+      lane_copy(a.ovals + vo[0], a.vals + vso[0], vl[0]);
     }
+#pragma unroll
+    for (uint32_t q = 0; q + 1 < R; ++q) {
+      kf[q] = kf[q + 1], kso[q] = kso[q + 1], kl[q] = kl[q + 1], vso[q] = vso[q + 1], vl[q] = vl[q + 1];
+      ko[q] = ko[q + 1], vo[q] = vo[q + 1];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < R; ++q) K0[q] = K0[q + 1], V0[q] = V0[q + 1];
   }
 }
 
@@ -1087,6 +1149,7 @@ __device__ __forceinline__ void or_need(uint32_t* flag, bool v) {
 // kRotWin) are staged in LDS once, coalesced, instead of every lane re-reading its ~30 successors
 // from L2; a walk past the window (blocks over 8 KiB) reads global memory.
 constexpr uint32_t kRotWin = 512;
+constexpr uint32_t kRotStep = 4;
 
 __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
   __shared__ uint32_t srec[256 + kRotWin], salcp[256 + kRotWin];
@@ -1101,16 +1164,50 @@ __global__ __launch_bounds__(256) void rot_next_kernel(RotArgs a) {
   bool short_chain = false;
   if (s < n) {
     const uint64_t bs = a.block_size;
-    uint64_t before = 2 + uint64_t(a.rec[s]) + 16;  // entry s always accepted, prefix 0
+    uint64_t before = 2 + uint64_t(srec[threadIdx.x]) + 16;  // entry s always accepted, prefix 0
     uint32_t pmin = kRotLcp;
-    bool direct = false;
+    bool direct = false, stop = false;
     uint32_t sp = 0, sl = 0;
     GKeys K;
     uint64_t e = s + 1;
-    for (; e < n; ++e) {
+    // Fast walk: sorted pairs inside the LDS window, kRotStep entries' (rec, alcp) read ahead of
+    // their use.  (A loop reading `in window ? LDS : global` was if-converted into a global load
+    // per entry as well, and each entry's LDS read waited for the previous entry's update.)
+    const uint64_t wend = min(n, s0 + 256 + kRotWin);
+    for (bool slow = false; !stop && !slow && e + kRotStep <= wend;) {
+      uint32_t r[kRotStep], al[kRotStep];
+#pragma unroll
+      for (uint32_t j = 0; j < kRotStep; ++j) {
+        r[j] = srec[e - s0 + j];
+        al[j] = salcp[e - s0 + j];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kRotStep; ++j) {
+        if (stop || slow) continue;
+        if (before + r[j] + 14 > bs) {
+          stop = true;  // BlockBuilder::add rejects (builder.rs:56-60)
+        } else if (al[j] & kRotUnsorted) {
+          slow = true;  // the general loop compares against the first key from here on
+        } else {
+          pmin = min(pmin, al[j] & kRotLcp);
+          before += uint64_t(r[j]) + 16 - pmin;
+          ++e;
+        }
+      }
+    }
+    // General walk: the window's last entries, past the window, and direct compares after an
+    // unsorted pair.
+    for (; !stop && e < n; ++e) {
       const uint64_t x = e - s0;
       const bool in = x < 256 + kRotWin;
-      const uint32_t r = in ? srec[x] : a.rec[e], al = in ? salcp[x] : a.alcp[e];
+      uint32_t r, al;
+      if (in) {
+        r = srec[x];
+        al = salcp[x];
+      } else {
+        r = a.rec[e];
+        al = a.alcp[e];
+      }
       if (before + r + 14 > bs) break;  // BlockBuilder::add rejects (builder.rs:56-60)
       uint32_t p;
       if (!direct && (al & kRotUnsorted)) {  // LCP vs the first key directly from here on

@@ -298,6 +298,42 @@ __device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4]
     if (x < hi) dst[x] = uint8_t(tw >> (8 * (x & 3)));
   }
 }
+
+// LDS image bytes [lo, lo + len) -> global memory, where image byte x mirrors global byte
+// gdst_aligned + x (gdst_aligned 16-B aligned, lo < 16), by threads tid < nthr of the caller:
+//   * every whole 16-B chunk with one aligned (nt) store, B chunks per thread per round (threads
+//     past the last chunk masked off: repeating a chunk from many lanes serialised the stores);
+//   * the at most two partial edge chunks (the head chunk when lo > 0 or the run ends inside it,
+//     the tail chunk when lo + len is not 16-aligned) one byte per thread, threads 0..15 the head
+//     and 16..31 the tail: one predicated byte store for both.
+// (Per-lane byte-masked edge stores inside the chunk loop compiled to ~15 exec-mask branches per
+// unrolled chunk, every round that held an edge: the scalar unit is the decode's busiest pipe.)
+template <uint32_t B>
+__device__ __forceinline__ void flush_chunks(uint8_t* gdst_aligned, const uint8_t* lds, uint32_t lo, uint32_t len,
+                                             uint32_t tid, uint32_t nthr) {
+  if (len == 0) return;
+  const uint32_t end = lo + len, nc = (end + 15) >> 4;
+  const bool head_part = lo != 0 || end < 16, tail_part = (end & 15) != 0;
+  const uint32_t cf = head_part ? 1u : 0u;                 // first whole chunk
+  const uint32_t ce = tail_part ? nc - 1 : nc;             // one past the last whole chunk
+  {
+    const uint32_t x = tid < 16 ? tid : 16 * (nc - 1) + (tid - 16);  // the edge byte of this thread
+    if (tid < 32 && (tid < 16 ? head_part : tail_part) && x >= lo && x < end) gdst_aligned[x] = lds[x];
+  }
+  if (ce > cf) {
+    const uint32_t nw = ce - cf;
+    for (uint32_t c0 = 0; c0 < nw; c0 += nthr * B) {
+      u32x4 q[B];
+#pragma unroll
+      for (uint32_t j = 0; j < B; ++j)
+        if (c0 + nthr * j + tid < nw) q[j] = *reinterpret_cast<const u32x4*>(lds + 16 * (cf + c0 + nthr * j + tid));
+#pragma unroll
+      for (uint32_t j = 0; j < B; ++j)
+        if (c0 + nthr * j + tid < nw)
+          __builtin_nontemporal_store(q[j], reinterpret_cast<u32x4*>(gdst_aligned + 16 * (cf + c0 + nthr * j + tid)));
+    }
+  }
+}
 }  // namespace
 
 

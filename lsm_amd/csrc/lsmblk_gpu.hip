@@ -63,8 +63,8 @@ constexpr uint32_t kTile = 64;  // blocks per count tile
 // trace per tile for the first kDbgTiles tiles: [0] finish start [1] bases published [2] first
 // decoder's base wait begins [3] ends [4] the tile's first count starts [5] its first decoder starts
 constexpr uint32_t kDbgTiles = 32768, kDbgWords = 16 + 8 * kDbgTiles;
-__device__ __forceinline__ void dbg_trace(uint64_t* dbg, uint64_t t, uint32_t k) {
-  if (dbg && t < kDbgTiles && lane_id() == 0) dbg[16 + 8 * t + k] = __builtin_amdgcn_s_memrealtime();
+__device__ __forceinline__ void dbg_trace(uint64_t* dbg, uint64_t t, uint32_t k) {  // diagnostics builds only
+  if (kDiag && dbg && t < kDbgTiles && lane_id() == 0) dbg[16 + 8 * t + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 
@@ -245,6 +245,12 @@ struct LdsSink {
 // Fast path, lane per entry: every entry lane writes its own key and value as contiguous
 // runs of 16-B pieces (the last piece overlaps the previous one), so runs of adjacent
 // entries abut and no lane needs a chunk -> entry search.
+// The piece loops run a wave-uniform trip count (the wave's longest run) with each lane's piece
+// index clamped to its last piece, so no per-piece exec mask is needed (PMC: the scalar unit,
+// which runs those masks, is the decode's busiest pipe).  Lanes past the block's entries are
+// masked off once per iteration (mirroring lane 0's entry instead made up to 63 lanes write the
+// same LDS words: bank-conflicted, the decode lost a third of its rate).  Keys under 16 B,
+// suffixes before the image start and values under 16 B keep per-lane paths.
 template <class Sink>
 __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, uint32_t lead, uint32_t n,
                                                const DecEnt (&ent)[2], uint64_t E0, uint64_t K0, uint64_t V0,
@@ -254,11 +260,19 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
   const uint32_t fk = lead + 4;  // image byte of the first key
 #pragma unroll
   for (uint32_t it = 0; it < 2; ++it) {
+    if (64 * it >= n) break;  // wave-uniform
     const uint32_t k = 64 * it + l;
-    if (k >= n) continue;
+    const bool live = k < n;
     const uint32_t epos = ent[it].epos, p = ent[it].p, s = ent[it].s;
     const uint32_t kout = ent[it].kout, vout = ent[it].vout, vl = ent[it].vl;
     const uint32_t sb = lead + epos + 4;  // image byte of the suffix
+    const uint32_t kl = p + s;
+    // wave-uniform trip counts and path choice, over the live lanes (all lanes active here)
+    const bool kirr = live && (kl < 16 || sb < p);
+    const bool kuni = !__ballot(kirr);
+    const uint32_t nkmax = __builtin_amdgcn_readlane(wave_incl_max32(live ? (kl + 15) >> 4 : 0u), 63);
+    const uint32_t nvmax = __builtin_amdgcn_readlane(wave_incl_max32(live && vl >= 16 ? (vl + 15) >> 4 : 0u), 63);
+    if (!live) continue;
     if (!(skip & 8)) {
       const uint64_t e = E0 + k;
       const u32x2 q = *reinterpret_cast<const u32x2*>(img + sb + s);
@@ -269,63 +283,83 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
     if (!(skip & 2)) {
       // key byte x = first key byte x (x < p) or suffix byte x - p: a 16-B piece is one
       // unaligned read of each, merged under a per-dword byte mask
-      const uint32_t kl = p + s;
-      for (uint32_t t = 0; t < kl; t += 16) {
-        const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
-        uint32_t v[4];
-        if (sb + o >= p) {
-          const u32x4 sq = *reinterpret_cast<const u32x4*>(img + sb + o - p);
-          const u32x4 fq = *reinterpret_cast<const u32x4*>(img + fk + o);
-          const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w}, fv[4] = {fq.x, fq.y, fq.z, fq.w};
+      auto merged = [&](uint32_t o, uint32_t (&v)[4]) {
+        const u32x4 sq = *reinterpret_cast<const u32x4*>(img + sb + o - p);
+        const u32x4 fq = *reinterpret_cast<const u32x4*>(img + fk + o);
+        const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w}, fv[4] = {fq.x, fq.y, fq.z, fq.w};
 #pragma unroll
-          for (uint32_t d = 0; d < 4; ++d) {
-            const int32_t nf = int32_t(p) - int32_t(o + 4 * d);  // leading bytes from the first key
-            const uint32_t m = nf <= 0 ? 0u : nf >= 4 ? ~0u : (1u << (8 * nf)) - 1;
-            v[d] = (fv[d] & m) | (sv[d] & ~m);
-          }
-        } else {  // suffix before the image start (a prefix longer than the entry offset)
-#pragma unroll
-          for (uint32_t d = 0; d < 4; ++d) {
-            uint32_t wd = 0;
-            for (uint32_t i = 0; i < 4; ++i) {
-              const uint32_t x = o + 4 * d + i;
-              wd |= uint32_t(x < p ? img[fk + x] : img[sb + x - p]) << (8 * i);
-            }
-            v[d] = wd;
-          }
+        for (uint32_t d = 0; d < 4; ++d) {
+          const int32_t nf = int32_t(p) - int32_t(o + 4 * d);  // leading bytes from the first key
+          const uint32_t m = nf <= 0 ? 0u : nf >= 4 ? ~0u : (1u << (8 * nf)) - 1;
+          v[d] = (fv[d] & m) | (sv[d] & ~m);
         }
-        if (kl >= 16) out.put16(false, kout + o, v);
-        else out.put_short(false, kout, kl, v);
+      };
+      if (kuni) {  // every live key >= 16 B, its suffix in the image
+        for (uint32_t t = 0; t < nkmax; ++t) {
+          const uint32_t o = min(16 * t, kl - 16);
+          uint32_t v[4];
+          merged(o, v);
+          out.put16(false, kout + o, v);
+        }
+      } else {
+        for (uint32_t t = 0; t < kl; t += 16) {
+          const uint32_t o = kl >= 16 ? min(t, kl - 16) : 0u;
+          uint32_t v[4];
+          if (sb + o >= p) {
+            merged(o, v);
+          } else {  // suffix before the image start (a prefix longer than the entry offset)
+#pragma unroll
+            for (uint32_t d = 0; d < 4; ++d) {
+              uint32_t wd = 0;
+              for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t x = o + 4 * d + i;
+                wd |= uint32_t(x < p ? img[fk + x] : img[sb + x - p]) << (8 * i);
+              }
+              v[d] = wd;
+            }
+          }
+          if (kl >= 16) out.put16(false, kout + o, v);
+          else out.put_short(false, kout, kl, v);
+        }
       }
     }
     if (!(skip & 4)) {
       const uint32_t src = sb + s + 10;  // image byte of the value
-      for (uint32_t t0 = 0; t0 < vl; t0 += 16 * kLB) {
-        u32x4 q[kLB];
+      if (vl >= 16) {
+        for (uint32_t i0 = 0; i0 < nvmax; i0 += kLB) {  // uniform trip count, pieces clamped
+          u32x4 q[kLB];
+          uint32_t o[kLB];
 #pragma unroll
-        for (uint32_t j = 0; j < kLB; ++j) {
-          const uint32_t t = t0 + 16 * j;
-          if (t < vl) q[j] = *reinterpret_cast<const u32x4*>(img + src + (vl >= 16 ? min(t, vl - 16) : 0u));
-        }
+          for (uint32_t j = 0; j < kLB; ++j) {
+            o[j] = min(16 * (i0 + j), vl - 16);
+            q[j] = *reinterpret_cast<const u32x4*>(img + src + o[j]);
+          }
 #pragma unroll
-        for (uint32_t j = 0; j < kLB; ++j) {
-          const uint32_t t = t0 + 16 * j;
-          if (t < vl) {
+          for (uint32_t j = 0; j < kLB; ++j) {
             const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-            if (vl >= 16) out.put16(true, vout + min(t, vl - 16), v);
-            else out.put_short(true, vout, vl, v);
+            out.put16(true, vout + o[j], v);
           }
         }
+      } else if (vl) {
+        const u32x4 q = *reinterpret_cast<const u32x4*>(img + src);
+        const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+        out.put_short(true, vout, vl, v);
       }
     }
   }
 }
 
-// Aligned flush of an LDS output run: LDS bytes [lo, lo + len) -> global bytes at gdst, with
-// lo == gdst & 15 (the LDS run mirrors the global 16-B alignment).  Interior chunks are one
-// b128 store; the two edge chunks store only their own bytes.
+// Aligned flush of an LDS output run by the wave: LDS bytes [lo, lo + len) -> global bytes at
+// gdst_aligned + lo, the LDS run mirroring the global 16-B alignment (flush_chunks).
 template <uint32_t B = kLB>
 __device__ __forceinline__ void flush_run(uint8_t* gdst_aligned, const uint8_t* lds, uint32_t lo, uint32_t len) {
+  flush_chunks<B>(gdst_aligned, lds, lo, len, lane_id(), 64);
+}
+
+// The same flush with the edge chunks byte-masked inside the chunk loop (emit: its register
+// budget has no room for flush_chunks' separate edge pass).
+template <uint32_t B>
+__device__ __forceinline__ void flush_run_masked(uint8_t* gdst_aligned, const uint8_t* lds, uint32_t lo, uint32_t len) {
   const uint32_t end = lo + len, nc = (end + 15) >> 4;
   const uint32_t l = lane_id();
   for (uint32_t c0 = 0; c0 < nc; c0 += 64 * B) {
@@ -968,7 +1002,7 @@ __device__ void lag_tile_finish(const DecodeArgs& a, uint64_t t, uint32_t& err) 
     gstore(a.bbase + 3 * (b0 + l) + 1, (sat47(X[1] + i1 - x1) << 16) | tg, a.poll);
     gstore(a.bbase + 3 * (b0 + l) + 2, (sat47(X[2] + i2 - x2) << 16) | tg, a.poll);
   }
-  if (a.dbg) {
+  if (kDiag && a.dbg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dbg_trace(a.dbg, t, 1);
   }
@@ -976,8 +1010,11 @@ __device__ void lag_tile_finish(const DecodeArgs& a, uint64_t t, uint32_t& err) 
 
 __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   __shared__ DecLds lds;
-  const uint64_t j = blockIdx.x;
-  const bool cnt = j < a.nblk;
+  // Workgroup indices, the lag and the block count are below 2^31 (lsmblk_decode_batch_ex), so the
+  // per-workgroup bookkeeping is 32-bit: the scalar unit, not the vector one, is the decode's most
+  // loaded pipe (PMC), and 64-bit scalar math costs it two to four times more.
+  const uint32_t j = blockIdx.x, nblk = uint32_t(a.nblk), lag0 = uint32_t(a.lag);
+  const bool cnt = j < nblk;
   // both blocks' ranges first, then the count's staging loads, then (inside decode_block) the
   // decode's: the count waits only for its own loads
   // (one load instruction: lanes 0-1 the count's range, lanes 2-3 the decode's at the largest lag)
@@ -988,28 +1025,28 @@ __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   // fetched for 4.3 GB of blocks), 2.02 at 640 (40 MiB, as 10240 x 4 KiB) and 2.01 at 320.
   const uint32_t l = lane_id();
   uint64_t o = 0;
-  if ((l < 2 && cnt) || (l >= 2 && l < 4 && j >= a.lag)) o = a.blk_off[(l < 2 ? j : j - a.lag) + (l & 1)];
+  if ((l < 2 && cnt) || (l >= 2 && l < 4 && j >= lag0)) o = a.blk_off[(l < 2 ? j : j - lag0) + (l & 1)];
   // the batch's first and last offsets: scalar loads (as vector-load lanes they cost U's decode ~1 %)
-  const uint64_t o0 = a.lag_bytes ? a.blk_off[0] : 0, o1 = a.lag_bytes ? a.blk_off[a.nblk] : 0;
+  const uint64_t o0 = a.lag_bytes ? a.blk_off[0] : 0, o1 = a.lag_bytes ? a.blk_off[nblk] : 0;
   const uint64_t cs = lane64(o, 0), ce = lane64(o, 1);
   CntPre C;
   const bool do_cnt = cnt && !(diag_mask(a.skip) & 1024);  // (1024: ablation, aggregates 0 without the count)
   if (do_cnt) C = cnt_issue(a.blocks, a.tail, cs, ce);
-  uint64_t lag = a.lag;  // (worked out under the count's loads)
+  uint32_t lag = lag0;  // (worked out under the count's loads)
   if (a.lag_bytes) {
-    // lag_bytes / mean block size < lag?  (4 KiB units; products below 2^57; the divide only then)
-    const uint64_t tot = (o1 - o0) >> 12, lb = a.lag_bytes >> 12;
-    if (lb * a.nblk < lag * tot) {
-      const uint64_t want = uint64_t(float(uint32_t(lb)) * (float(uint32_t(a.nblk)) / float(uint32_t(tot))));
+    // lag_bytes / mean block size < lag?  (4 KiB units: 32 x 32-bit products; the divide only then)
+    const uint32_t tot = uint32_t(min((o1 - o0) >> 12, uint64_t(0xFFFFFFFFu))), lb = uint32_t(a.lag_bytes >> 12);
+    if (uint64_t(lb) * nblk < uint64_t(lag) * tot) {
+      const uint32_t want = uint32_t(float(lb) * (float(nblk) / float(tot)));
       lag = want < 2 * kTile ? 2 * kTile : want;
     }
   }
-  if (j >= a.nblk + lag) return;  // (the grid is sized for the largest lag; no count was issued here)
+  if (j >= nblk + lag) return;  // (the grid is sized for the largest lag; no count was issued here)
   const bool dec = j >= lag;
   if (j % kTile == 0) dbg_trace(a.dbg, j / kTile, 4);                       // the tile's first count starts
   if (dec && (j - lag) % kTile == 0) dbg_trace(a.dbg, (j - lag) / kTile, 5);  // its first decoder starts
-  const uint64_t b = j - lag;
-  if (lag != a.lag && dec && l >= 2 && l < 4) o = a.blk_off[b + (l & 1)];  // (wave-uniform branch)
+  const uint32_t b = j - lag;
+  if (lag != lag0 && dec && l >= 2 && l < 4) o = a.blk_off[b + (l & 1)];  // (wave-uniform branch)
   const uint64_t ds = lane64(o, 2), de = lane64(o, 3);
   uint32_t err = 0;
   BlkCount r{0, 0, 0, false};
@@ -1029,9 +1066,9 @@ __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
   // tile finish on the slowest XCD -- which then stayed `lag` behind, the other XCDs' decoders
   // waiting (2.8 ms at every lag); the tile's last block finishing it after its own decode
   // chained the tiles `lag` apart into one serial sequence (2.7 ms).
-  const uint64_t D = lag / 2 + 63;
-  const uint64_t ft = j >= D ? (j - D + 8) / kTile : ~0ull;  // the tile workgroup j finishes, if any
-  const bool fin = j >= D && ft * kTile + D - (ft & 7) == j && ft * kTile < a.nblk;
+  const uint32_t D = lag / 2 + 63;
+  const uint32_t ft = j >= D ? (j - D + 8) / kTile : ~0u;  // the tile workgroup j finishes, if any
+  const bool fin = j >= D && ft * kTile + D - (ft & 7) == j && ft * kTile < nblk;
   auto publish = [&] {
     if (!cnt || (diag_mask(a.skip) & 16384)) return;  // (16384: ablation, no publish)
     // (a malformed block is reported by its decoder; its aggregate is 0 there too)
@@ -1399,7 +1436,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     if (s1 < s0) s1 = s0;
   }
   const PlanKeys K = plan_keys(a);
-  uint64_t* const tr = a.dbg && g < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(g) : nullptr;  // (diagnostics)
+  uint64_t* const tr = kDiag && a.dbg && g < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(g) : nullptr;  // (diagnostics)
   if (wv >= 4) {
     plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
     const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
@@ -1876,22 +1913,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         vp = vo0 - vb0;
         vl = vo1 - vo0;
         if (k != 0 && !(diag_mask(a.skip) & 128)) {
+          // the first 16 bytes by selects, no branches: z = the first differing byte (16 if none);
+          // bytes read past either key do not matter, p is capped at m (the key image has 16 B
+          // of slack before the value image, which is LDS too)
           const uint32_t m = fl < kl ? fl : kl;
-          p = m;
-          bool done = false;
+          uint32_t z = 16;
 #pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) {
-            if (!done && 4 * i < m) {
-              const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
-              if (x) {
-                const uint32_t z = 4 * i + (__builtin_ctz(x) >> 3);
-                p = z < m ? z : m;
-                done = true;
-              }
-            } else {
-              done = true;
-            }
+          for (int i = 3; i >= 0; --i) {
+            const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
+            z = x ? 4 * i + (__builtin_ctz(x) >> 3) : z;
           }
+          p = z < 16 && z < m ? z : m;  // (z == 16: m unless the loop below finds a difference)
+          bool done = z < 16 || m <= 16;
           for (uint32_t q = 16; !done && q < m; q += 4) {
             const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
             if (x) {
@@ -2013,7 +2046,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     wave_sync();
     // flush the image: 16-B chunks; only the two end chunks can be partial
     // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
-    if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
+    if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run_masked<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
     wave_sync();
     if (!has_next) break;
     cur = nxt;
@@ -2887,7 +2920,7 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->skip = value;
   } else if (key == LSMBLK_DEBUG_TWO_PASS_DECODE) {
     c->dec_two_pass = value != 0;
-  } else if (key == LSMBLK_DEBUG_COUNTERS) {
+  } else if (key == LSMBLK_DEBUG_COUNTERS && kDiag) {  // realtime traces: diagnostics builds only
     if (value && !c->dbg) {
       DeviceGuard dg(c->device, c);
       if (!dg.ok || hipMalloc(reinterpret_cast<void**>(&c->dbg), kDbgWords * 8) != hipSuccess) {

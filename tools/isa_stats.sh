@@ -1,10 +1,13 @@
 #!/bin/bash
-# Resource usage (VGPRs, LDS, spills) of the hot kernels from the gfx950 ISA of lsmblk_gpu.hip.
+# Resource usage (VGPRs, LDS, spills) of kernels from the gfx950 ISA of one source file.
+# usage: tools/isa_stats.sh [SRC (default lsmblk_gpu.hip)] [NAME_SUBSTRING...]
+SRC=lsmblk_gpu.hip
+case "$1" in *.hip) SRC=$1; shift;; esac
 cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I/root/repo/include -DLSMBLK_DIAG_BUILD=0 --offload-device-only -S \
-  -o /tmp/lsmblk_gpu.s /root/repo/lsm_amd/csrc/lsmblk_gpu.hip 2>/dev/null || exit 1
+  -o /tmp/isa_stats.s /root/repo/lsm_amd/csrc/$SRC 2>/dev/null || exit 1
 python3 - "$@" <<'PY'
 import re, sys
-s = open('/tmp/lsmblk_gpu.s').read()
+s = open('/tmp/isa_stats.s').read()
 md = s[s.index('amdhsa.kernels'):]
 pat = sys.argv[1:] or ['decode', 'dec_count', 'emit_kernel', 'plan_walk']
 for blk in md.split('  - .agpr_count')[1:]:

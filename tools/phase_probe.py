@@ -27,6 +27,9 @@ def main():
     blocks, blk_off = batch.encode_kv(kv, seg, synth.BLOCK_SIZE["U"])
     ctx = batch._ctx(0)
     check(lib().lsmblk_debug_set(ctx, 1, mask))
+    check(lib().lsmblk_debug_set(ctx, 3, int(os.environ.get("PROBE_TWO_PASS", "0"))))  # two-pass decode (A/B)
+    if os.environ.get("PROBE_LAG"):
+        check(lib().lsmblk_debug_set(ctx, 4, int(os.environ["PROBE_LAG"])))
     for _ in range(3):
         if which == "encode":
             batch.encode_kv(kv, seg, synth.BLOCK_SIZE["U"])

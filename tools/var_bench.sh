@@ -10,5 +10,5 @@ for v in "$@"; do
     --steps 20 $BENCH_ARGS > gpurun_out/var_$v.json 2> gpurun_out/var_$v.log || exit 1
   python3 -c "
 import json; d=json.load(open('gpurun_out/var_$v.json')); r=d['roofline']
-print('$v', d['value'], d['ms_per_step'], {k: round(x, 3) for k, x in r['kernels_ms'].items()}, d['config']['roundtrip_bit_exact'])"
+print('$v', d['value'], d['ms_per_step'], {k: round(x, 3) for k, x in r['kernels_ms'].items()}, d['config'].get('roundtrip_bit_exact', d['config'].get('oracle_checked')))"
 done
