@@ -33,17 +33,20 @@
 
 namespace {
 
-#ifndef LSMBLK_MERGE_SPACING
-#define LSMBLK_MERGE_SPACING 128
-#endif
-constexpr uint32_t kMS = LSMBLK_MERGE_SPACING;  // every kMS-th entry of a run is a merge candidate
+constexpr uint32_t kMS = 128;  // every kMS-th entry of a run is a merge candidate
 constexpr uint32_t kMaxRuns = 64;   // runs per merge (one lane per run in the tile kernels)
-// Tile entries with LDS tables (larger tiles: the one-wave global path).  Tile sizes are about
-// exponential with mean kMS (the gaps between consecutive candidates of all runs), so the limit
-// trades the global path's share against residency: merge_tile on config C took 5.3 / 3.1 / 2.8 /
-// 2.8 / 3.5 / 6.9 ms at 256 / 384 / 512 / 640 / 1024 / 2048.
-constexpr uint32_t kMTE = 4 * kMS;
-constexpr uint32_t kMTT = kMS;      // threads per tile workgroup
+// Tile entries with LDS tables.  Tile sizes average kMS (the gaps between consecutive candidates
+// of all runs) with a long tail, so the limit trades residency against the share of tiles left
+// to merge_big_kernel: merge_tile on config C took 5.3 / 3.1 / 2.8 / 2.8 / 3.5 / 6.9 ms at
+// 256 / 384 / 512 / 640 / 1024 / 2048 entries when larger tiles went to the one-wave global path
+// (and 3.2 / 3.8 ms at mean tile sizes 192 / 256 with the limit at 4x the mean).
+constexpr uint32_t kMTE = 512;
+constexpr uint32_t kMTT = 128;      // threads per tile workgroup
+// merge_big_kernel: tiles of kMTE < total <= kBigTE entries (about 1 % of the tiles; 0.8 ms of
+// config C's 2.9 ms merge_tile as a global-memory tail), workgroups of kBigTT threads
+constexpr uint32_t kBigTE = 2048;
+constexpr uint32_t kBigTT = 256;
+constexpr uint32_t kBigGrid = 1024;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------- key access
@@ -107,7 +110,8 @@ struct MergeArgs {
   uint32_t* tcnt;           // nc_max: survivors per tile
   uint64_t* tpre;           // nc_max + 1: tile bases
   uint32_t* perm;           // n: merged position -> input index
-  uint64_t* mstats;         // [0] merged entries [1] candidates (tiles) [3] error flags
+  uint32_t* big;            // nc_max: tiles left to merge_big_kernel (their count in mstats[5])
+  uint64_t* mstats;         // [0] merged entries [1] candidates (tiles) [3] error flags [5] big tiles
   uint32_t two;             // LSMBLK_MERGE_TWO_LEVEL: TwoMergeIterator(runs 0..nrun-2, run nrun-1)
   uint32_t two_end;         // two-level, key-range shard: LSMBLK_TWO_END_* (where b's last key lies)
 };
@@ -219,15 +223,18 @@ struct TileHdr {
   uint32_t lo[kMaxRuns], tb[kMaxRuns + 1];  // run r's sub-range start; tile index of its first entry
   uint32_t rsp[kMaxRuns], rsv[kMaxRuns];   // survivors before run r's sub-range / inside it
   uint32_t total, nsurv;
-  uint32_t wsum[kMTT / 64];
+  uint32_t wsum[kBigTT / 64];
 };
-struct alignas(16) MTileLds {
+template <uint32_t E>
+struct alignas(16) MTileLdsT {
   TileHdr h;
-  u32x4 kw[kMTE];          // first 16 key bytes as big-endian words, zero padded
-  uint32_t klen[kMTE];
-  uint16_t sp[kMTE + 1];   // survivor prefix over the tile (run-major order)
-  uint8_t surv[kMTE];
+  u32x4 kw[E];          // first 16 key bytes as big-endian words, zero padded
+  uint32_t klen[E];
+  uint16_t sp[E + 1];   // survivor prefix over the tile (run-major order)
+  uint8_t surv[E];
 };
+using MTileLds = MTileLdsT<kMTE>;
+using MTileBigLds = MTileLdsT<kBigTE>;
 
 // The tile's per-run sub-ranges (wave 0; lane r = run r).
 __device__ __forceinline__ void tile_ranges(const MergeArgs& a, TileHdr& H, uint32_t t) {
@@ -305,9 +312,10 @@ __device__ __forceinline__ TwoEnd two_end(const MergeArgs& a, const GKeys& G) {
 }
 
 // Every tile entry's first 16 key bytes and length into LDS.
-__device__ __forceinline__ void load_tile_keys(const MergeArgs& a, MTileLds& L, const GKeys& G) {
+template <uint32_t E, uint32_t T>
+__device__ __forceinline__ void load_tile_keys(const MergeArgs& a, MTileLdsT<E>& L, const GKeys& G) {
   const TileHdr& H = L.h;
-  for (uint32_t u = threadIdx.x; u < H.total; u += kMTT) {
+  for (uint32_t u = threadIdx.x; u < H.total; u += T) {
     const uint32_t r = find_run(H.tb, a.nrun, u), g = H.lo[r] + u - H.tb[r];
     const uint32_t p = a.key_off[g], len = a.key_off[g + 1] - p;
     L.kw[u] = key16(G, p, len);
@@ -316,11 +324,12 @@ __device__ __forceinline__ void load_tile_keys(const MergeArgs& a, MTileLds& L, 
 }
 
 // Survivor prefix over the tile (L.sp, H.nsurv, H.rsp, H.rsv) from L.surv.
-__device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLds& L) {
+template <uint32_t E, uint32_t T>
+__device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLdsT<E>& L) {
   TileHdr& H = L.h;
   const uint32_t tid = threadIdx.x, l = lane_id(), w = tid >> 6, nrun = a.nrun, total = H.total;
   uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < total; c0 += kMTT) {
+  for (uint32_t c0 = 0; c0 < total; c0 += T) {
     const uint32_t u = c0 + tid;
     const uint32_t sv = u < total ? L.surv[u] : 0u;
     const uint32_t inc = wave_incl_scan32(sv);
@@ -328,7 +337,7 @@ __device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLd
     __syncthreads();
     uint32_t before = 0, tot = 0;
 #pragma unroll
-    for (uint32_t x = 0; x < kMTT / 64; ++x) {
+    for (uint32_t x = 0; x < T / 64; ++x) {
       before += x < w ? H.wsum[x] : 0u;
       tot += H.wsum[x];
     }
@@ -349,11 +358,12 @@ __device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLd
 }
 
 // LDS fast path: 128 threads per tile; every key's first 16 bytes in LDS.
-__device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
+template <uint32_t E, uint32_t T>
+__device__ void merge_tile_lds(const MergeArgs& a, MTileLdsT<E>& L, uint32_t t) {
   TileHdr& H = L.h;
   const uint32_t tid = threadIdx.x, nrun = a.nrun, total = H.total;
   const GKeys G = gkeys(a.keys, a.key_off[a.n]);
-  load_tile_keys(a, L, G);
+  load_tile_keys<E, T>(a, L, G);
   __syncthreads();
   // first index of run r2's sub-range whose key is >= (x, xl) (> with upper)
   auto bound = [&](uint32_t r2, const u32x4& x, uint32_t xl, uint32_t xg, bool upper) -> uint32_t {
@@ -371,7 +381,7 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
   TwoEnd te{};
   if (a.two) te = two_end(a, G);
   // phase A: survival -- no lower-index run holds the key (MergeIterator advances those heads)
-  for (uint32_t u = tid; u < total; u += kMTT) {
+  for (uint32_t u = tid; u < total; u += T) {
     const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
     const u32x4 x = L.kw[u];
     const uint32_t xl = L.klen[u];
@@ -388,10 +398,10 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLds& L, uint32_t t) {
     L.surv[u] = uint8_t(sv);
   }
   __syncthreads();
-  tile_survivor_prefix(a, L);
+  tile_survivor_prefix<E, T>(a, L);
   // phase B: merged rank inside the tile = survivors with a smaller key in every other run +
   // survivors before this entry in its own run (its group's earlier versions included)
-  for (uint32_t u = tid; u < total; u += kMTT) {
+  for (uint32_t u = tid; u < total; u += T) {
     const uint32_t r = find_run(H.tb, nrun, u), g = H.lo[r] + u - H.tb[r];
     uint32_t rank = kNone;
     if (L.surv[u]) {
@@ -518,9 +528,25 @@ __global__ __launch_bounds__(kMTT) void merge_tile_kernel(MergeArgs a) {
     return;
   }
   if (total <= kMTE) {
-    merge_tile_lds(a, L, t);
-  } else if (threadIdx.x < 64) {
-    merge_tile_global(a, L.h, t);
+    merge_tile_lds<kMTE, kMTT>(a, L, t);
+  } else if (threadIdx.x == 0) {  // to merge_big_kernel
+    const uint64_t i = atomicAdd(reinterpret_cast<unsigned long long*>(a.mstats + 5), 1ull);
+    a.big[i] = t;
+  }
+}
+
+// The tiles merge_tile_kernel left (over kMTE entries): kBigGrid persistent workgroups over the
+// list, LDS tables up to kBigTE entries, the one-wave global path beyond.
+__global__ __launch_bounds__(kBigTT) void merge_big_kernel(MergeArgs a) {
+  __shared__ MTileBigLds L;
+  const uint32_t nb = uni(uint32_t(a.mstats[5]));
+  for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
+    const uint32_t t = a.big[i];
+    if (threadIdx.x < 64) tile_ranges(a, L.h, t);
+    __syncthreads();
+    if (L.h.total <= kBigTE) merge_tile_lds<kBigTE, kBigTT>(a, L, t);
+    else if (threadIdx.x < 64) merge_tile_global(a, L.h, t);
+    __syncthreads();
   }
 }
 
@@ -1612,6 +1638,7 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   P.m.tcnt = cv.take<uint32_t>(nc_max + 1);
   P.m.tpre = cv.take<uint64_t>(nc_max + 2);
   P.m.perm = cv.take<uint32_t>(n + 1);
+  P.m.big = cv.take<uint32_t>(nc_max + 1);
   P.m.mstats = cv.take<uint64_t>(8);
   P.keep = cv.take<uint32_t>(n + 1);
   P.ksame = cv.take<uint8_t>(n + 1);
@@ -1658,6 +1685,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   const uint64_t nb = (uint64_t(nc) + 1) * nrun;
   LSM_LAUNCH(bounds_kernel, dim3(uint32_t((nb + 255) / 256)), dim3(256), 0, st, m);
   LSM_LAUNCH(merge_tile_kernel, dim3(nc), dim3(kMTT), 0, st, m);
+  LSM_LAUNCH(merge_big_kernel, dim3(std::min(nc, kBigGrid)), dim3(kBigTT), 0, st, m);
   LSM_LAUNCH(tile_scan_kernel, dim3(1), dim3(1024), 0, st, m);
   LSM_LAUNCH(perm_kernel, dim3(nc), dim3(64), 0, st, m);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;

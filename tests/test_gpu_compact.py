@@ -213,6 +213,31 @@ def test_two_level_synthetic_and_big_tiles():
     assert gpu_merge_mode(big, LSMBLK_MERGE_RUNS) == pyref.merge_runs_rule(big)
 
 
+@pytest.mark.parametrize("versions", [(130, 150, 200, 170), (400, 380, 300, 420), (520, 1, 0, 600)])
+def test_merge_tiles_over_the_small_lds_limit(versions):
+    """Tiles of 512 < n <= 2048 entries go to merge_big_kernel's LDS tables (and past 2048 to the
+    global path): hot keys with hundreds of versions per run, next to ordinary keys."""
+    rng = np.random.default_rng(sum(versions))
+    runs = []
+    for r, nv in enumerate(versions):
+        run = [(b"k%05d" % i, 7, b"v%d" % r) for i in sorted(rng.choice(4000, 300, replace=False))]
+        run += [(b"k02000x", int(t), b"h%d" % r) for t in range(nv + 1000 * (4 - r), 1000 * (4 - r), -1)]
+        run += [(b"k03000y", int(t), b"y%d" % r) for t in range(nv // 2 + 1000 * (4 - r), 1000 * (4 - r), -1)]
+        runs.append(sorted(run, key=lambda e: e[0]))  # stable: versions stay newest first
+    assert gpu_merge_mode(runs, TWO) == pyref.two_merge_rule(runs)
+    assert gpu_merge_mode(runs, LSMBLK_MERGE_RUNS) == pyref.merge_runs_rule(runs)
+
+
+def test_merge_many_runs_natural_big_tiles():
+    """Twelve overlapping runs: candidate gaps leave a few percent of the tiles over 512 entries
+    (merge_big_kernel) among the ordinary ones."""
+    keys, ko, vals, vo, ts, rs = synth.gen_runs(60000, nrun=12, seed=17, versions=2)
+    ents = O.KV(keys, ko, vals, vo, ts).entries()
+    runs = [ents[rs[r]:rs[r + 1]] for r in range(12)]
+    assert gpu_merge_mode(runs, LSMBLK_MERGE_RUNS) == pyref.merge_runs_rule(runs)
+    assert gpu_merge_mode(runs, TWO) == pyref.two_merge_rule(runs)
+
+
 def test_two_level_key_range_argument_errors():
     """Key ranges take the two-level merge through lsmblk_compact_merge_batch_ex only, with the
     kept entries' same_as_last_key output and a valid b-end mode (tests/test_gpu_shard.py runs it)."""
