@@ -24,10 +24,10 @@
 //   merge_tile_kernel  one wave per tile: the tile's keys staged in LDS, survival (search the
 //                      lower-index runs), survivor prefix, in-tile merged rank (search every
 //                      other run); equal keys never straddle tiles (key-only lower bounds)
-//   tile_scan_kernel   exclusive scan of per-tile survivor counts -> tile bases
+//   tscan_*_kernel     exclusive scan of per-tile survivor counts -> tile bases
 //   perm_kernel        perm[tile base + in-tile rank] = input index
 // Then, over the merged order:
-//   mflag_kernel / mscan_kernel / mwrite_kernel   the compaction rules (or keep-all for a plain
+//   mflag_kernel / mscan_*_kernel / mwrite_kernel   the compaction rules (or keep-all for a plain
 //                      merge), output offsets, and the gather of the kept entries.
 #include "lsmblk_dev.hpp"
 
@@ -108,7 +108,9 @@ struct MergeArgs {
   uint32_t* mrank;          // n: in-tile merged rank of a surviving entry, kNone if dropped
   uint32_t* sp;             // n: survivor prefix (tiles too large for LDS)
   uint32_t* tcnt;           // nc_max: survivors per tile
-  uint64_t* tpre;           // nc_max + 1: tile bases
+  uint64_t* tpre;           // nc_max + 1: tile bases inside their scan part (kTScan tiles)
+  uint64_t* tpart;          // per scan part: its tiles' survivors
+  uint64_t* tbase;          // per scan part + 1: the part's base (the last: all survivors)
   uint32_t* perm;           // n: merged position -> input index
   uint32_t* big;            // nc_max: tiles left to merge_big_kernel (their count in mstats[5])
   uint64_t* mstats;         // [0] merged entries [1] candidates (tiles) [3] error flags [5] big tiles
@@ -550,24 +552,46 @@ __global__ __launch_bounds__(kBigTT) void merge_big_kernel(MergeArgs a) {
   }
 }
 
-// One workgroup: exclusive scan of the tile survivor counts (rounds of 1024 threads x 16
-// consecutive tiles).
-__global__ __launch_bounds__(1024) void tile_scan_kernel(MergeArgs a) {
-  constexpr uint32_t kPer = 16;
-  const uint32_t t = threadIdx.x, w = t >> 6;
+// Exclusive scan of the tile survivor counts in two levels (one workgroup over all the tiles
+// took 0.25 ms at config C's 254 K tiles): tscan_part_kernel scans kTScan tiles per workgroup
+// into tpre[] and writes the part's total; tscan_top_kernel scans the parts into tbase[], the
+// bases perm_kernel adds.
+constexpr uint32_t kTScan = 2048;  // tiles per part (256 threads x 8)
+
+__global__ __launch_bounds__(256) void tscan_part_kernel(MergeArgs a) {
+  constexpr uint32_t kPer = kTScan / 256;
+  __shared__ uint32_t ws[4];
   const uint32_t NC = uint32_t(a.mstats[1]);
+  const uint64_t i0 = uint64_t(blockIdx.x) * kTScan + threadIdx.x * kPer;
+  if (uint64_t(blockIdx.x) * kTScan >= NC) return;  // (uniform)
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    v[j] = i0 + j < NC ? a.tcnt[i0 + j] : 0u;
+    sum += v[j];
+  }
+  const uint32_t inc = wave_incl_scan32(sum), w = wave_id();
+  if (lane_id() == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t x = 0; x < w; ++x) run += ws[x];
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    if (i0 + j < NC) a.tpre[i0 + j] = run;
+    run += v[j];
+  }
+  if (threadIdx.x == 0) a.tpart[blockIdx.x] = uint64_t(ws[0]) + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(1024) void tscan_top_kernel(MergeArgs a) {
+  const uint32_t t = threadIdx.x, w = t >> 6;
+  const uint32_t NC = uint32_t(a.mstats[1]), np = (NC + kTScan - 1) / kTScan;
   __shared__ uint64_t wsum[16];
   uint64_t carry = 0;
-  for (uint32_t r = 0; r < NC; r += 1024 * kPer) {
-    const uint32_t i0 = r + t * kPer;
-    uint32_t v[kPer];
-    uint64_t sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-      v[j] = i0 + j < NC ? a.tcnt[i0 + j] : 0u;
-      sum += v[j];
-    }
-    const uint64_t inc = wave_incl_scan<uint64_t>(sum);
+  for (uint32_t r = 0; r < np; r += 1024) {
+    const uint32_t i = r + t;
+    const uint64_t v = i < np ? a.tpart[i] : 0ull;
+    const uint64_t inc = wave_incl_scan<uint64_t>(v);
     if (lane_id() == 63) wsum[w] = inc;
     __syncthreads();
     uint64_t base = carry, tot = carry;
@@ -575,17 +599,12 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(MergeArgs a) {
       if (x < w) base += wsum[x];
       tot += wsum[x];
     }
-    uint64_t run = base + inc - sum;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-      if (i0 + j < NC) a.tpre[i0 + j] = run;
-      run += v[j];
-    }
+    if (i < np) a.tbase[i] = base + inc - v;
     carry = tot;
     __syncthreads();
   }
   if (t == 0) {
-    a.tpre[NC] = carry;
+    a.tbase[np] = carry;
     a.mstats[0] = carry;
   }
 }
@@ -596,7 +615,7 @@ __global__ __launch_bounds__(64) void perm_kernel(MergeArgs a) {
   if (t >= uni(uint32_t(a.mstats[1]))) return;
   tile_ranges(a, H, t);
   wave_sync();
-  const uint64_t base = a.tpre[t];
+  const uint64_t base = a.tpre[t] + a.tbase[t / kTScan];
   const uint32_t cnt = a.tcnt[t];
   for (uint32_t u = lane_id(); u < H.total; u += 64) {
     const uint32_t r = find_run(H.tb, a.nrun, u), g = H.lo[r] + u - H.tb[r];
@@ -635,7 +654,9 @@ struct GatherArgs {
   uint64_t entry_cap, key_cap, val_cap;
   uint32_t* keep;           // n_max
   uint64_t* tile_sum;       // 3 per tile
-  uint64_t* tile_pre;       // 3 per tile
+  uint64_t* tile_pre;       // 3 per tile: exclusive prefix inside its scan part (kGScan tiles)
+  uint64_t* part_sum;       // 3 per scan part
+  uint64_t* part_pre;       // 3 per scan part: the part's base
   uint64_t* stats;          // [0] kept [1] key bytes [2] value bytes [3] error flags
   const uint64_t* merr;     // the merge stage's error flags (bad run table)
   lsmblk_key_range range;   // key-range shard (has_lo / has_hi 0: unbounded)
@@ -798,17 +819,57 @@ __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
   }
 }
 
-__global__ __launch_bounds__(1024) void mscan_kernel(GatherArgs a) {
-  const uint32_t t = threadIdx.x, w = t >> 6;
+// Exclusive scan of the gather tiles' (kept, key bytes, value bytes) in two levels, as the
+// merge's tile scan: parts of kGScan tiles (mscan_part_kernel), then the parts' bases and the
+// totals (mscan_top_kernel); mwrite adds its part's base.
+constexpr uint32_t kGScan = 1024;  // gather tiles per part (256 threads x 4)
+
+__global__ __launch_bounds__(256) void mscan_part_kernel(GatherArgs a) {
+  constexpr uint32_t kPer = kGScan / 256;
+  __shared__ uint64_t ws[4][3];
   const uint64_t N = *a.nm, ntiles = (N + kGTile - 1) / kGTile;
+  const uint64_t i0 = uint64_t(blockIdx.x) * kGScan + threadIdx.x * kPer;
+  if (uint64_t(blockIdx.x) * kGScan >= ntiles) return;  // (uniform)
+  const uint32_t w = wave_id();
+  uint64_t v[kPer][3], sum[3] = {0, 0, 0};
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j)
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+      v[j][q] = i0 + j < ntiles ? a.tile_sum[3 * (i0 + j) + q] : 0ull;
+      sum[q] += v[j][q];
+    }
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    const uint64_t inc = wave_incl_scan<uint64_t>(sum[q]);
+    if (lane_id() == 63) ws[w][q] = inc;
+    sum[q] = inc - sum[q];  // the thread's exclusive prefix inside its wave
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    uint64_t run = sum[q];
+    for (uint32_t x = 0; x < w; ++x) run += ws[x][q];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      if (i0 + j < ntiles) a.tile_pre[3 * (i0 + j) + q] = run;
+      run += v[j][q];
+    }
+    if (threadIdx.x == 0) a.part_sum[3 * uint64_t(blockIdx.x) + q] = ws[0][q] + ws[1][q] + ws[2][q] + ws[3][q];
+  }
+}
+
+__global__ __launch_bounds__(1024) void mscan_top_kernel(GatherArgs a) {
+  const uint32_t t = threadIdx.x, w = t >> 6;
+  const uint64_t N = *a.nm, ntiles = (N + kGTile - 1) / kGTile, np = (ntiles + kGScan - 1) / kGScan;
   __shared__ uint64_t wsum[16][3];
   uint64_t carry[3] = {0, 0, 0};
-  for (uint64_t r = 0; r < ntiles; r += 1024) {
+  for (uint64_t r = 0; r < np; r += 1024) {
     const uint64_t i = r + t;
     uint64_t v[3], inc[3];
 #pragma unroll
     for (uint32_t q = 0; q < 3; ++q) {
-      v[q] = i < ntiles ? a.tile_sum[3 * i + q] : 0ull;
+      v[q] = i < np ? a.part_sum[3 * i + q] : 0ull;
       inc[q] = wave_incl_scan<uint64_t>(v[q]);
       if (lane_id() == 63) wsum[w][q] = inc[q];
     }
@@ -820,7 +881,7 @@ __global__ __launch_bounds__(1024) void mscan_kernel(GatherArgs a) {
         if (x < w) base += wsum[x][q];
         tot += wsum[x][q];
       }
-      if (i < ntiles) a.tile_pre[3 * i + q] = base + inc[q] - v[q];
+      if (i < np) a.part_pre[3 * i + q] = base + inc[q] - v[q];
       carry[q] = tot;
     }
     __syncthreads();
@@ -985,8 +1046,10 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
     vo[r] = iv - vl[r];
   }
   __syncthreads();
-  uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)], a.tile_pre[3 * uint64_t(blockIdx.x) + 1],
-                       a.tile_pre[3 * uint64_t(blockIdx.x) + 2]};
+  const uint64_t gp = blockIdx.x / kGScan;
+  uint64_t carry[3] = {a.tile_pre[3 * uint64_t(blockIdx.x)] + a.part_pre[3 * gp],
+                       a.tile_pre[3 * uint64_t(blockIdx.x) + 1] + a.part_pre[3 * gp + 1],
+                       a.tile_pre[3 * uint64_t(blockIdx.x) + 2] + a.part_pre[3 * gp + 2]};
   uint64_t K0[R + 1], V0[R + 1];
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
@@ -1637,13 +1700,15 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   P.m.sp = cv.take<uint32_t>(n + 1);
   P.m.tcnt = cv.take<uint32_t>(nc_max + 1);
   P.m.tpre = cv.take<uint64_t>(nc_max + 2);
+  P.m.tpart = cv.take<uint64_t>(nc_max / kTScan + 2);
+  P.m.tbase = cv.take<uint64_t>(nc_max / kTScan + 3);
   P.m.perm = cv.take<uint32_t>(n + 1);
   P.m.big = cv.take<uint32_t>(nc_max + 1);
   P.m.mstats = cv.take<uint64_t>(8);
   P.keep = cv.take<uint32_t>(n + 1);
   P.ksame = cv.take<uint8_t>(n + 1);
   P.gtiles = (n + kGTile - 1) / kGTile + 1;
-  P.gtile = cv.take<uint64_t>(6 * P.gtiles);
+  P.gtile = cv.take<uint64_t>(6 * P.gtiles + 6 * (P.gtiles / kGScan + 2));
   P.bytes = cv.off;
   return P;
 }
@@ -1686,7 +1751,8 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   LSM_LAUNCH(bounds_kernel, dim3(uint32_t((nb + 255) / 256)), dim3(256), 0, st, m);
   LSM_LAUNCH(merge_tile_kernel, dim3(nc), dim3(kMTT), 0, st, m);
   LSM_LAUNCH(merge_big_kernel, dim3(std::min(nc, kBigGrid)), dim3(kBigTT), 0, st, m);
-  LSM_LAUNCH(tile_scan_kernel, dim3(1), dim3(1024), 0, st, m);
+  LSM_LAUNCH(tscan_part_kernel, dim3((nc + kTScan - 1) / kTScan), dim3(256), 0, st, m);
+  LSM_LAUNCH(tscan_top_kernel, dim3(1), dim3(1024), 0, st, m);
   LSM_LAUNCH(perm_kernel, dim3(nc), dim3(64), 0, st, m);
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   GatherArgs g;
@@ -1715,6 +1781,8 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   g.keep = P.keep;
   g.tile_sum = P.gtile;
   g.tile_pre = P.gtile + 3 * P.gtiles;
+  g.part_sum = P.gtile + 6 * P.gtiles;
+  g.part_pre = g.part_sum + 3 * (P.gtiles / kGScan + 2);
   g.stats = stats;
   g.merr = m.mstats + 3;
   g.range = range ? *range : lsmblk_key_range{};
@@ -1723,7 +1791,8 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   const uint32_t gt = uint32_t((n + kGTile - 1) / kGTile);
   if (two && rules) LSM_LAUNCH(mgroup_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, g);
   LSM_LAUNCH(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
-  LSM_LAUNCH(mscan_kernel, dim3(1), dim3(1024), 0, st, g);
+  LSM_LAUNCH(mscan_part_kernel, dim3(uint32_t((P.gtiles + kGScan - 1) / kGScan)), dim3(256), 0, st, g);
+  LSM_LAUNCH(mscan_top_kernel, dim3(1), dim3(1024), 0, st, g);
   LSM_LAUNCH(mwrite_kernel, dim3(gt), dim3(256), 0, st, g);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
