@@ -37,7 +37,7 @@ def needs_build(so=SO):
 def _cmd(so, diag):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     return [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-            "-Wall", "-Wno-unused-function", f"-DLSMBLK_DIAG_BUILD={1 if diag else 0}",
+            "-Wall", "-Wshadow", "-Wno-unused-function", f"-DLSMBLK_DIAG_BUILD={1 if diag else 0}",
             "-I" + os.path.join(ROOT, "include"), *SOURCES, "-o", so + ".tmp"]
 
 

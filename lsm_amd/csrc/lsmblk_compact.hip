@@ -104,6 +104,10 @@ struct MergeArgs {
   uint32_t nrun;
   uint32_t nc_max;          // bound on candidates (= tiles)
   uint32_t* cand;           // nc_max: sorted candidate -> input index
+  u32x4* ck;                // nc_max: first 16 key bytes (big-endian words) per candidate, run-major
+  uint32_t* cklen;          // nc_max: its key length
+  u32x4* cks;               // nc_max: ck in sorted candidate order
+  uint32_t* ckslen;
   uint32_t* bounds;         // (nc_max + 1) x nrun: tile t's first entry in run r
   uint32_t* mrank;          // n: in-tile merged rank of a surviving entry, kNone if dropped
   uint32_t* sp;             // n: survivor prefix (tiles too large for LDS)
@@ -157,108 +161,6 @@ __device__ __forceinline__ uint32_t find_run(const uint32_t* v, uint32_t nrun, u
   return lo;
 }
 
-__global__ __launch_bounds__(256) void cand_rank_kernel(MergeArgs a) {
-  __shared__ uint32_t s_rs[kMaxRuns + 1], s_cb[kMaxRuns + 1];
-  load_runs(a, s_rs, s_cb);
-  bool ok = s_rs[0] == 0 && uint64_t(s_rs[a.nrun]) == a.n;
-  for (uint32_t r = 0; r < a.nrun; ++r) ok = ok && s_rs[r] <= s_rs[r + 1];
-  const uint32_t NC = ok ? s_cb[a.nrun] : 0u;  // a bad run table merges nothing
-  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
-  if (c == 0) {
-    a.mstats[1] = NC;
-    if (!ok) atomicOr(reinterpret_cast<unsigned long long*>(a.mstats + 3), (unsigned long long)LSMBLK_ERR_SEGMENTS);
-  }
-  if (c >= NC) return;
-  const GKeys K = gkeys(a.keys, a.key_off[a.n]);
-  const uint32_t r = find_run(s_cb, a.nrun, c), j = c - s_cb[r];
-  const uint32_t p = s_rs[r] + j * kMS;
-  const uint32_t xp = a.key_off[p], xl = a.key_off[p + 1] - xp;
-  uint32_t rank = j;
-  for (uint32_t r2 = 0; r2 < a.nrun; ++r2) {
-    if (r2 == r) continue;
-    // candidates of r2 ordered before (x, r, j): key < x, or key == x and r2 < r
-    uint32_t lo = 0, hi = s_cb[r2 + 1] - s_cb[r2];
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1, q = s_rs[r2] + mid * kMS;
-      const uint32_t qp = a.key_off[q];
-      const int cm = key_cmp(K, qp, a.key_off[q + 1] - qp, xp, xl);
-      if (cm < 0 || (cm == 0 && r2 < r)) lo = mid + 1;
-      else hi = mid;
-    }
-    rank += lo;
-  }
-  a.cand[rank] = p;
-}
-
-__global__ __launch_bounds__(256) void bounds_kernel(MergeArgs a) {
-  __shared__ uint32_t s_rs[kMaxRuns + 1], s_cb[kMaxRuns + 1];
-  load_runs(a, s_rs, s_cb);
-  const uint32_t NC = uint32_t(a.mstats[1]);
-  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  const uint32_t t = uint32_t(i / a.nrun), r = uint32_t(i % a.nrun);
-  if (t > a.nc_max || r >= a.nrun) return;
-  uint32_t* out = a.bounds + uint64_t(t) * a.nrun + r;  // tile-major: a tile's bounds share a line
-  if (t >= NC) {  // (rows past the last tile too: the tile kernels see those tiles empty)
-    *out = s_rs[r + 1];
-    return;
-  }
-  const GKeys K = gkeys(a.keys, a.key_off[a.n]);
-  const uint32_t x = a.cand[t], xp = a.key_off[x], xl = a.key_off[x + 1] - xp;
-  const uint32_t base = s_rs[r], C = s_cb[r + 1] - s_cb[r];
-  uint32_t lo = 0, hi = C;  // first candidate of r with key >= x
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1, q = base + mid * kMS, qp = a.key_off[q];
-    if (key_cmp(K, qp, a.key_off[q + 1] - qp, xp, xl) < 0) lo = mid + 1;
-    else hi = mid;
-  }
-  uint32_t e0 = lo == 0 ? base : base + (lo - 1) * kMS + 1;
-  uint32_t e1 = lo < C ? base + lo * kMS : s_rs[r + 1];
-  while (e0 < e1) {  // first entry in [e0, e1) with key >= x (else e1)
-    const uint32_t mid = (e0 + e1) >> 1, qp = a.key_off[mid];
-    if (key_cmp(K, qp, a.key_off[mid + 1] - qp, xp, xl) < 0) e0 = mid + 1;
-    else e1 = mid;
-  }
-  *out = e0;
-}
-
-struct TileHdr {
-  uint32_t lo[kMaxRuns], tb[kMaxRuns + 1];  // run r's sub-range start; tile index of its first entry
-  uint32_t rsp[kMaxRuns], rsv[kMaxRuns];   // survivors before run r's sub-range / inside it
-  uint32_t total, nsurv;
-  uint32_t wsum[kBigTT / 64];
-};
-template <uint32_t E>
-struct alignas(16) MTileLdsT {
-  TileHdr h;
-  u32x4 kw[E];          // first 16 key bytes as big-endian words, zero padded
-  uint32_t klen[E];
-  uint16_t sp[E + 1];   // survivor prefix over the tile (run-major order)
-  uint8_t surv[E];
-};
-using MTileLds = MTileLdsT<kMTE>;
-using MTileBigLds = MTileLdsT<kBigTE>;
-
-// The tile's per-run sub-ranges (wave 0; lane r = run r).
-__device__ __forceinline__ void tile_ranges(const MergeArgs& a, TileHdr& H, uint32_t t) {
-  const uint32_t l = lane_id();
-  uint32_t lo = 0, hi = 0;
-  if (l < a.nrun) {
-    const uint32_t* row = a.bounds + uint64_t(t) * a.nrun;
-    lo = row[l];
-    hi = row[a.nrun + l];
-    if (hi < lo) hi = lo;  // only with unsorted runs (output then unspecified, flagged by mflag)
-  }
-  const uint32_t m = hi - lo, mi = wave_incl_scan32(m);
-  if (l < a.nrun) {
-    H.lo[l] = lo;
-    H.tb[l] = mi - m;
-  }
-  if (l == 63) {
-    H.total = mi;
-    H.tb[a.nrun] = mi;
-  }
-}
-
 // First 16 bytes of the key at arena position pos (len bytes) as big-endian words, zero padded:
 // five aligned dword loads through the descriptor (none straddles its bound) and alignbytes.
 __device__ __forceinline__ u32x4 key16(const GKeys& G, uint32_t pos, uint32_t len) {
@@ -287,6 +189,128 @@ __device__ __forceinline__ int kcmp16(const MergeArgs& a, const GKeys& G, const 
   if (x.w != y.w) return x.w < y.w ? -1 : 1;
   if (xl <= 16 || yl <= 16) return xl < yl ? -1 : (xl > yl ? 1 : 0);
   return key_cmp(G, a.key_off[xg] + 16, xl - 16, a.key_off[yg] + 16, yl - 16);
+}
+
+// Every candidate's first 16 key bytes and length, in run-major candidate order (ck, cklen): the
+// rank and bound searches below then read one 16-B word per step instead of an offset and then
+// the key bytes (two dependent round trips).
+__global__ __launch_bounds__(256) void cand_key_kernel(MergeArgs a) {
+  __shared__ uint32_t s_rs[kMaxRuns + 1], s_cb[kMaxRuns + 1];
+  load_runs(a, s_rs, s_cb);
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= s_cb[a.nrun] || c >= a.nc_max) return;
+  const uint32_t r = find_run(s_cb, a.nrun, c), p = s_rs[r] + (c - s_cb[r]) * kMS;
+  if (p >= a.n) return;  // (a bad run table: cand_rank_kernel merges nothing)
+  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
+  const uint32_t kp = a.key_off[p], kl = a.key_off[p + 1] - kp;
+  a.ck[c] = key16(G, kp, kl);
+  a.cklen[c] = kl;
+}
+
+__global__ __launch_bounds__(256) void cand_rank_kernel(MergeArgs a) {
+  __shared__ uint32_t s_rs[kMaxRuns + 1], s_cb[kMaxRuns + 1];
+  load_runs(a, s_rs, s_cb);
+  bool ok = s_rs[0] == 0 && uint64_t(s_rs[a.nrun]) == a.n;
+  for (uint32_t r = 0; r < a.nrun; ++r) ok = ok && s_rs[r] <= s_rs[r + 1];
+  const uint32_t NC = ok ? s_cb[a.nrun] : 0u;  // a bad run table merges nothing
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c == 0) {
+    a.mstats[1] = NC;
+    if (!ok) atomicOr(reinterpret_cast<unsigned long long*>(a.mstats + 3), (unsigned long long)LSMBLK_ERR_SEGMENTS);
+  }
+  if (c >= NC) return;
+  const GKeys K = gkeys(a.keys, a.key_off[a.n]);
+  const uint32_t r = find_run(s_cb, a.nrun, c), j = c - s_cb[r];
+  const uint32_t p = s_rs[r] + j * kMS;
+  const u32x4 x = a.ck[c];
+  const uint32_t xl = a.cklen[c];
+  uint32_t rank = j;
+  for (uint32_t r2 = 0; r2 < a.nrun; ++r2) {
+    if (r2 == r) continue;
+    // candidates of r2 ordered before (x, r, j): key < x, or key == x and r2 < r
+    uint32_t lo = 0, hi = s_cb[r2 + 1] - s_cb[r2];
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1, q = s_cb[r2] + mid;
+      const int cm = kcmp16(a, K, a.ck[q], a.cklen[q], s_rs[r2] + mid * kMS, x, xl, p);
+      if (cm < 0 || (cm == 0 && r2 < r)) lo = mid + 1;
+      else hi = mid;
+    }
+    rank += lo;
+  }
+  a.cand[rank] = p;
+  a.cks[rank] = x;
+  a.ckslen[rank] = xl;
+}
+
+__global__ __launch_bounds__(256) void bounds_kernel(MergeArgs a) {
+  __shared__ uint32_t s_rs[kMaxRuns + 1], s_cb[kMaxRuns + 1];
+  load_runs(a, s_rs, s_cb);
+  const uint32_t NC = uint32_t(a.mstats[1]);
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint32_t t = uint32_t(i / a.nrun), r = uint32_t(i % a.nrun);
+  if (t > a.nc_max || r >= a.nrun) return;
+  uint32_t* out = a.bounds + uint64_t(t) * a.nrun + r;  // tile-major: a tile's bounds share a line
+  if (t >= NC) {  // (rows past the last tile too: the tile kernels see those tiles empty)
+    *out = s_rs[r + 1];
+    return;
+  }
+  const GKeys K = gkeys(a.keys, a.key_off[a.n]);
+  const uint32_t x = a.cand[t], xl = a.ckslen[t];
+  const u32x4 xk = a.cks[t];
+  const uint32_t base = s_rs[r], C = s_cb[r + 1] - s_cb[r];
+  uint32_t lo = 0, hi = C;  // first candidate of r with key >= x
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1, q = s_cb[r] + mid;
+    if (kcmp16(a, K, a.ck[q], a.cklen[q], base + mid * kMS, xk, xl, x) < 0) lo = mid + 1;
+    else hi = mid;
+  }
+  uint32_t e0 = lo == 0 ? base : base + (lo - 1) * kMS + 1;
+  uint32_t e1 = lo < C ? base + lo * kMS : s_rs[r + 1];
+  const uint32_t xp = a.key_off[x];
+  while (e0 < e1) {  // first entry in [e0, e1) with key >= x (else e1)
+    const uint32_t mid = (e0 + e1) >> 1, qp = a.key_off[mid];
+    if (key_cmp(K, qp, a.key_off[mid + 1] - qp, xp, xl) < 0) e0 = mid + 1;
+    else e1 = mid;
+  }
+  *out = e0;
+}
+
+struct TileHdr {
+  uint32_t lo[kMaxRuns], tb[kMaxRuns + 1];  // run r's sub-range start; tile index of its first entry
+  uint32_t rsp[kMaxRuns];                  // survivors before run r's sub-range
+  uint32_t total, nsurv;
+  uint32_t wsum[kBigTT / 64];
+};
+template <uint32_t E>
+struct alignas(16) MTileLdsT {
+  TileHdr h;
+  u32x4 kw[E];          // first 16 key bytes as big-endian words, zero padded
+  uint16_t klen[E];        // (key lengths are u16 in the block format)
+  uint16_t sp[E + 1];   // survivor prefix over the tile (run-major order)
+  uint8_t surv[E];
+};
+using MTileLds = MTileLdsT<kMTE>;
+using MTileBigLds = MTileLdsT<kBigTE>;
+
+// The tile's per-run sub-ranges (wave 0; lane r = run r).
+__device__ __forceinline__ void tile_ranges(const MergeArgs& a, TileHdr& H, uint32_t t) {
+  const uint32_t l = lane_id();
+  uint32_t lo = 0, hi = 0;
+  if (l < a.nrun) {
+    const uint32_t* row = a.bounds + uint64_t(t) * a.nrun;
+    lo = row[l];
+    hi = row[a.nrun + l];
+    if (hi < lo) hi = lo;  // only with unsorted runs (output then unspecified, flagged by mflag)
+  }
+  const uint32_t m = hi - lo, mi = wave_incl_scan32(m);
+  if (l < a.nrun) {
+    H.lo[l] = lo;
+    H.tb[l] = mi - m;
+  }
+  if (l == 63) {
+    H.total = mi;
+    H.tb[a.nrun] = mi;
+  }
 }
 
 // Two-level mode: b's last key, where the reference's stream ends.  In a key-range shard
@@ -321,11 +345,11 @@ __device__ __forceinline__ void load_tile_keys(const MergeArgs& a, MTileLdsT<E>&
     const uint32_t r = find_run(H.tb, a.nrun, u), g = H.lo[r] + u - H.tb[r];
     const uint32_t p = a.key_off[g], len = a.key_off[g + 1] - p;
     L.kw[u] = key16(G, p, len);
-    L.klen[u] = len;
+    L.klen[u] = uint16_t(len);
   }
 }
 
-// Survivor prefix over the tile (L.sp, H.nsurv, H.rsp, H.rsv) from L.surv.
+// Survivor prefix over the tile (L.sp, H.nsurv, H.rsp) from L.surv.
 template <uint32_t E, uint32_t T>
 __device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLdsT<E>& L) {
   TileHdr& H = L.h;
@@ -354,7 +378,6 @@ __device__ __forceinline__ void tile_survivor_prefix(const MergeArgs& a, MTileLd
   __syncthreads();
   if (tid < nrun) {
     H.rsp[tid] = L.sp[H.tb[tid]];
-    H.rsv[tid] = L.sp[H.tb[tid + 1]] - L.sp[H.tb[tid]];
   }
   __syncthreads();
 }
@@ -425,7 +448,7 @@ __device__ void merge_tile_lds(const MergeArgs& a, MTileLdsT<E>& L, uint32_t t) 
 // Global path (a tile of more than kMTE entries: many versions of one key, or many runs), one
 // wave: keys compared in global memory, survival kept in mrank[] and the survivor prefix in
 // sp[], handed between lanes through L2 (sc1 stores / loads, drained with vmcnt(0)).
-__device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
+__device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t* rsv, uint32_t t) {  // rsv: LDS, kMaxRuns
   const uint32_t l = lane_id(), nrun = a.nrun, total = H.total;
   const GKeys G = gkeys(a.keys, a.key_off[a.n]);
   auto kpos = [&](uint32_t r, uint32_t k, uint32_t& len) -> uint32_t {
@@ -497,7 +520,7 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
   if (l < nrun) {
     const uint32_t b0 = sp_at(H.tb[l]), b1 = sp_at(H.tb[l + 1]);
     H.rsp[l] = b0;
-    H.rsv[l] = b1 - b0;
+    rsv[l] = b1 - b0;
   }
   wave_sync();
   for (uint32_t u = l; u < total; u += 64) {  // phase B: rank
@@ -511,7 +534,7 @@ __device__ void merge_tile_global(const MergeArgs& a, TileHdr& H, uint32_t t) {
         const uint32_t m2 = H.tb[r2 + 1] - H.tb[r2];
         if (r2 == r || m2 == 0) continue;
         const uint32_t p = bound(r2, xp, xl, a.two && r2 == B);
-        rank += p == m2 ? H.rsv[r2] : ld(a.sp + H.lo[r2] + p) - H.rsp[r2];
+        rank += p == m2 ? rsv[r2] : ld(a.sp + H.lo[r2] + p) - H.rsp[r2];
       }
     }
     a.mrank[g] = rank;  // each lane reads and rewrites only its own entries' words here
@@ -541,13 +564,14 @@ __global__ __launch_bounds__(kMTT) void merge_tile_kernel(MergeArgs a) {
 // list, LDS tables up to kBigTE entries, the one-wave global path beyond.
 __global__ __launch_bounds__(kBigTT) void merge_big_kernel(MergeArgs a) {
   __shared__ MTileBigLds L;
+  __shared__ uint32_t rsv[kMaxRuns];  // the global path's per-run survivor counts
   const uint32_t nb = uni(uint32_t(a.mstats[5]));
   for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
     const uint32_t t = a.big[i];
     if (threadIdx.x < 64) tile_ranges(a, L.h, t);
     __syncthreads();
     if (L.h.total <= kBigTE) merge_tile_lds<kBigTE, kBigTT>(a, L, t);
-    else if (threadIdx.x < 64) merge_tile_global(a, L.h, t);
+    else if (threadIdx.x < 64) merge_tile_global(a, L.h, rsv, t);
     __syncthreads();
   }
 }
@@ -696,30 +720,25 @@ __device__ __forceinline__ bool same_key_g(const GatherArgs& a, uint32_t i, uint
   return true;
 }
 
-// The merged order must be non-decreasing in the user key: an unsorted input run (which
-// MergeIterator assumes away, merge_iterator.rs:135-138) is reported, never followed.
-__device__ __forceinline__ bool merged_in_order(const GatherArgs& a, uint64_t j) {
-  const uint32_t i = a.perm[j];
-  if (i >= a.n_max) return false;
-  if (j == 0) return true;
-  const uint32_t ip = a.perm[j - 1];
-  if (ip >= a.n_max) return false;
-  const GKeys K = gkeys(a.keys, a.key_off[a.n_max]);
-  const uint32_t p0 = a.key_off[ip], p1 = a.key_off[i];
-  return key_cmp(K, p0, a.key_off[ip + 1] - p0, p1, a.key_off[i + 1] - p1) <= 0;
+// Byte order of the keys at arena positions (pa, la) and (pb, lb): their first 16 bytes by one
+// round of descriptor loads each decide unless equal with both keys longer (then the tails).
+__device__ __forceinline__ int key_cmp16(const GKeys& G, uint32_t pa, uint32_t la, uint32_t pb, uint32_t lb) {
+  const u32x4 x = key16(G, pa, la), y = key16(G, pb, lb);
+  if (x.x != y.x) return x.x < y.x ? -1 : 1;
+  if (x.y != y.y) return x.y < y.y ? -1 : 1;
+  if (x.z != y.z) return x.z < y.z ? -1 : 1;
+  if (x.w != y.w) return x.w < y.w ? -1 : 1;
+  if (la <= 16 || lb <= 16) return la < lb ? -1 : (la > lb ? 1 : 0);
+  return key_cmp(G, pa + 16, la - 16, pb + 16, lb - 16);
 }
 
-__device__ __forceinline__ bool mkeep(const GatherArgs& a, uint64_t j) {
+// mkeep with the merged predecessor ip's key compare already done (same: equal user keys).
+__device__ __forceinline__ bool mkeep(const GatherArgs& a, uint64_t j, uint32_t i, uint32_t ip, bool same) {
   if (!a.rules) return true;
-  const uint32_t i = a.perm[j];
   const uint64_t t = a.ts[i];
   if (t > a.wm) return true;
-  bool start = true;
-  if (j > 0) {
-    const uint32_t ip = a.perm[j - 1];
-    start = !same_key_g(a, ip, i);
-    if (!start && a.ts[ip] <= a.wm) return false;  // a later version at or below the watermark
-  }
+  const bool start = !(j > 0 && same);
+  if (!start && a.ts[ip] <= a.wm) return false;  // a later version at or below the watermark
   if (a.bottom && start && a.val_off[i + 1] == a.val_off[i]) return false;  // :244-254
   const uint32_t k0 = a.key_off[i], kl = a.key_off[i + 1] - k0;
   for (uint32_t f = 0; f < a.npfx; ++f) {  // CompactionFilter::Prefix, :264-275
@@ -779,6 +798,7 @@ __global__ __launch_bounds__(256) void mgroup_kernel(GatherArgs a) {
 
 __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
   const uint64_t N = *a.nm;
+  const GKeys G = gkeys(a.keys, a.key_off[a.n_max]);
   uint32_t c = 0;
   uint64_t kb = 0, vb = 0;
 #pragma unroll
@@ -787,20 +807,30 @@ __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
     if (j < N) {
       bool k = false;
       uint32_t same = 0;
-      if (merged_in_order(a, j)) {
+      // the merged order must be non-decreasing in the user key: an unsorted input run (which
+      // MergeIterator assumes away, merge_iterator.rs:135-138) is reported, never followed.  One
+      // compare with the merged predecessor gives the order and the rules' same-key test.
+      const uint32_t i = a.perm[j], ip = j > 0 ? a.perm[j - 1] : 0u;
+      bool ordered = i < a.n_max && ip < a.n_max;
+      int cmp = -1;
+      if (ordered && j > 0) {
+        const uint32_t p0 = a.key_off[ip], p1 = a.key_off[i];
+        cmp = key_cmp16(G, p0, a.key_off[ip + 1] - p0, p1, a.key_off[i + 1] - p1);
+        ordered = cmp <= 0;
+      }
+      if (ordered) {
         if (a.two && a.rules) {
           const uint32_t g = a.keep[j];
-          k = (g & 1u) && in_range(a, a.perm[j]);
+          k = (g & 1u) && in_range(a, i);
           same = g & 2u;
         } else {
-          k = in_range(a, a.perm[j]) && mkeep(a, j);
+          k = in_range(a, i) && mkeep(a, j, i, ip, cmp == 0);
         }
       } else {
         atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)LSMBLK_ERR_MALFORMED);
       }
       a.keep[j] = (k ? 1u : 0u) | same;
       if (k) {
-        const uint32_t i = a.perm[j];
         c += 1;
         kb += a.key_off[i + 1] - a.key_off[i];
         vb += a.val_off[i + 1] - a.val_off[i];
@@ -1695,6 +1725,10 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   const uint32_t nc_max = uint32_t(n / kMS + nrun + 1);
   P.m.nc_max = nc_max;
   P.m.cand = cv.take<uint32_t>(nc_max + 1);
+  P.m.ck = cv.take<u32x4>(nc_max + 1);
+  P.m.cklen = cv.take<uint32_t>(nc_max + 1);
+  P.m.cks = cv.take<u32x4>(nc_max + 1);
+  P.m.ckslen = cv.take<uint32_t>(nc_max + 1);
   P.m.bounds = cv.take<uint32_t>(uint64_t(nrun) * (nc_max + 1));
   P.m.mrank = cv.take<uint32_t>(n + 1);
   P.m.sp = cv.take<uint32_t>(n + 1);
@@ -1746,6 +1780,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   }
   if (hipMemsetAsync(m.mstats, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t nc = m.nc_max;
+  LSM_LAUNCH(cand_key_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   LSM_LAUNCH(cand_rank_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   const uint64_t nb = (uint64_t(nc) + 1) * nrun;
   LSM_LAUNCH(bounds_kernel, dim3(uint32_t((nb + 255) / 256)), dim3(256), 0, st, m);

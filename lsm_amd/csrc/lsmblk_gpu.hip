@@ -822,11 +822,11 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
     } else if (big) {
       uint64_t kr = 0, vr = 0;
       for (uint32_t c0 = 0; c0 < h.n; c0 += kDecMaxE) {
-        const uint32_t cn = min(kDecMaxE, h.n - c0);
+        const uint32_t nc = min(kDecMaxE, h.n - c0);
         wave_sync();  // the previous chunk's table reads are done
-        parse_tables(GlbImg{R, lead}, c0, cn, kr, vr);
+        parse_tables(GlbImg{R, lead}, c0, nc, kr, vr);
         wave_sync();
-        dec_big_outputs(a, T, R, lead, h, cn, E0 + c0, K0, V0, uint32_t(K), uint32_t(V), reinterpret_cast<uint32_t*>(L.out));
+        dec_big_outputs(a, T, R, lead, h, nc, E0 + c0, K0, V0, uint32_t(K), uint32_t(V), reinterpret_cast<uint32_t*>(L.out));
       }
     } else if (fits) {
       dec_simple_outputs(a, LdsImg{L.img, lead}, h, E0, K0, V0);
@@ -1928,8 +1928,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
           for (uint32_t q = 16; !done && q < m; q += 4) {
             const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
             if (x) {
-              const uint32_t z = q + (__builtin_ctz(x) >> 3);
-              p = z < m ? z : m;
+              const uint32_t zq = q + (__builtin_ctz(x) >> 3);
+              p = zq < m ? zq : m;
               done = true;
             }
           }
@@ -1950,7 +1950,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         {
           const uint32_t vdb = olead + pos + 14 + sfx;  // image byte of the value
           const uint32_t srcb = vlead + vp - vdb;       // + image byte = staged byte (mod 2^32)
-          for (uint32_t c = (vdb + 15) >> 4; 16 * c + 16 <= vdb + vl; ++c) L.cent[c] = srcb + 16 * c;
+          for (uint32_t cc = (vdb + 15) >> 4; 16 * cc + 16 <= vdb + vl; ++cc) L.cent[cc] = srcb + 16 * cc;
         }
       }
     }
@@ -2253,7 +2253,7 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
       // land the chunk at S + lead; the lead bytes before it (lane l0's window reaches them) and
       // the t < 4 bytes after it (up to the next 4-aligned byte: crc_chunk's aligned windows)
       // are zeroed in registers first
-      const uint32_t P = lead + sz, t = (0u - P) & 3u;
+      const uint32_t P = lead + sz, tz = (0u - P) & 3u;  // zero bytes after the chunk
       if (l == 0) {
         uint32_t* v = reinterpret_cast<uint32_t*>(&q[0]);
 #pragma unroll
@@ -2262,7 +2262,7 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
           v[d] &= z <= 0 ? ~0u : z >= 4 ? 0u : ~0u << (8 * z);
         }
       }
-      if (t && l == ((P >> 4) & 63)) {
+      if (tz && l == ((P >> 4) & 63)) {
 #pragma unroll
         for (uint32_t i = 0; i < 5; ++i) {
           if (i != (P >> 10)) continue;
@@ -2288,7 +2288,7 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
         if (more || has_next) issue(uni64(ncs), uni(nsz));
       }
       if (nch) {
-        const uint32_t part = crc_chunk(T, S + lead, sz, c == 0, t);
+        const uint32_t part = crc_chunk(T, S + lead, sz, c == 0, tz);
         acc = c == 0 ? part : crc_apply(T.shift[6], acc) ^ part;
       }
       if (COUNT && nch <= 1) count_block(LdsImg{S, lead}, len, len_ok, a.agg + 3 * b, err);

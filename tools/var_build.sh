@@ -4,6 +4,6 @@
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-function -DLSMBLK_DIAG_BUILD=${DIAG:-0} "$@" -Iinclude \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wshadow -Wno-unused-function -DLSMBLK_DIAG_BUILD=${DIAG:-0} "$@" -Iinclude \
   lsm_amd/csrc/lsmblk_gpu.hip lsm_amd/csrc/lsmblk_compact.hip lsm_amd/csrc/lsmblk_sst.hip lsm_amd/csrc/lsmblk_host.cpp \
   -o lsm_amd/var_$NAME.so
