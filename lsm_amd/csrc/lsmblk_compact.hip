@@ -1360,7 +1360,10 @@ constexpr uint32_t kRotPer = 4;
 __global__ __launch_bounds__(256) void rot_double_kernel(RotArgs a, uint32_t k) {
   if (!*(volatile uint32_t*)(a.need + k - 1)) return;  // every chain done one level down
   const uint64_t n = rot_n(a);
-  const uint64_t s0 = uint64_t(blockIdx.x) * 256 * kRotPer + threadIdx.x;
+  // (XCD-aware tile order: the gathers J_{k-1}(s) land a few tiles ahead, on the same XCD, whose
+  // L2 then serves both them and that tile's own linear read -- 1.84 -> 1.61 ms on config C; the
+  // same order made rot_next and rot_f slower, 0.55 -> 0.62 and 0.54 -> 0.57 ms)
+  const uint64_t s0 = uint64_t(xcd_tile(blockIdx.x, gridDim.x)) * 256 * kRotPer + threadIdx.x;
   const uint64_t N1 = a.n_max + 1;
   const u32x2* L0 = a.JS + (k - 1) * N1;
   bool short_chain = false;

@@ -32,6 +32,15 @@ __device__ __forceinline__ uint32_t diag_mask(uint32_t skip) { return kDiag ? sk
 // ---------------------------------------------------------------- wave primitives
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// XCD-aware tile order: workgroup b runs on XCD b mod 8 (dispatch is round-robin over the eight
+// XCDs, each with its own L2); tile xcd_tile(b) gives XCD x the contiguous tiles
+// [x q + min(x, r), ...) of the G = 8 q + r, so kernels whose tiles read their neighbours' data
+// (windows, near gathers) find it in their own XCD's L2.  A bijection on [0, G).
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t G) {
+  const uint32_t x = b & 7, i = b >> 3, q = G >> 3, r = G & 7;
+  return x * q + (x < r ? x : r) + i;
+}
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return (uint64_t(uni(uint32_t(x >> 32))) << 32) | uni(uint32_t(x));
 }
