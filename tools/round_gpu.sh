@@ -1,8 +1,8 @@
 #!/bin/bash
 # GPU-box: parity tests -> full bench (cpu baseline + pcie) -> rocprof stats -> PMC traffic passes.
-# usage: tools/round_gpu.sh TAG
+# usage: tools/round_gpu.sh TAG COMMIT [--no-pmc]   (the box has no .git: COMMIT stamps traffic.json)
 set -o pipefail
-TAG=$1; shift
+TAG=$1; COMMIT=$2; shift 2
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -17,6 +17,6 @@ for cfg in M C; do
 done
 head -6 gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -d, -f1-4
 if [ "$1" != "--no-pmc" ]; then
-  bash tools/traffic.sh gpurun_out/traffic_$TAG.json || exit 1
+  bash tools/traffic.sh gpurun_out/traffic_$TAG.json "$COMMIT" U Z M C || exit 1
   cat gpurun_out/traffic_$TAG.json
 fi
