@@ -29,8 +29,10 @@ SLOTS = {"decode": ["decode_lag_kernel"], "dec_count": ["dec_count_staged_kernel
 
 
 def short(name):
-    """Kernel function name without namespace, return type and argument list."""
-    n = re.sub(r"\(.*$", "", name.split("(anonymous namespace)::")[-1] if "(" in name else name)
+    """Kernel function name without namespace, return type and argument list
+    ("(anonymous namespace)::decode_lag_kernel((anonymous namespace)::DecodeArgs)" ->
+    "decode_lag_kernel")."""
+    n = re.sub(r"\(.*$", "", name.replace("(anonymous namespace)::", ""))
     n = n.split("::")[-1]
     return n.replace("void ", "").strip()
 
