@@ -103,6 +103,7 @@ struct MergeArgs {
   const uint32_t* run_start;
   uint32_t nrun;
   uint32_t nc_max;          // bound on candidates (= tiles)
+  const u32x4* k16;         // n: every input key's first 16 bytes as big-endian words (key16_kernel)
   uint32_t* cand;           // nc_max: sorted candidate -> input index
   u32x4* ck;                // nc_max: first 16 key bytes (big-endian words) per candidate, run-major
   uint32_t* cklen;          // nc_max: its key length
@@ -191,6 +192,18 @@ __device__ __forceinline__ int kcmp16(const MergeArgs& a, const GKeys& G, const 
   return key_cmp(G, a.key_off[xg] + 16, xl - 16, a.key_off[yg] + 16, yl - 16);
 }
 
+// Every input key's first 16 bytes, once, in entry order (coalesced: the key arena is read front
+// to back): the merge tiles, the bound searches and the rules then read one 16-B word per key in
+// the same round trip as its offsets, instead of the offsets and then the key bytes.
+__global__ __launch_bounds__(256) void key16_kernel(const uint8_t* keys, const uint32_t* key_off, uint64_t n,
+                                                    u32x4* k16) {
+  const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= n) return;
+  const GKeys G = gkeys(keys, key_off[n]);
+  const uint32_t p = key_off[e];
+  k16[e] = key16(G, p, key_off[e + 1] - p);
+}
+
 // Every candidate's first 16 key bytes and length, in run-major candidate order (ck, cklen): the
 // rank and bound searches below then read one 16-B word per step instead of an offset and then
 // the key bytes (two dependent round trips).
@@ -201,10 +214,8 @@ __global__ __launch_bounds__(256) void cand_key_kernel(MergeArgs a) {
   if (c >= s_cb[a.nrun] || c >= a.nc_max) return;
   const uint32_t r = find_run(s_cb, a.nrun, c), p = s_rs[r] + (c - s_cb[r]) * kMS;
   if (p >= a.n) return;  // (a bad run table: cand_rank_kernel merges nothing)
-  const GKeys G = gkeys(a.keys, a.key_off[a.n]);
-  const uint32_t kp = a.key_off[p], kl = a.key_off[p + 1] - kp;
-  a.ck[c] = key16(G, kp, kl);
-  a.cklen[c] = kl;
+  a.ck[c] = a.k16[p];
+  a.cklen[c] = a.key_off[p + 1] - a.key_off[p];
 }
 
 __global__ __launch_bounds__(256) void cand_rank_kernel(MergeArgs a) {
@@ -266,10 +277,9 @@ __global__ __launch_bounds__(256) void bounds_kernel(MergeArgs a) {
   }
   uint32_t e0 = lo == 0 ? base : base + (lo - 1) * kMS + 1;
   uint32_t e1 = lo < C ? base + lo * kMS : s_rs[r + 1];
-  const uint32_t xp = a.key_off[x];
   while (e0 < e1) {  // first entry in [e0, e1) with key >= x (else e1)
-    const uint32_t mid = (e0 + e1) >> 1, qp = a.key_off[mid];
-    if (key_cmp(K, qp, a.key_off[mid + 1] - qp, xp, xl) < 0) e0 = mid + 1;
+    const uint32_t mid = (e0 + e1) >> 1;
+    if (kcmp16(a, K, a.k16[mid], a.key_off[mid + 1] - a.key_off[mid], mid, xk, xl, x) < 0) e0 = mid + 1;
     else e1 = mid;
   }
   *out = e0;
@@ -343,9 +353,8 @@ __device__ __forceinline__ void load_tile_keys(const MergeArgs& a, MTileLdsT<E>&
   const TileHdr& H = L.h;
   for (uint32_t u = threadIdx.x; u < H.total; u += T) {
     const uint32_t r = find_run(H.tb, a.nrun, u), g = H.lo[r] + u - H.tb[r];
-    const uint32_t p = a.key_off[g], len = a.key_off[g + 1] - p;
-    L.kw[u] = key16(G, p, len);
-    L.klen[u] = uint16_t(len);
+    L.kw[u] = a.k16[g];
+    L.klen[u] = uint16_t(a.key_off[g + 1] - a.key_off[g]);
   }
 }
 
@@ -664,6 +673,7 @@ struct GatherArgs {
   const uint32_t* val_off;
   const uint64_t* ts;
   const uint32_t* perm;
+  const u32x4* k16;         // n_max: the input keys' first 16 bytes (key16_kernel)
   const uint64_t* nm;       // device: merged entries
   uint64_t n_max;           // bound on merged entries (grid)
   uint32_t rules;           // 0: keep all; 1: compaction rules
@@ -722,10 +732,10 @@ __device__ __forceinline__ bool same_key_g(const GatherArgs& a, uint32_t i, uint
   return true;
 }
 
-// Byte order of the keys at arena positions (pa, la) and (pb, lb): their first 16 bytes by one
-// round of descriptor loads each decide unless equal with both keys longer (then the tails).
-__device__ __forceinline__ int key_cmp16(const GKeys& G, uint32_t pa, uint32_t la, uint32_t pb, uint32_t lb) {
-  const u32x4 x = key16(G, pa, la), y = key16(G, pb, lb);
+// Byte order of the keys at arena positions (pa, la) and (pb, lb), x / y their first 16 bytes
+// (k16): those decide unless equal with both keys longer (then the tails, in global memory).
+__device__ __forceinline__ int key_cmp16(const GKeys& G, const u32x4& x, uint32_t pa, uint32_t la, const u32x4& y,
+                                         uint32_t pb, uint32_t lb) {
   if (x.x != y.x) return x.x < y.x ? -1 : 1;
   if (x.y != y.y) return x.y < y.y ? -1 : 1;
   if (x.z != y.z) return x.z < y.z ? -1 : 1;
@@ -817,7 +827,7 @@ __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
       int cmp = -1;
       if (ordered && j > 0) {
         const uint32_t p0 = a.key_off[ip], p1 = a.key_off[i];
-        cmp = key_cmp16(G, p0, a.key_off[ip + 1] - p0, p1, a.key_off[i + 1] - p1);
+        cmp = key_cmp16(G, a.k16[ip], p0, a.key_off[ip + 1] - p0, a.k16[i], p1, a.key_off[i + 1] - p1);
         ordered = cmp <= 0;
       }
       if (ordered) {
@@ -1729,6 +1739,7 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   Carve cv{base};
   const uint32_t nc_max = uint32_t(n / kMS + nrun + 1);
   P.m.nc_max = nc_max;
+  P.m.k16 = cv.take<u32x4>(n + 1);
   P.m.cand = cv.take<uint32_t>(nc_max + 1);
   P.m.ck = cv.take<u32x4>(nc_max + 1);
   P.m.cklen = cv.take<uint32_t>(nc_max + 1);
@@ -1785,6 +1796,8 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   }
   if (hipMemsetAsync(m.mstats, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t nc = m.nc_max;
+  LSM_LAUNCH(key16_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, m.keys, m.key_off, n,
+             const_cast<u32x4*>(m.k16));
   LSM_LAUNCH(cand_key_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   LSM_LAUNCH(cand_rank_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   const uint64_t nb = (uint64_t(nc) + 1) * nrun;
@@ -1802,6 +1815,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   g.val_off = in->val_off;
   g.ts = in->ts;
   g.perm = m.perm;
+  g.k16 = m.k16;
   g.nm = m.mstats;
   g.n_max = n;
   g.rules = rules;
