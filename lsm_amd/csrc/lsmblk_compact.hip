@@ -698,6 +698,7 @@ struct GatherArgs {
   lsmblk_key_range range;   // key-range shard (has_lo / has_hi 0: unbounded)
   uint32_t two;             // two-level merge order: the rules run as the loop (mgroup_kernel)
   uint8_t* ksame;           // two-level: per kept entry, the loop's same_as_last_key (or null)
+  uint32_t* kidx;           // per kept entry, its input index (or null)
 };
 
 // Byte order of key (x, xl) against a range bound (y, yl) in device memory: -1, 0, 1.
@@ -1045,6 +1046,10 @@ constexpr uint32_t kGVImg = 28672;  // LDS image of a round's values
 // The tile's four rounds load their entry metadata (keep -> perm -> offsets, ts) up front, so the
 // tile waits out those two dependent round trips once instead of once per round: rounds that
 // each waited keep -> perm -> offsets -> bytes held the kernel at about half the HBM rate.
+// META: the kept entries' offsets, ts, same-key flags (and kidx); BYTES: their key and value
+// bytes.  lsmblk_compact_batch runs the two halves apart (META first, then BYTES beside the SST
+// rotation, which needs only the metadata); every other caller runs both in one launch.
+template <bool META, bool BYTES>
 __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
   if (a.stats[3]) return;
   const uint64_t N = *a.nm;
@@ -1107,13 +1112,15 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
     V0[r] = carry[2];
 #pragma unroll
     for (uint32_t q = 0; q < 3; ++q) carry[q] += ws[r][0][q] + ws[r][1][q] + ws[r][2][q] + ws[r][3][q];
-    if (kf[r] & 1u) {
+    if (META && (kf[r] & 1u)) {
       a.okey_off[o[r]] = uint32_t(ko[r]);
       a.oval_off[o[r]] = uint32_t(vo[r]);
       a.ots[o[r]] = tsv[r];
       if (a.ksame) a.ksame[o[r]] = uint8_t(kf[r] >> 1);
+      if (a.kidx) a.kidx[o[r]] = ix[r];
     }
   }
+  if (!BYTES) return;
   K0[R] = carry[1];
   V0[R] = carry[2];
   // the copy rounds, not unrolled (each round's copy loop holds 8 x 16 B of loads per lane):
@@ -1221,6 +1228,14 @@ struct RotArgs {
   uint64_t* sstate;         // kShardWords: the carry step's result
   const uint8_t* ksame;     // two-level merge: same_as_last_key per entry from the rules loop
                             // (null: a key equal to its predecessor's)
+  // lsmblk_compact_batch: the kept stream's key bytes are written beside the rotation, so rot_adj
+  // reads each kept key in the merge input instead: kidx[e] = its input index, k16 = the input
+  // keys' first 16 bytes, akeys / akey_off = the input key arena (kidx null: the kept stream)
+  const uint32_t* kidx;
+  const u32x4* k16;
+  const uint8_t* akeys;
+  const uint32_t* akey_off;
+  uint64_t an;              // input entries
 };
 
 // sstate words
@@ -1250,6 +1265,32 @@ __device__ __forceinline__ uint32_t glcp(const GKeys& K, uint32_t pp, uint32_t p
   return m;
 }
 
+// LCP of two keys from their first 16 bytes (big-endian words, zero padded) and, past a tie on
+// those, the tails at arena positions pp / kp; *order as glcp's (the first key against the second).
+__device__ __forceinline__ uint32_t lcp_k16(const GKeys& G, const u32x4& x, uint32_t pp, uint32_t pl, const u32x4& y,
+                                          uint32_t kp, uint32_t kl, int* order) {
+  const uint32_t m = pl < kl ? pl : kl;
+  const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+  for (uint32_t w = 0; w < 4; ++w) {
+    if (xs[w] != ys[w]) {
+      const uint32_t z = 4 * w + (__builtin_clz(xs[w] ^ ys[w]) >> 3);
+      if (z < m) {
+        const uint32_t sh = 24 - 8 * (z & 3);
+        *order = ((xs[w] >> sh) & 0xFF) < ((ys[w] >> sh) & 0xFF) ? -1 : 1;
+        return z;
+      }
+      *order = pl < kl ? -1 : (pl > kl ? 1 : 0);  // (a zero pad against a key byte)
+      return m;
+    }
+  }
+  if (m <= 16) {
+    *order = pl < kl ? -1 : (pl > kl ? 1 : 0);
+    return m;
+  }
+  return 16 + glcp(G, pp + 16, pl - 16, kp + 16, kl - 16, order);
+}
+
 __global__ __launch_bounds__(256) void rot_adj_kernel(RotArgs a) {
   const uint64_t n = rot_n(a);
   const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -1257,7 +1298,15 @@ __global__ __launch_bounds__(256) void rot_adj_kernel(RotArgs a) {
   const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
   a.rec[e] = kl + (a.val_off[e + 1] - a.val_off[e]);
   uint32_t al = 0;
-  if (e > 0) {
+  if (e > 0 && a.kidx) {  // the kept keys through the merge input (see RotArgs)
+    const GKeys K = gkeys(a.akeys, a.akey_off[a.an]);
+    const uint32_t i = a.kidx[e], ip = a.kidx[e - 1];
+    const uint32_t pl = kp - a.key_off[e - 1];
+    int ord = 0;
+    const uint32_t lcp = lcp_k16(K, a.k16[ip], a.akey_off[ip], pl, a.k16[i], a.akey_off[i], kl, &ord);
+    const bool same = a.ksame ? a.ksame[e] != 0 : ord == 0;
+    al = (lcp < kRotLcp ? lcp : kRotLcp) | (ord > 0 ? kRotUnsorted : 0u) | (same ? kRotSame : 0u);
+  } else if (e > 0) {
     const GKeys K = gkeys(a.keys, a.key_off[n]);
     const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
     int ord = 0;
@@ -1727,6 +1776,7 @@ struct MergePlan {
   MergeArgs m;
   uint32_t* keep;
   uint8_t* ksame;    // two-level: same_as_last_key per kept entry
+  uint32_t* kidx;    // per kept entry, its input index (the deferred gather, lsmblk_compact_batch)
   uint64_t* gtile;   // 6 per gather tile
   uint64_t gtiles;
   uint64_t bytes;
@@ -1757,6 +1807,7 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   P.m.mstats = cv.take<uint64_t>(8);
   P.keep = cv.take<uint32_t>(n + 1);
   P.ksame = cv.take<uint8_t>(n + 1);
+  P.kidx = cv.take<uint32_t>(n + 1);
   P.gtiles = (n + kGTile - 1) / kGTile + 1;
   P.gtile = cv.take<uint64_t>(6 * P.gtiles + 6 * (P.gtiles / kGScan + 2));
   P.bytes = cv.off;
@@ -1773,7 +1824,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
                         uint32_t rules, uint64_t wm, int bottom, const uint8_t* pfx, const uint32_t* pfx_off,
                         uint32_t npfx, const lsmblk_key_range* range, const lsmblk_kv_stream* out, uint64_t* stats,
                         hipStream_t st, MergePlan* plan_out, uint32_t two, uint32_t two_end = LSMBLK_TWO_END_IN_RANGE,
-                        uint8_t* ksame_out = nullptr) {
+                        uint8_t* ksame_out = nullptr, GatherArgs* defer = nullptr) {
   const uint64_t n = in->n;
   MergePlan P = plan_merge(nullptr, n, nrun);
   int rc = ensure_ws(c, P.bytes);
@@ -1847,7 +1898,21 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   LSM_LAUNCH(mflag_kernel, dim3(gt), dim3(256), 0, st, g);
   LSM_LAUNCH(mscan_part_kernel, dim3(uint32_t((P.gtiles + kGScan - 1) / kGScan)), dim3(256), 0, st, g);
   LSM_LAUNCH(mscan_top_kernel, dim3(1), dim3(1024), 0, st, g);
-  LSM_LAUNCH(mwrite_kernel, dim3(gt), dim3(256), 0, st, g);
+  if (defer) {  // the metadata now (with kidx), the bytes by the caller (mwrite_bytes)
+    g.kidx = P.kidx;
+    LSM_LAUNCH(mwrite_kernel<true, false>, dim3(gt), dim3(256), 0, st, g);
+    *defer = g;
+  } else {
+    g.kidx = nullptr;
+    LSM_LAUNCH(mwrite_kernel<true, true>, dim3(gt), dim3(256), 0, st, g);
+  }
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+// The deferred half of merge_gather_locked: the kept entries' key and value bytes.
+int mwrite_bytes(const GatherArgs& g, uint64_t n, hipStream_t st) {
+  if (n == 0) return LSMBLK_OK;
+  LSM_LAUNCH(mwrite_kernel<false, true>, dim3(uint32_t((n + kGTile - 1) / kGTile)), dim3(256), 0, st, g);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -2195,9 +2260,16 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if (hipMemsetAsync(sts, 0, 4 * 64, st) != hipSuccess) return LSMBLK_E_HIP;
   if (hipMemsetAsync(stats, 0, LSMBLK_COMPACT_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
+  // The rotation needs only the kept entries' metadata (and their keys, read in the merge input
+  // through kidx), so the kept stream's key and value bytes are gathered on `st` while the
+  // rotation runs on the context's second stream; the encode waits for both.
+  if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return LSMBLK_E_HIP;
+  if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
+  if (!c->join_ev && hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
   MergePlan MP{};
+  GatherArgs G{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
-                                o->nprefix, nullptr, kept, fst, st, &MP, two)))
+                                o->nprefix, nullptr, kept, fst, st, &MP, two, LSMBLK_TWO_END_IN_RANGE, nullptr, &G)))
     return rc;
   R = plan_rot(c->cws, M.bytes, n, o->target_sst_size);
   LSM_LAUNCH(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
@@ -2211,7 +2283,17 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   r.sst_cap = sst_cap;
   r.stats = rst;
   r.ksame = two ? MP.ksame : nullptr;
-  if ((rc = rotation_locked(c, r, st))) return rc;
+  r.kidx = MP.kidx;
+  r.k16 = MP.m.k16;
+  r.akeys = in->keys;
+  r.akey_off = in->key_off;
+  r.an = n;
+  if (hipEventRecord(c->fork_ev, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess)
+    return LSMBLK_E_HIP;
+  if ((rc = rotation_locked(c, r, c->aux))) return rc;
+  if (hipEventRecord(c->join_ev, c->aux) != hipSuccess) return LSMBLK_E_HIP;
+  if ((rc = mwrite_bytes(G, n, st))) return rc;
+  if (hipStreamWaitEvent(st, c->join_ev, 0) != hipSuccess) return LSMBLK_E_HIP;
   lsmblk_kv_stream ks = *kept;
   ks.n = n;  // bound; the encode reads the kept count from fst[0]
   if ((rc = lsmblk_impl::encode_locked(c, &ks, R.dn, sst_start, r.nsst, sst_cap - 1, o->block_size, out, out_cap,

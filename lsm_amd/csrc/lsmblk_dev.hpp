@@ -558,6 +558,10 @@ struct lsmblk_ctx {
   uint64_t cws_cap = 0;
   // CRC-verified decode (lsmblk_decode_batch_ex): per-block CRCs
   uint32_t* vcrc = nullptr;
+  // lsmblk_compact_batch: a second stream for the SST rotation beside the kept stream's byte
+  // gather, and the fork / join events (created on first use)
+  hipStream_t aux = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   uint64_t vcrc_cap = 0;
   // SST files (lsmblk_sst.hip)
   uint8_t* sws = nullptr;

@@ -2880,6 +2880,9 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   if (!c) return;
   DeviceGuard dg(c->device, c);
   (void)hipDeviceSynchronize();
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipFree(c->counters);
   (void)hipFree(c->dec_agg);
   (void)hipFree(c->tile_sum);
