@@ -2263,9 +2263,6 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   // The rotation needs only the kept entries' metadata (and their keys, read in the merge input
   // through kidx), so the kept stream's key and value bytes are gathered on `st` while the
   // rotation runs on the context's second stream; the encode waits for both.
-  if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return LSMBLK_E_HIP;
-  if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
-  if (!c->join_ev && hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
   MergePlan MP{};
   GatherArgs G{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
@@ -2288,12 +2285,10 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   r.akeys = in->keys;
   r.akey_off = in->key_off;
   r.an = n;
-  if (hipEventRecord(c->fork_ev, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess)
-    return LSMBLK_E_HIP;
+  if ((rc = lsmblk_impl::fork_aux(c, st))) return rc;
   if ((rc = rotation_locked(c, r, c->aux))) return rc;
-  if (hipEventRecord(c->join_ev, c->aux) != hipSuccess) return LSMBLK_E_HIP;
   if ((rc = mwrite_bytes(G, n, st))) return rc;
-  if (hipStreamWaitEvent(st, c->join_ev, 0) != hipSuccess) return LSMBLK_E_HIP;
+  if ((rc = lsmblk_impl::join_aux(c, st))) return rc;
   lsmblk_kv_stream ks = *kept;
   ks.n = n;  // bound; the encode reads the kept count from fst[0]
   if ((rc = lsmblk_impl::encode_locked(c, &ks, R.dn, sst_start, r.nsst, sst_cap - 1, o->block_size, out, out_cap,
