@@ -558,10 +558,6 @@ struct lsmblk_ctx {
   uint64_t cws_cap = 0;
   // CRC-verified decode (lsmblk_decode_batch_ex): per-block CRCs
   uint32_t* vcrc = nullptr;
-  // lsmblk_compact_batch: a second stream for the SST rotation beside the kept stream's byte
-  // gather, and the fork / join events (created on first use)
-  hipStream_t aux = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   uint64_t vcrc_cap = 0;
   // SST files (lsmblk_sst.hip)
   uint8_t* sws = nullptr;
@@ -688,10 +684,6 @@ int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nse
 int ensure_crc_tabs(lsmblk_ctx* c);
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg = nullptr);
-// The context's second stream and its fork / join events (created on first use): work launched
-// on c->aux after fork(c, st) runs beside st; join(c, st) makes st wait for it.
-int fork_aux(lsmblk_ctx* c, hipStream_t st);
-int join_aux(lsmblk_ctx* c, hipStream_t st);
 // lsmblk_block_meta_batch with the context lock held.
 int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                       const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off,

@@ -2880,9 +2880,6 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   if (!c) return;
   DeviceGuard dg(c->device, c);
   (void)hipDeviceSynchronize();
-  if (c->aux) (void)hipStreamDestroy(c->aux);
-  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipFree(c->counters);
   (void)hipFree(c->dec_agg);
   (void)hipFree(c->tile_sum);
@@ -3394,21 +3391,6 @@ int ensure_crc_tabs(lsmblk_ctx* c) {
     return LSMBLK_E_NOMEM;
   }
   return hipMemcpy(c->crc_tabs, &h, sizeof(CrcTabs), hipMemcpyHostToDevice) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
-}
-
-int fork_aux(lsmblk_ctx* c, hipStream_t st) {
-  if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return LSMBLK_E_HIP;
-  if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
-  if (!c->join_ev && hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
-  if (hipEventRecord(c->fork_ev, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess)
-    return LSMBLK_E_HIP;
-  return LSMBLK_OK;
-}
-
-int join_aux(lsmblk_ctx* c, hipStream_t st) {
-  if (hipEventRecord(c->join_ev, c->aux) != hipSuccess || hipStreamWaitEvent(st, c->join_ev, 0) != hipSuccess)
-    return LSMBLK_E_HIP;
-  return LSMBLK_OK;
 }
 
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
