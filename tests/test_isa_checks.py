@@ -41,6 +41,6 @@ def test_every_inline_asm_site_is_checked(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asm_inflight_check.py"), "--all", *paths],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    # decode_lag_kernel (staging loads), the crc / bloom kernels (SDWA), plan / merge-tile waits
-    for k in ("decode_lag_kernel", "crc_kernel", "plan_walk_kernel", "merge_tile_kernel", "sst_bloom_kernel"):
+    # decode_lag_kernel (staging loads), the crc / bloom kernels (SDWA), plan / large merge-tile waits
+    for k in ("decode_lag_kernel", "crc_kernel", "plan_walk_kernel", "merge_big_kernel", "sst_bloom_kernel"):
         assert k in r.stdout, r.stdout
