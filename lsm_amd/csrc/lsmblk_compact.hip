@@ -33,15 +33,24 @@
 
 namespace {
 
-constexpr uint32_t kMS = 128;  // every kMS-th entry of a run is a merge candidate
+#ifndef LSMBLK_MS
+#define LSMBLK_MS 128
+#endif
+#ifndef LSMBLK_MTE
+#define LSMBLK_MTE 512
+#endif
+#ifndef LSMBLK_MTT
+#define LSMBLK_MTT 128
+#endif
+constexpr uint32_t kMS = LSMBLK_MS;  // every kMS-th entry of a run is a merge candidate
 constexpr uint32_t kMaxRuns = 64;   // runs per merge (one lane per run in the tile kernels)
 // Tile entries with LDS tables.  Tile sizes average kMS (the gaps between consecutive candidates
 // of all runs) with a long tail, so the limit trades residency against the share of tiles left
 // to merge_big_kernel: merge_tile on config C took 5.3 / 3.1 / 2.8 / 2.8 / 3.5 / 6.9 ms at
 // 256 / 384 / 512 / 640 / 1024 / 2048 entries when larger tiles went to the one-wave global path
 // (and 3.2 / 3.8 ms at mean tile sizes 192 / 256 with the limit at 4x the mean).
-constexpr uint32_t kMTE = 512;
-constexpr uint32_t kMTT = 128;      // threads per tile workgroup
+constexpr uint32_t kMTE = LSMBLK_MTE;
+constexpr uint32_t kMTT = LSMBLK_MTT;  // threads per tile workgroup
 // merge_big_kernel: tiles of kMTE < total <= kBigTE entries (about 1 % of the tiles; 0.8 ms of
 // config C's 2.9 ms merge_tile as a global-memory tail), workgroups of kBigTT threads
 constexpr uint32_t kBigTE = 2048;

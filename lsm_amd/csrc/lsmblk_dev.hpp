@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "lsmblk.h"
@@ -261,15 +262,20 @@ struct GlbImg {
   __device__ __forceinline__ uint32_t u8(uint32_t i) const {
     return __builtin_amdgcn_raw_buffer_load_b8(r, lead + i, 0, 0);
   }
-  __device__ __forceinline__ uint32_t u16(uint32_t i) const { return (u8(i) << 8) | u8(i + 1); }
+  // Wider fields as one unaligned buffer load each (the gfx9 unaligned access mode) instead of a
+  // byte load per byte.  A load that reaches past the descriptor bound returns 0 as a whole
+  // (byte loads would return the bytes before the bound): the parse rules reject every entry
+  // whose fields reach past the block before using them, so the results agree on valid blocks
+  // and the MALFORMED verdicts agree on all.
+  __device__ __forceinline__ uint32_t u16(uint32_t i) const {
+    return bswap16(__builtin_amdgcn_raw_buffer_load_b16(r, lead + i, 0, 0));
+  }
   __device__ __forceinline__ uint32_t le32(uint32_t i) const {
-    return u8(i) | (u8(i + 1) << 8) | (u8(i + 2) << 16) | (u8(i + 3) << 24);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, lead + i, 0, 0);
   }
   __device__ __forceinline__ uint64_t u64(uint32_t i) const {
-    uint64_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v = (v << 8) | u8(i + j);
-    return v;
+    const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, lead + i, 0, 0);
+    return (uint64_t(__builtin_bswap32(q.x)) << 32) | __builtin_bswap32(q.y);
   }
 };
 

@@ -916,12 +916,27 @@ __device__ __forceinline__ BlkCount cnt_finish(const CntPre& C, uint8_t* img) {
       return;
     }
     r.n = h.n;
-    for (uint32_t c = 0; c < h.n; c += 64) {
-      const uint32_t k = c + l;
-      uint32_t off = 0, p = 0, s = 0, vl = 0;
-      if (k < h.n && !parse_entry(im, h, k, off, p, s, vl)) bad = true;
-      r.K += wave_sum<uint32_t>(p + s);
-      r.V += wave_sum<uint32_t>(vl);
+    if constexpr (std::is_same_v<std::decay_t<decltype(im)>, GlbImg>) {
+      // a large block's headers from global memory: entries l and l + 64 parsed side by side
+      // (indices clamped, so both dependent load chains are straight-line code and overlap)
+      for (uint32_t c = 0; c < h.n; c += 128) {
+        const uint32_t k0 = c + l, k1 = c + 64 + l;
+        const bool l0 = k0 < h.n, l1 = k1 < h.n;
+        uint32_t o0, p0, s0, v0, o1, p1, s1, v1;
+        const bool ok0 = parse_entry(im, h, l0 ? k0 : h.n - 1, o0, p0, s0, v0);
+        const bool ok1 = parse_entry(im, h, l1 ? k1 : h.n - 1, o1, p1, s1, v1);
+        if ((l0 && !ok0) || (l1 && !ok1)) bad = true;
+        r.K += wave_sum<uint32_t>((l0 ? p0 + s0 : 0u) + (l1 ? p1 + s1 : 0u));
+        r.V += wave_sum<uint32_t>((l0 ? v0 : 0u) + (l1 ? v1 : 0u));
+      }
+    } else {
+      for (uint32_t c = 0; c < h.n; c += 64) {
+        const uint32_t k = c + l;
+        uint32_t off = 0, p = 0, s = 0, vl = 0;
+        if (k < h.n && !parse_entry(im, h, k, off, p, s, vl)) bad = true;
+        r.K += wave_sum<uint32_t>(p + s);
+        r.V += wave_sum<uint32_t>(vl);
+      }
     }
   };
   if (C.staged) {

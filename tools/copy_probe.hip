@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <utility>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -21,6 +22,29 @@ __global__ __launch_bounds__(256) void copy_k(const u32x4* __restrict__ a, u32x4
         if (NT) __builtin_nontemporal_store(v[j], b + i + 256 * j);
         else b[i + 256 * j] = v[j];
       }
+  }
+}
+
+// The same copy at byte offsets (so, dof) through buffer descriptors (as the product's large-block
+// run copies do): unaligned 16-B loads and stores.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <int U>
+__global__ __launch_bounds__(256) void copy_u(const uint8_t* a, uint8_t* b, uint32_t n16, uint32_t so, uint32_t dof,
+                                              uint32_t bytes) {
+  const __amdgpu_buffer_rsrc_t RA = rsrc(a, bytes + 64), RB = rsrc(b, bytes + 64);
+  const uint32_t stride = gridDim.x * 256 * U;
+  for (uint32_t i = blockIdx.x * 256 * U + threadIdx.x; i < n16; i += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (i + 256 * j < n16)
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(RA, so + 16 * (i + 256 * j), 0, 0);
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (i + 256 * j < n16)
+        __builtin_amdgcn_raw_buffer_store_b128(v[j], RB, dof + 16 * (i + 256 * j), 0, 0);
   }
 }
 
@@ -74,6 +98,21 @@ int main() {
     (void)hipEventElapsedTime(&ms, e0, e1);
     ms /= 10;
     printf("read  WG/CU %2d: %.3f ms = %.0f GB/s\n", wg, ms, 1.0 * bytes / ms / 1e6);
+  }
+  // unaligned 16-B copies (1 GiB, byte offsets so / dof): what misalignment costs each side
+  const uint32_t ub = 1u << 30;
+  for (auto [so, dof] : {std::pair<uint32_t, uint32_t>{0, 0}, {3, 0}, {0, 7}, {3, 7}, {5, 5}}) {
+    float ms = 0;
+    const uint32_t grid = uint32_t(cus * 8);
+    copy_u<4><<<grid, 256>>>(reinterpret_cast<uint8_t*>(a), reinterpret_cast<uint8_t*>(b), ub / 16, so, dof, ub);
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < 10; ++r)
+      copy_u<4><<<grid, 256>>>(reinterpret_cast<uint8_t*>(a), reinterpret_cast<uint8_t*>(b), ub / 16, so, dof, ub);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ms /= 10;
+    printf("copy_u src+%u dst+%u: %.3f ms = %.0f GB/s read+write\n", so, dof, ms, 2.0 * ub / ms / 1e6);
   }
   return 0;
 }
