@@ -1369,24 +1369,21 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
           uint32_t lcp = m, w0 = 0, w1 = 0;
           bool done = false;
           if (K.glead + kp[i] + 16 <= klim && K.glead + pp[i] + 16 <= klim) {
+            // first differing byte z of the 16 loaded (16: none), by selects instead of a branch per
+            // dword (the helper shares its SIMD with the walker: its instructions are the walk's time)
             const uint32_t P[4] = {xp[i].x, xp[i].y, xp[i].z, xp[i].w}, Q[4] = {xk[i].x, xk[i].y, xk[i].z, xk[i].w};
+            uint32_t t[4];
 #pragma unroll
-            for (uint32_t d = 0; d < 4; ++d) {
-              if (!done && 4 * d < m) {
-                if (P[d] != Q[d]) {
-                  const uint32_t z = 4 * d + (__builtin_ctz(P[d] ^ Q[d]) >> 3);
-                  if (z < m) {
-                    lcp = z;
-                    w0 = P[d];
-                    w1 = Q[d];
-                  }
-                  done = true;
-                }
-              } else {
-                done = true;
-              }
+            for (uint32_t d = 0; d < 4; ++d) t[d] = uint32_t(__builtin_ctzg(P[d] ^ Q[d], 32)) >> 3;  // 4: equal
+            const uint32_t z16 = t[0] < 4 ? t[0] : t[1] < 4 ? 4 + t[1] : t[2] < 4 ? 8 + t[2] : 12 + t[3];
+            const uint32_t zd = z16 >> 2;  // (z16 < 16 only)
+            if (z16 < m) {
+              lcp = z16;
+              w0 = zd == 0 ? P[0] : zd == 1 ? P[1] : zd == 2 ? P[2] : P[3];
+              w1 = zd == 0 ? Q[0] : zd == 1 ? Q[1] : zd == 2 ? Q[2] : Q[3];
             }
-            if (!done && m > 16) {  // equal first 16 bytes: the rest by dwords
+            done = z16 < m || m <= 16;
+            if (!done) {  // equal first 16 bytes: the rest by dwords
               for (uint32_t d = 4; 4 * d < m; ++d) {
                 const uint32_t y0 = K.dword(pp[i] + 4 * d), y1 = K.dword(kp[i] + 4 * d);
                 if (y0 != y1) {
