@@ -1483,6 +1483,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
   uint32_t nb = 0;
   uint64_t bytes = 0;
   const uint64_t bs = a.block_size;
+  const bool narrow = bs < (1ull << 30);
   for (uint32_t s = s0; s < s1;) {
     uint64_t carry = 2;           // estimated_size() of an empty builder
     uint32_t pmin = kAlcpLcp;     // running min of alcp over (s, window start)
@@ -1525,13 +1526,27 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
         p = key_lcp(K, sp, sl, kp, kl, w0, w1);
       }
       if (e == s) p = 0;
-      const uint64_t gr = valid ? uint64_t(r) + 16 - p : 0;  // data growth + offset slot
-      // u32 DPP scan when every lane's growth is < 2^25 (sum fits), else the 64-bit scan
-      const uint64_t incl = __ballot(gr >= (1u << 25)) == 0 ? uint64_t(wave_incl_scan32(uint32_t(gr)))
-                                                             : wave_incl_scan<uint64_t>(gr);
-      const uint64_t before = carry + incl - gr;  // estimated_size() before adding e
-      // builder.rs:56-60: reject when est + raw_len + vlen + 6 > block_size (not first entry)
-      const bool stop = !valid || (e != s && before + r + 14 > bs);
+      // data growth + offset slot, its inclusive scan and estimated_size() before adding e.  u32
+      // throughout when the block size is < 2^30 and every lane's growth < 2^25 (then carry <= bs +
+      // 2, the scan < 2^31 and before + r + 14 < 2^32: exact), else 64-bit.
+      uint64_t before, incl_all;
+      bool stop;
+      if (narrow && __ballot(valid && r >= (1u << 25) - 16) == 0) {
+        const uint32_t g32 = valid ? r + 16 - p : 0u;
+        const uint32_t i32 = wave_incl_scan32(g32);
+        const uint32_t b32 = uint32_t(carry) + i32 - g32;
+        // builder.rs:56-60: reject when est + raw_len + vlen + 6 > block_size (not first entry)
+        stop = !valid || (e != s && b32 + r + 14 > uint32_t(bs));
+        before = b32;
+        incl_all = uint32_t(__builtin_amdgcn_readlane(i32, 63));
+      } else {
+        const uint64_t gr = valid ? uint64_t(r) + 16 - p : 0;
+        const uint64_t incl = __ballot(gr >= (1u << 25)) == 0 ? uint64_t(wave_incl_scan32(uint32_t(gr)))
+                                                               : wave_incl_scan<uint64_t>(gr);
+        before = carry + incl - gr;
+        stop = !valid || (e != s && before + r + 14 > bs);
+        incl_all = lane64(incl, 63);
+      }
       const uint64_t m = __ballot(stop);
       if (m) {
         uint32_t f = uint32_t(__builtin_ctzll(m));
@@ -1578,7 +1593,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
         if (open) continue;  // next window, same block
         break;
       }
-      carry += lane64(incl, 63);
+      carry += incl_all;
     }
   }
   if (tr && l == 0) {
