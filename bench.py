@@ -557,7 +557,7 @@ def compaction_roofline(ctx, step, dev, E, D, Dk, n, nblk, s, step_bytes, ms, de
             "mwrite_kernel": 2 * Dk + 4 * merged,             # kept entries gathered in merged order
             "mflag_kernel": s[6] + 12 * merged,               # keys + ts + order in, keep flags out
             "emit_kernel": Dk + s[1], "plan_walk_kernel": 8 * (kept + 1) + s[6] + 8 * s[0]}
-    b = algo.get(dom)
+    b = algo.get(dom.split("<")[0])  # (templates log as name<args>)
     achieved = b / (per[dom] * 1e-3) / 1e9 if b else None
     traffic, why = measured_traffic("C", dom, launches=prof[dom][0], default_size=default_size)
     top = sorted(per.items(), key=lambda kv: -kv[1])[:10]

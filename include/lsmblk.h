@@ -164,6 +164,9 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
                                      blocks at the batch's mean block size, at most 10240); setting it fixes the lag, 0 restores the default */
 #define LSMBLK_DEBUG_DECODE_LAG_BYTES 6 /* the lagged decode's lag in bytes of blocks (default 40 MiB; 0: the lag set by key 4) */
 #define LSMBLK_DEBUG_COUNTERS 5 /* 1: the lagged decode records a realtime trace per tile (lsmblk_debug_counters) */
+#define LSMBLK_DEBUG_ROT_POISON 7 /* diagnostics builds only (fault injection): 1 = the SST rotation's block-chain levels
+                                     get links that do not advance (J(s) = s, S(s) = 0) over a third of the
+                                     stream; the rotation must report LSMBLK_E_INTERNAL, never loop */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* The trace of the last lagged decode with LSMBLK_DEBUG_COUNTERS on (n <= 16 + 8 * 32768 words;
  * synchronizes).  Words 16 + 8 t + k, 100 MHz s_memrealtime stamps of 64-block tile t: k = 0 tile
@@ -298,7 +301,8 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, uin
  * by key (the reference's debug_assert :135-138); a merged order that is not reports
  * LSMBLK_ERR_MALFORMED.  The merged stream is written to `out` (any alignment; capacities as
  * for decode).  stats: [0] entries [1] key bytes [2] value bytes [3] error flags (CAPACITY with
- * the required sizes in [0..2]; SEGMENTS: bad run_start).  Asynchronous. */
+ * the required sizes in [0..2]; SEGMENTS: bad run_start, or a key over 65 535 bytes -- the merge
+ * tiles hold u16 key lengths, as the block format does).  Asynchronous. */
 int lsmblk_merge_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* run_start, uint32_t nrun,
                        const lsmblk_kv_stream* out, uint64_t* stats, void* stream);
 /* lsmblk_merge_batch in merge_mode LSMBLK_MERGE_RUNS or LSMBLK_MERGE_TWO_LEVEL (run nrun-1 = b). */

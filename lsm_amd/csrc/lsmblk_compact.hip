@@ -204,13 +204,18 @@ __device__ __forceinline__ int kcmp16(const MergeArgs& a, const GKeys& G, const 
 // Every input key's first 16 bytes, once, in entry order (coalesced: the key arena is read front
 // to back): the merge tiles, the bound searches and the rules then read one 16-B word per key in
 // the same round trip as its offsets, instead of the offsets and then the key bytes.
+// A key over 65 535 bytes is refused (LSMBLK_ERR_SEGMENTS -> LSMBLK_E_INVAL): the merge tiles
+// keep u16 key lengths (a longer key's truncated length could rank two distinct keys
+// as equal and drop one), and the block format stores key lengths `as u16` anyway
+// (src/block/builder.rs:63-64).
 __global__ __launch_bounds__(256) void key16_kernel(const uint8_t* keys, const uint32_t* key_off, uint64_t n,
-                                                    u32x4* k16) {
+                                                    u32x4* k16, uint64_t* merr) {
   const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (e >= n) return;
   const GKeys G = gkeys(keys, key_off[n]);
-  const uint32_t p = key_off[e];
-  k16[e] = key16(G, p, key_off[e + 1] - p);
+  const uint32_t p = key_off[e], kl = key_off[e + 1] - p;
+  k16[e] = key16(G, p, kl);
+  if (kl > 0xFFFFu) atomicOr(reinterpret_cast<unsigned long long*>(merr), (unsigned long long)LSMBLK_ERR_SEGMENTS);
 }
 
 // Every candidate's first 16 key bytes and length, in run-major candidate order (ck, cklen): the
@@ -1225,6 +1230,8 @@ struct RotArgs {
   uint32_t* F2;
   uint32_t* need;           // kRotMaxLevels: level k still has a chain short of target and end
   uint32_t* chain_end;      // [0] set once the SST chain reached the end
+  uint32_t* rerr;           // [0] error flags of the lifting walks (a chain link that does not advance)
+  uint32_t poison;          // diagnostics (LSMBLK_DEBUG_ROT_POISON): corrupt the levels before the lifting
   uint32_t* starts;         // sst_cap: SST start entries (the chain), then n
   uint32_t sst_cap;
   uint32_t* nsst;           // device: SST count handed to the encode (0 after an error)
@@ -1469,12 +1476,19 @@ __device__ __forceinline__ uint32_t rot_top(const RotArgs& a) {
 
 // Lifting from block start pos with acc bytes of data section: the longest block chain prefix
 // whose data stays below the target.  Returns its last block start (acc updated).
+// Every chain link advances (J_k(s) > s for s < n): a link that does not -- corrupt or stale
+// levels -- ends the walk with LSMBLK_ERR_INTERNAL instead of looping (each walk is then at most
+// n steps).
 __device__ __forceinline__ uint64_t lift_target(const RotArgs& a, uint64_t pos, uint64_t& acc, uint64_t n,
-                                                uint32_t top) {
+                                                uint32_t top, uint64_t& err) {
   const uint64_t N1 = a.n_max + 1;
   while (pos < n) {
     const u32x2 v = a.JS[top * N1 + pos];
     if (acc + v.y >= a.target) break;
+    if (v.x <= pos) {
+      err |= LSMBLK_ERR_INTERNAL;
+      break;
+    }
     acc += v.y;
     pos = v.x;
   }
@@ -1493,11 +1507,15 @@ __device__ __forceinline__ uint64_t lift_target(const RotArgs& a, uint64_t pos, 
 // Lifting from block start pos < bound: the last block start below bound in its chain (acc
 // updated with the data of the blocks passed).
 __device__ __forceinline__ uint64_t lift_before(const RotArgs& a, uint64_t pos, uint64_t& acc, uint64_t bound,
-                                                uint32_t top) {
+                                                uint32_t top, uint64_t& err) {
   const uint64_t N1 = a.n_max + 1;
   for (;;) {
     const u32x2 v = a.JS[top * N1 + pos];
     if (v.x >= bound) break;
+    if (v.x <= pos) {  // (a link that does not advance: see lift_target)
+      err |= LSMBLK_ERR_INTERNAL;
+      break;
+    }
     acc += v.y;
     pos = v.x;
   }
@@ -1529,15 +1547,23 @@ __global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
   const uint64_t N1 = a.n_max + 1;
   // lifting: the longest chain prefix from g whose data stays below the target
   uint64_t p0 = g0, p1 = g1, c0 = 0, c1 = 0;
-  for (;;) {  // top level, repeated while it fits
+  bool stuck = false;
+  for (;;) {  // top level, repeated while it fits (every move advances: at most n moves)
     bool m0 = false, m1 = false;
     u32x2 v0{0u, 0u}, v1{0u, 0u};
     if (p0 < n) v0 = a.JS[top * N1 + p0];
     if (p1 < n) v1 = a.JS[top * N1 + p1];
-    if (p0 < n && c0 + v0.y < a.target) c0 += v0.y, p0 = v0.x, m0 = true;
-    if (p1 < n && c1 + v1.y < a.target) c1 += v1.y, p1 = v1.x, m1 = true;
-    if (!m0 && !m1) break;
+    if (p0 < n && c0 + v0.y < a.target) {
+      stuck = stuck || v0.x <= p0;
+      c0 += v0.y, p0 = v0.x, m0 = true;
+    }
+    if (p1 < n && c1 + v1.y < a.target) {
+      stuck = stuck || v1.x <= p1;
+      c1 += v1.y, p1 = v1.x, m1 = true;
+    }
+    if ((!m0 && !m1) || stuck) break;
   }
+  if (stuck) atomicOr(a.rerr, LSMBLK_ERR_INTERNAL);  // (a link that does not advance: lift_target)
   for (int k = int(top) - 1; k >= 0; --k) {
     u32x2 v0{0u, 0u}, v1{0u, 0u};
     if (p0 < n) v0 = a.JS[uint64_t(k) * N1 + p0];
@@ -1550,6 +1576,15 @@ __global__ __launch_bounds__(256) void rot_f_kernel(RotArgs a) {
   else if (g0 == n) a.F0[g0] = uint32_t(n);
   if (g1 < n) a.F0[g1] = uint32_t(p1 < n ? key_change_after(a, a.JS[p1].x, n) : n);
   else if (g1 == n) a.F0[g1] = uint32_t(n);
+}
+
+// Fault injection (LSMBLK_DEBUG_ROT_POISON, diagnostics builds): every level's link of the entries
+// in [n/3, 2n/3) made a self-loop of size 0 -- the shape a stale or raced level would have.
+__global__ __launch_bounds__(256) void rot_poison_kernel(RotArgs a) {
+  const uint64_t n = rot_n(a), N1 = a.n_max + 1;
+  const uint64_t s = n / 3 + uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (s >= 2 * n / 3) return;
+  for (uint32_t k = 0; k < a.levels; ++k) a.JS[k * N1 + s] = u32x2{uint32_t(s), 0u};
 }
 
 // ---------------------------------------------------------------- key-range shard rotation
@@ -1581,7 +1616,7 @@ __global__ void shard_carry_kernel(RotArgs a, const uint64_t* cin, uint64_t* cou
   const uint64_t n = rot_n(a), m = a.m, N1 = a.n_max + 1;
   const uint32_t top = rot_top(a);
   const uint64_t p = cin[0], D0 = cin[1];
-  uint64_t err = 0, E1 = m, cnt = 0, end = m, pout = 0, Dout = 0, segs = 0;
+  uint64_t err = *a.rerr, E1 = m, cnt = 0, end = m, pout = 0, Dout = 0, segs = 0;
   // the range must end at a key change (all versions of a user key on one rank)
   if (m > 0 && m < n && (a.alcp[m] & kRotSame)) err |= LSMBLK_ERR_SEGMENTS;
   if (p >= m) {  // the crossing block from an earlier rank covers the whole range
@@ -1592,7 +1627,7 @@ __global__ void shard_carry_kernel(RotArgs a, const uint64_t* cin, uint64_t* cou
     uint64_t sj = p;
     if (D0 < a.target) {
       uint64_t acc = D0;
-      const uint64_t pos = lift_target(a, p, acc, n, top);
+      const uint64_t pos = lift_target(a, p, acc, n, top, err);
       sj = pos < n ? a.JS[pos].x : n;
     }
     E1 = key_change_after(a, sj, n);
@@ -1615,7 +1650,7 @@ __global__ void shard_carry_kernel(RotArgs a, const uint64_t* cin, uint64_t* cou
     if (fl == m) {  // the last SST ends where the next range starts (or the stream ends)
       end = m;
     } else {        // it continues: its block chain crosses m
-      const uint64_t pos = lift_before(a, x, accx, m, top);
+      const uint64_t pos = lift_before(a, x, accx, m, top, err);
       const u32x2 v = a.JS[pos];
       const uint64_t b = v.x;
       if (b >= n && !a.shard_last) err |= LSMBLK_ERR_SEGMENTS;  // the halo is too short
@@ -1757,7 +1792,7 @@ __global__ __launch_bounds__(256) void rot_finish_kernel(RotArgs a) {
       }
     }
     s_ns = lo;
-    uint32_t err = 0;
+    uint32_t err = *a.rerr;
     if (uint64_t(lo) + 1 > a.sst_cap) err |= LSMBLK_ERR_CAPACITY;  // the chain did not end in the array
     a.stats[0] = lo;
     *a.nsst = err ? 0u : lo;
@@ -1857,7 +1892,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   if (hipMemsetAsync(m.mstats, 0, 64, st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t nc = m.nc_max;
   LSM_LAUNCH(key16_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, m.keys, m.key_off, n,
-             const_cast<u32x4*>(m.k16));
+             const_cast<u32x4*>(m.k16), m.mstats + 3);
   LSM_LAUNCH(cand_key_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   LSM_LAUNCH(cand_rank_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, m);
   const uint64_t nb = (uint64_t(nc) + 1) * nrun;
@@ -1909,11 +1944,11 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
   LSM_LAUNCH(mscan_top_kernel, dim3(1), dim3(1024), 0, st, g);
   if (defer) {  // the metadata now (with kidx), the bytes by the caller (mwrite_bytes)
     g.kidx = P.kidx;
-    LSM_LAUNCH(mwrite_kernel<true, false>, dim3(gt), dim3(256), 0, st, g);
+    LSM_LAUNCH_NAMED("mwrite_kernel<true,false>", mwrite_kernel<true, false>, dim3(gt), dim3(256), 0, st, g);
     *defer = g;
   } else {
     g.kidx = nullptr;
-    LSM_LAUNCH(mwrite_kernel<true, true>, dim3(gt), dim3(256), 0, st, g);
+    LSM_LAUNCH_NAMED("mwrite_kernel<true,true>", mwrite_kernel<true, true>, dim3(gt), dim3(256), 0, st, g);
   }
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -1921,7 +1956,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
 // The deferred half of merge_gather_locked: the kept entries' key and value bytes.
 int mwrite_bytes(const GatherArgs& g, uint64_t n, hipStream_t st) {
   if (n == 0) return LSMBLK_OK;
-  LSM_LAUNCH(mwrite_kernel<false, true>, dim3(uint32_t((n + kGTile - 1) / kGTile)), dim3(256), 0, st, g);
+  LSM_LAUNCH_NAMED("mwrite_kernel<false,true>", mwrite_kernel<false, true>, dim3(uint32_t((n + kGTile - 1) / kGTile)), dim3(256), 0, st, g);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -1972,9 +2007,10 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, u
     P.r.F1 = cv.take<uint32_t>(N1);
     P.r.F2 = cv.take<uint32_t>(N1);
   }
-  P.r.need = cv.take<uint32_t>(kRotMaxLevels + 2);
+  P.r.need = cv.take<uint32_t>(kRotMaxLevels + 3);
   P.r.chain_end = P.r.need + kRotMaxLevels;
   P.r.nsst = P.r.need + kRotMaxLevels + 1;
+  P.r.rerr = P.r.need + kRotMaxLevels + 2;
   P.dn = cv.take<uint64_t>(2);
   P.bytes = cv.off;
   return P;
@@ -1983,12 +2019,13 @@ RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, u
 // SST cut points of the stream (keys, key_off, val_off; *dn entries, <= n_max) into starts[]
 // The carry-independent part: adjacency, block chains and their doubling levels, F.
 int rotation_chains(const RotArgs& r, hipStream_t st) {
-  if (hipMemsetAsync(r.need, 0, (kRotMaxLevels + 2) * sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipMemsetAsync(r.need, 0, (kRotMaxLevels + 3) * sizeof(uint32_t), st) != hipSuccess) return LSMBLK_E_HIP;
   const uint32_t g = uint32_t((r.n_max + 1 + 255) / 256);
   LSM_LAUNCH(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
   LSM_LAUNCH(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
   const uint32_t gd = uint32_t((r.n_max + 1 + 256 * kRotPer - 1) / (256 * kRotPer));
   for (uint32_t k = 1; k < r.levels; ++k) LSM_LAUNCH(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
+  if (kDiag && r.poison) LSM_LAUNCH(rot_poison_kernel, dim3(uint32_t((r.n_max / 3 + 256) / 256)), dim3(256), 0, st, r);
   LSM_LAUNCH(rot_f_kernel, dim3(uint32_t((r.n_max + 1 + 511) / 512)), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -2146,6 +2183,7 @@ int lsmblk_shard_rotation_prepare_ex(lsmblk_ctx* c, const lsmblk_kv_stream* ext,
   c->shard_sst_cap = sst_cap;
   RotArgs r = shard_args(c, ext);
   r.ksame = ext_same;  // two-level: the loop's same_as_last_key (baked into alcp by rot_adj)
+  r.poison = c->rot_poison;
   LSM_LAUNCH(set_u64_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(r.dn), uint64_t(ext->n));
   if ((rc = rotation_chains(r, st))) return rc;
   const uint32_t gr = uint32_t((ext->n + 1 + 255) / 256);
@@ -2239,6 +2277,7 @@ int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_
   r.starts = sst_start;
   r.sst_cap = sst_cap;
   r.stats = stats;
+  r.poison = c->rot_poison;
   return rotation_locked(c, r, st);
 }
 
@@ -2296,6 +2335,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   r.akeys = in->keys;
   r.akey_off = in->key_off;
   r.an = n;
+  r.poison = c->rot_poison;
   if ((rc = rotation_locked(c, r, st))) return rc;
   if ((rc = mwrite_bytes(G, n, st))) return rc;
   lsmblk_kv_stream ks = *kept;

@@ -525,6 +525,7 @@ struct lsmblk_ctx {
   uint64_t rec_cap = 0;
   uint64_t* lag_gran = nullptr;  // lagged decode granules (uncached): 3 aggregate + 3 base per block,
   uint64_t lag_blk_cap = 0;      //   then 3 aggregate + 3 inclusive per 64-block tile; blocks covered
+  uint32_t rot_poison = 0;       // diagnostics builds only: LSMBLK_DEBUG_ROT_POISON
   bool dec_two_pass = false;     // diagnostics: count + scan + decode instead of the lagged decode (A/B)
   uint32_t dec_lag = kDecLagDefault;  // blocks the lagged decode's counts run ahead of its decodes, at most;
   uint64_t dec_lag_bytes = kDecLagBytesDefault;  // that many bytes of blocks at the mean block size (0: exactly dec_lag)
@@ -673,6 +674,9 @@ inline void lsm_launch(const char* name, int slot, K kern, dim3 grid, dim3 block
 #define LSM_LAUNCH(kern, grid, block, shmem, st, ...) lsm_launch(#kern, -1, kern, grid, block, shmem, st, __VA_ARGS__)
 #define LSM_LAUNCH_SLOT(slot, kern, grid, block, shmem, st, ...) \
   lsm_launch(#kern, slot, kern, grid, block, shmem, st, __VA_ARGS__)
+// A kernel template with several arguments: #kern would stop at the first comma of its argument
+// list, so the log name is given explicitly.
+#define LSM_LAUNCH_NAMED(name, kern, grid, block, shmem, st, ...) lsm_launch(name, -1, kern, grid, block, shmem, st, __VA_ARGS__)
 
 // Internal entry points shared between translation units (called with ctx->mu held).
 namespace lsmblk_impl {

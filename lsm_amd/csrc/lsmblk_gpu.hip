@@ -628,15 +628,16 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
                              Post&& post, PreWait&& pre_wait) {
   const uint32_t l = lane_id();
   uint32_t err = 0;
-  // output-base loads depend only on b: issue them first, they land during staging + parse.
-  // Lagged decode: the block's base granules (lanes 0-2); two-pass: the tile prefix + the
-  // aggregates of the tile's earlier blocks.
+  // Output-base loads depend only on b.  Two-pass: the tile prefix + the aggregates of the tile's
+  // earlier blocks, issued first, they land during staging + parse.  Lagged decode: the block's
+  // base granules (lanes 0-2), issued after the landing, under the entry parse: issued first they
+  // returned before the tile finisher had published them about half the time (trace: the finish
+  // ends ~1.6 us after the tile's first decoder starts), and the decoder then waited a re-poll
+  // round trip (~1 us median); moved, decode 2.09 -> 2.05 ms at U (A/B, one box).
   const uint64_t tb = b / kTile, jb = b % kTile;
   uint32_t cn = 0, ck = 0, cv = 0;
   uint64_t tp0 = 0, tp1 = 0, tp2 = 0, gb = 0;
-  if constexpr (lagm) {
-    if (l < 3 && !(diag_mask(a.skip) & 4096)) gb = gload(a.bbase + 3 * b + l, 0);  // (4096: ablation)
-  } else {
+  if constexpr (!lagm) {
     if (l < jb) {
       const uint64_t q = tb * kTile + l;
       cn = a.agg[3 * q];
@@ -690,10 +691,12 @@ __device__ void decode_block(const DecodeArgs& a, DecLds& L, uint64_t b, uint64_
       if (l + 64 * i < nchunk) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = v[i];
     wave_sync();
     post();
+    if (lagm && l < 3 && !(diag_mask(a.skip) & 4096)) gb = gload(a.bbase + 3 * b + l, 0);  // (4096: ablation)
     h = parse_hdr(LdsImg{L.img, lead}, len);
   } else {
     mid();
     post();
+    if (lagm && l < 3 && !(diag_mask(a.skip) & 4096)) gb = gload(a.bbase + 3 * b + l, 0);
     h = parse_hdr(GlbImg{R, lead}, len);
   }
   if (diag_mask(a.skip) & 256) return;  // ablation: staging only
@@ -959,18 +962,29 @@ __device__ __forceinline__ BlkCount cnt_finish(const CntPre& C, uint8_t* img) {
 
 // The last counter of tile t: waits for the tile's aggregates, publishes the tile aggregate, looks
 // back over the tiles for its prefix, publishes the inclusive prefix and every block's base.
-__device__ void lag_tile_finish(const DecodeArgs& a, uint64_t t, uint32_t& err) {
+struct FinPf {
+  uint64_t g0, g1, g2;
+};
+__device__ __forceinline__ FinPf fin_prefetch(const DecodeArgs& a, uint64_t t) {
+  const uint32_t l = lane_id();
+  const uint64_t b0 = t * kTile, nb = min(uint64_t(kTile), a.nblk - b0);
+  const uint64_t want = (uint64_t(a.tag) << 2) | 1;
+  FinPf f{want, want, want};  // lanes >= nb read as present zeros
+  if (l < nb) {
+    f.g0 = gload(a.bagg + 3 * (b0 + l), 0);
+    f.g1 = gload(a.bagg + 3 * (b0 + l) + 1, 0);
+    f.g2 = gload(a.bagg + 3 * (b0 + l) + 2, 0);
+  }
+  return f;
+}
+__device__ void lag_tile_finish(const DecodeArgs& a, uint64_t t, uint32_t& err, const FinPf* pf = nullptr) {
   const uint32_t l = lane_id();
   dbg_trace(a.dbg, t, 0);
   const uint64_t b0 = t * kTile, nb = min(uint64_t(kTile), a.nblk - b0);
   const uint64_t want = (uint64_t(a.tag) << 2) | 1;
-  uint64_t g0 = want, g1 = want, g2 = want;  // lanes >= nb read as present zeros
   const bool mine = l < nb;
-  if (mine) {
-    g0 = gload(a.bagg + 3 * (b0 + l), 0);
-    g1 = gload(a.bagg + 3 * (b0 + l) + 1, 0);
-    g2 = gload(a.bagg + 3 * (b0 + l) + 2, 0);
-  }
+  const FinPf f0 = pf ? *pf : fin_prefetch(a, t);
+  uint64_t g0 = f0.g0, g1 = f0.g1, g2 = f0.g2;
   uint32_t spins = 0;
   for (;;) {
     const bool here = (g0 & 0xFFFF) == want && (g1 & 0xFFFF) == want && (g2 & 0xFFFF) == want;
@@ -1090,8 +1104,13 @@ __global__ __launch_bounds__(64) void decode_lag_kernel(DecodeArgs a) {
     publish3(a.bagg, j, r.n, r.K, r.V, a.tag, 1, a.poll);
     if (r.K > 0xFFFFFFFFull || r.V > 0xFFFFFFFFull) err |= LSMBLK_ERR_OVERFLOW;
   };
+  // a finisher loads its tile's aggregates now, under its own staging and count (they are
+  // normally all there: the tile's counts ran lag / 2 workgroups earlier); its finish re-polls
+  // only those that were not
+  FinPf fpf{};
+  if (fin) fpf = fin_prefetch(a, ft);
   auto finish = [&] {
-    if (fin && !(diag_mask(a.skip) & (8192 | 16384))) lag_tile_finish(a, ft, err);  // (8192: ablation, no tile finish)
+    if (fin && !(diag_mask(a.skip) & (8192 | 16384))) lag_tile_finish(a, ft, err, &fpf);  // (8192: ablation, no tile finish)
   };
   if (dec) {
     decode_block<true>(a, lds, b, ds, de, count, publish, finish);
@@ -2956,6 +2975,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
       }
     }
     c->dbg_on = value != 0;
+  } else if (key == LSMBLK_DEBUG_ROT_POISON && kDiag) {  // fault injection: diagnostics builds only
+    c->rot_poison = value;
   } else if (key == LSMBLK_DEBUG_DECODE_LAG_BYTES) {
     c->dec_lag_bytes = value;
   } else if (key == LSMBLK_DEBUG_DECODE_LAG && value == 0) {  // the default

@@ -254,6 +254,8 @@ class RangeShard:
     def b_end(self):
         """The last key of this range's input b run (run nrun - 1), or None if it holds none: the
         maximum over the ranges is b's last key over the whole compaction."""
+        if self.dev.type == "cuda":
+            self.stream.synchronize()  # the input may have been decoded on the shard's stream (ADVICE round 4)
         a, b = int(self.rs[self.nrun - 1].item()) & 0xFFFFFFFF, int(self.rs[self.nrun].item()) & 0xFFFFFFFF
         if b <= a:
             return None

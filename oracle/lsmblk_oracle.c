@@ -512,6 +512,15 @@ done:
 int orc_shard_rotation(const orc_kv* ext, uint64_t m, int last, uint64_t p, uint64_t d0, size_t block_size,
                        uint64_t target, uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg, uint64_t* p_out,
                        uint64_t* d_out) {
+  return orc_shard_rotation_ex(ext, NULL, m, last, p, d0, block_size, target, seg_start, seg_cap, nseg, p_out, d_out);
+}
+
+/* The same with the loop's own same_as_last_key per ext entry (same != NULL): a two-level
+ * (TwoMergeIterator) compaction, where a dropped bottom-level tombstone moves last_key
+ * (src/compact.rs:244-254) so that "same" is not the previous kept entry's key. */
+int orc_shard_rotation_ex(const orc_kv* ext, const uint8_t* same_in, uint64_t m, int last, uint64_t p, uint64_t d0,
+                          size_t block_size, uint64_t target, uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg,
+                          uint64_t* p_out, uint64_t* d_out) {
   const uint64_t n = ext->n;
   uint64_t g = 0, data_len = d0;
   *nseg = 0;
@@ -523,7 +532,7 @@ int orc_shard_rotation(const orc_kv* ext, uint64_t m, int last, uint64_t p, uint
   for (uint64_t e = p; e < n; ++e) {
     const uint8_t* k = ext->keys + ext->key_off[e];
     size_t kl = ext->key_off[e + 1] - ext->key_off[e];
-    int same = e > 0 && same_key(ext, e - 1, e);
+    int same = same_in ? same_in[e] != 0 : (e > 0 && same_key(ext, e - 1, e));
     if (e > p && data_len >= target && !same) {              /* a new SST starts at e */
       if (e >= m) { *p_out = e - m; *d_out = 0; rc = ORC_OK; break; }
       ++g;

@@ -116,6 +116,11 @@ int orc_compact(const orc_kv* in, const uint32_t* src, uint64_t n, uint64_t wate
 int orc_shard_rotation(const orc_kv* ext, uint64_t m, int last, uint64_t p, uint64_t d0, size_t block_size,
                        uint64_t target, uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg, uint64_t* p_out,
                        uint64_t* d_out);
+/* orc_shard_rotation with the loop's same_as_last_key per ext entry (two-level compactions);
+ * same == NULL: the previous ext entry's key. */
+int orc_shard_rotation_ex(const orc_kv* ext, const uint8_t* same, uint64_t m, int last, uint64_t p, uint64_t d0,
+                          size_t block_size, uint64_t target, uint32_t* seg_start, uint64_t seg_cap, uint64_t* nseg,
+                          uint64_t* p_out, uint64_t* d_out);
 
 /* CRC-32/ISO-HDLC (crc32fast 1.4.0 == zlib crc32), used by SST framing. */
 uint32_t orc_crc32(const uint8_t* p, size_t n);

@@ -54,6 +54,8 @@ def lib():
                                   ctypes.POINTER(U64)]
         L.orc_shard_rotation.argtypes = [P, U64, I, U64, U64, S, U64, P, U64, ctypes.POINTER(U64),
                                          ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.orc_shard_rotation_ex.argtypes = [P, P, U64, I, U64, U64, S, U64, P, U64, ctypes.POINTER(U64),
+                                            ctypes.POINTER(U64), ctypes.POINTER(U64)]
         _lib = L
     return _lib
 
@@ -217,14 +219,18 @@ def compact(kv: KV, src, watermark, bottom, prefixes, block_size, target):
                 sst_ent=sst_ent[:nsst.value + 1], kept=kept[:nk.value])
 
 
-def shard_rotation(ext: KV, m: int, last: bool, p: int, d0: int, block_size: int, target: int):
+def shard_rotation(ext: KV, m: int, last: bool, p: int, d0: int, block_size: int, target: int, same=None):
     """compact_generate_sst's rotation resumed at a range's carry-in (orc_shard_rotation) ->
-    (rc, segments u32[nseg+1], (p_out, d_out))."""
+    (rc, segments u32[nseg+1], (p_out, d_out)).  same: the loop's same_as_last_key per ext entry
+    (two-level compactions; None: the previous entry's key)."""
     seg = np.zeros(ext.n + 3, np.uint32)
     ns, po, do = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
     c = ext._c()
-    rc = lib().orc_shard_rotation(ctypes.byref(c), m, int(bool(last)), p, d0, block_size, target, seg.ctypes.data,
-                                  len(seg), ctypes.byref(ns), ctypes.byref(po), ctypes.byref(do))
+    sm = None if same is None else np.ascontiguousarray(same, np.uint8)
+    assert sm is None or len(sm) >= ext.n
+    rc = lib().orc_shard_rotation_ex(ctypes.byref(c), None if sm is None else sm.ctypes.data, m, int(bool(last)), p,
+                                     d0, block_size, target, seg.ctypes.data, len(seg), ctypes.byref(ns),
+                                     ctypes.byref(po), ctypes.byref(do))
     return rc, seg[:ns.value + 1] if ns.value else seg[:0], (po.value, do.value)
 
 

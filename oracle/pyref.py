@@ -328,15 +328,18 @@ def two_merge_runs(runs):
     return drain(two_merge_iter(runs))
 
 
-def two_merge_rule(runs):
+def two_merge_rule(runs, kb=Ellipsis):
     """The closed form the GPU evaluates for LSMBLK_MERGE_TWO_LEVEL (lsmblk_compact.hip), b =
     runs[-1]: nothing past b's last key kb (and nothing at all for an empty b); a key of the upper
     runs only: its lowest-index upper run's versions (below kb); a key of b only: all of b's
-    versions; a key of both: b's 2nd, 4th, ... versions, then (below kb) the upper run's."""
+    versions; a key of both: b's 2nd, 4th, ... versions, then (below kb) the upper run's.
+    kb given (a key range of a sharded compaction, whose runs are the range's slices): the whole
+    compaction's b last key, None for an empty b."""
     upper, b = runs[:-1], runs[-1]
-    if not b:
+    if kb is Ellipsis:
+        kb = b[-1][0] if b else None
+    if kb is None:
         return []
-    kb = b[-1][0]
     owner, av, bv = {}, {}, {}
     for r, run in enumerate(upper):
         for e in run:
@@ -435,6 +438,32 @@ def compact_generate_sst(it, watermark, bottom_level, prefixes, block_size, targ
     if builder is not None:  # :301-309
         new_sst.append(builder.build())
     return new_sst
+
+
+def compact_rules_trace(entries, watermark, bottom_level, prefixes=()):
+    """The rules half of compact_generate_sst (src/compact.rs:239-297) over a merged entry list:
+    [(entry, same_as_last_key)] for every entry handed to SsTableBuilder::add, with the loop's
+    own same_as_last_key (a dropped bottom-level tombstone moves last_key, :244-254; a prefix-filter
+    drop does not).  The rotation (:278-289) reads only those flags, so the rules and the rotation
+    separate."""
+    out, last_key, first_below = [], b"", False
+    for key, ts, value in entries:
+        same = key == last_key
+        if not same:
+            first_below = True
+        if bottom_level and not same and ts <= watermark and len(value) == 0:
+            last_key, first_below = key, False
+            continue
+        if ts <= watermark:
+            if same and not first_below:
+                continue
+            first_below = False
+            if any(key.startswith(p) for p in prefixes):
+                continue
+        out.append(((key, ts, value), same))
+        if not same:
+            last_key = key
+    return out
 
 
 def compact_filter_rule(entries, watermark, bottom_level, prefixes=()):

@@ -123,6 +123,22 @@ def test_merge_errors():
     assert e.value.status == LSMBLK_E_MALFORMED
 
 
+def test_merge_rejects_keys_over_64k():
+    """A key over 65 535 bytes is refused with LSMBLK_E_INVAL (the merge tiles keep
+    u16 key lengths, so 65 537 and 1 bytes would compare as one length); 65 535 bytes still merge."""
+    a, b = b"k" * 65536 + b"a", b"k"
+    kv, rs = kv_runs([[(a, 2, b"x")], [(b, 1, b"y")]])
+    with pytest.raises(LsmBlkError) as e:
+        batch.merge_runs(to_dev(kv), rs)
+    assert e.value.status == LSMBLK_E_INVAL
+    with pytest.raises(LsmBlkError) as e:
+        batch.compact_runs(to_dev(kv), rs, 0, False, (), 4096, 1 << 20)
+    assert e.value.status == LSMBLK_E_INVAL
+    a2 = b"k" * 65534 + b"a"
+    kv, rs = kv_runs([[(a2, 2, b"x")], [(b, 1, b"y"), (a2, 1, b"z")]])
+    assert dev_entries(batch.merge_runs(to_dev(kv), rs)) == [(b, 1, b"y"), (a2, 2, b"x")]
+
+
 # ---------------------------------------------------------------- two-level (TwoMergeIterator) input
 from test_merge_oracle import DIFF_CLASSES, WEEK1_DAY5  # noqa: E402  (fixture tables, CPU-side data)
 
@@ -282,20 +298,30 @@ def test_sst_rotation_vs_restated_loop(bs, target):
 def test_sst_rotation_large_capacity_long_chain(versions):
     """A capacity far above 2^17 (n + 2 ~ 2^18, so every doubling level runs and no walk / fill
     does) with a long chain (64-B blocks and target 1: one entry per block and an SST at every key
-    change, 10^4 - 10^5 of them): bit-exact, and bounded in time -- the fill's serial loads never grow
-    with the capacity (K = lc - 9 made each fill thread follow ~sst_cap / 512 elements)."""
-    import time
+    change, 10^4 - 10^5 of them): bit-exact, and no serial chain walk that grows with the capacity
+    (K = lc - 9 made each fill thread follow ~sst_cap / 512 elements) -- checked on
+    the launches themselves (the context's kernel log), not on wall-clock time."""
+    from lsm_amd._lib import check, kernel_log, lib
     keys, ko, vals, vo, ts, rs = synth.gen_runs(200000 // versions, nrun=2, seed=17, versions=versions)
     kv = O.KV(keys, ko, vals, vo, ts)
     kept = O.gather(kv, O.merge_runs(kv, rs))
     want = O.segment_like_compaction(kept, 64, 1)
     d = to_dev(kept)
-    batch.sst_rotation(d, 64, 1)
-    t0 = time.perf_counter()
-    got = batch.sst_rotation(d, 64, 1)
-    dt = time.perf_counter() - t0
+    ctx = batch._ctx(torch.cuda.current_device())
+    torch.cuda.synchronize()
+    check(lib().lsmblk_debug_set(ctx, 2, 1))
+    try:
+        kernel_log(ctx)  # empties the log
+        got = batch.sst_rotation(d, 64, 1)
+        log = kernel_log(ctx)
+    finally:
+        check(lib().lsmblk_debug_set(ctx, 2, 0))
     np.testing.assert_array_equal(got, want)
-    assert kept.n + 2 > (1 << 17) and len(want) > 20000 and dt < 0.5, (kept.n, len(want), dt)
+    cap = kept.n + 2
+    levels = int(np.ceil(np.log2(cap)))
+    assert cap > (1 << 17) and len(want) > 20000, (kept.n, len(want))
+    assert "rot_walk_kernel" not in log and "rot_fill_kernel" not in log, log
+    assert log["rot_chain_kernel"][0] <= levels, (log["rot_chain_kernel"], levels)
 
 
 def test_sst_rotation_unsorted_and_long_keys():
