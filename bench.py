@@ -27,6 +27,7 @@ scaling: every rank owns its own batch; no collective on the data path, only the
 barrier / max-reduce).
 """
 import argparse
+import gc
 import json
 import os
 import platform
@@ -60,9 +61,10 @@ def parse(argv=None):
     p.add_argument("--config", default="U", choices=["U", "Z", "M", "C"])
     p.add_argument("--blocks", type=int, default=None, help="blocks per GPU (default 1 Mi for U/Z/C, 64 Ki for M)")
     p.add_argument("--segment-bytes", type=int, default=2 << 20)
-    p.add_argument("--ranges-per-gpu", type=int, default=1,
-                   help="config C: key ranges per GPU (each under one call's 4 GiB KV arenas); e.g. "
-                        "--blocks 3145728 --ranges-per-gpu 3 is 12.5 GiB of input per GPU (100 GiB on 8)")
+    p.add_argument("--ranges-per-gpu", type=int, default=None,
+                   help="config C: key ranges per GPU (each under one call's 4 GiB KV arenas; default 1 at "
+                        "N=1, and at N>1 3 ranges of 1 Mi blocks = 12.5 GiB of input per GPU, 100 GiB on 8: "
+                        "SURVEY.md section 8(d) config 5)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip the Z / M / C extra configs at N=1")
@@ -474,8 +476,35 @@ def oracle_check_range(hostb, rs, opts, sh, res, lo=None, hi=None):
     return res["nblk"] if ok else 0
 
 
+C_RANGES_NGPU = 3          # config C at N > 1: key ranges per GPU by default ...
+C_RANGE_BLOCKS = 1 << 20   # ... of 1 Mi input blocks each (12.5 GiB per GPU: configs[4]'s 100 GiB on 8)
+C_BLOCK_BYTES = 4033       # mean encoded 4 KiB input block (SURVEY.md section 8 table, U-shaped data)
+
+
+def c_plan(args, world):
+    """(ranges per GPU, input blocks per GPU) of config C: as given, else 1 x 1 Mi at N = 1 and
+    C_RANGES_NGPU x C_RANGE_BLOCKS at N > 1 (the north star's 100 GiB compaction on 8 GPUs)."""
+    R = args.ranges_per_gpu or (C_RANGES_NGPU if world > 1 else 1)
+    blocks = args.blocks or (R * C_RANGE_BLOCKS if world > 1 and args.ranges_per_gpu is None else 1 << 20)
+    return R, blocks
+
+
+def c_plan_summary(args, world):
+    R, blocks = c_plan(args, world)
+    per = blocks * C_BLOCK_BYTES
+    return {"ranges_per_gpu": R, "input_blocks_per_gpu": blocks, "blocks_per_range": blocks // R,
+            "input_gb_per_gpu": round(per / 1e9, 2), "input_gib_per_gpu": round(per / GiB, 2),
+            "total_input_gb": round(world * per / 1e9, 1)}
+
+
+def host_rss_gib():
+    """This process's peak resident host memory (GiB)."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / (1 << 20)
+
+
 def run_compaction(args, steps, warmup, rank, world, local, dev, extra=False):
-    if world > 1 or args.ranges_per_gpu > 1:
+    if world > 1 or c_plan(args, world)[0] > 1:
         return run_compaction_sharded(args, steps, warmup, rank, world, local, dev)
     nblk_in = args.blocks or (1 << 20)
     nrun = 8
@@ -594,8 +623,8 @@ def range_input(sl_lo, sl_hi, lo, hi, nrun, dev):
     range's lower half) and sl_hi (its upper half), every block of every run whose keys meet the
     range -- BlockMeta first / last keys decide, no decode -- so a block straddling a splitter is
     read by both ranges.  Runs keep their order (run r = slice sl_lo's selected run-r blocks, then
-    sl_hi's).  Returns the device blocks, offsets, run entry starts, and the host blocks / offsets
-    for the oracle."""
+    sl_hi's).  Returns the device blocks, offsets and run entry starts (the oracle check reads the
+    blocks back from the device, one range at a time)."""
     pieces, run_start, nent = [], [0], 0
     for r in range(nrun):
         for sl, cond in ((sl_lo, lambda b, s: lo is None or s["last"][b] >= lo),
@@ -617,8 +646,7 @@ def range_input(sl_lo, sl_hi, lo, hi, nrun, dev):
     offs.append(np.array([base], np.int64))
     blocks = torch.cat(parts) if parts else torch.zeros(16, dtype=torch.uint8, device=dev)
     off = np.concatenate(offs)
-    return (blocks.contiguous(), torch.from_numpy(off.copy()).to(dev), np.array(run_start, np.uint32),
-            blocks.cpu().numpy(), off.astype(np.uint64))
+    return blocks.contiguous(), torch.from_numpy(off.copy()).to(dev), np.array(run_start, np.uint32)
 
 
 def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
@@ -634,27 +662,37 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
     included (checked per range against the oracle)."""
     import torch.distributed as dist
     from lsm_amd import shard
-    R = max(1, args.ranges_per_gpu)
+    R, blocks_gpu = c_plan(args, world)
     WR = world * R
-    nblk_range = (args.blocks or (1 << 20)) // R
+    nblk_range = blocks_gpu // R
     nrun = 8
     t0 = time.time()
-    # this rank's ranges g = rank*R .. rank*R+R-1 read storage slices g and g+1
-    slices = {k: storage_slice(k, WR, nblk_range, nrun, args.segment_bytes, dev) for k in range(rank * R, rank * R + R + 1)}
+    # this rank's ranges g = rank*R .. rank*R+R-1 read storage slices g and g+1; slices are built
+    # one ahead and freed once their second range has its input, so the host holds at most two
+    # slices' KV at a time (the oracle check later reads the range inputs back from the device)
+    slices, parts, wm_local = {}, [], 0
 
-    def splitter(k):  # the median first key of storage slice k (k = 1 .. WR-1)
-        f = sorted(slices[k]["first"])
-        return f[len(f) // 2]
-    parts = []
+    def get_slice(k):
+        nonlocal wm_local
+        if k not in slices:
+            sl = storage_slice(k, WR, nblk_range, nrun, args.segment_bytes, dev)
+            f = sorted(sl["first"])
+            sl["splitter"] = f[len(f) // 2]  # the median BlockMeta first key (k = 1 .. WR-1)
+            wm_local = max(wm_local, int(sl["host"][4].max()))
+            slices[k] = sl
+        return slices[k]
     for i in range(R):
         g = rank * R + i
-        lo = splitter(g) if g > 0 else None
-        hi = splitter(g + 1) if g + 1 < WR else None
-        blocks_i, off_i, rs, hb, ho = range_input(slices[g], slices[g + 1], lo, hi, nrun, dev)
-        parts.append((blocks_i, off_i, rs, (hb, ho), lo, hi))
+        a, b = get_slice(g), get_slice(g + 1)
+        lo = a["splitter"] if g > 0 else None
+        hi = b["splitter"] if g + 1 < WR else None
+        blocks_i, off_i, rs = range_input(a, b, lo, hi, nrun, dev)
+        parts.append((blocks_i, off_i, rs, lo, hi))
+        del slices[g], a
+        gc.collect()
     straddling = sum(int(p[1].numel() - 1) for p in parts)
     # one wm for the whole job (the reference's LsmMvccInner::watermark is global)
-    wm_local = max(int(sl["host"][4].max()) for sl in slices.values()) // 2
+    wm_local //= 2
     if world > 1:
         cdev = shard.comm_device(dev)
         wm = torch.tensor([wm_local], dtype=torch.int64, device=cdev)
@@ -670,7 +708,7 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
                               target_sst_size=args.segment_bytes, device=dev)
     stream = torch.cuda.current_stream(dev)
     kvs, decs, shards, sizes = [], [], [], []
-    for i, (blocks_i, off_i, rs, hostb, lo, hi) in enumerate(parts):
+    for i, (blocks_i, off_i, rs, lo, hi) in enumerate(parts):
         # decoded sizes bound by the encoded bytes (every entry >= 16 B encoded)
         E_i = int(blocks_i.numel())
         n, K, V = int(rs[-1]), E_i + 16, E_i + 16
@@ -686,7 +724,7 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        for (blocks_i, off_i, rs, hostb, lo, hi), kv, sd, (n, K, V) in zip(parts, kvs, decs, sizes):
+        for (blocks_i, off_i, rs, lo, hi), kv, sd, (n, K, V) in zip(parts, kvs, decs, sizes):
             batch.decode_into(blocks_i, off_i, off_i.numel() - 1, kv, sd, n, K, V)
             kv.n = n
         if ev is not None:
@@ -699,8 +737,13 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
     ok = all(sd.cpu().tolist()[3] == 0 and sd.cpu().tolist()[0] == int(p[2][-1]) for sd, p in zip(decs, parts))
     checked = 0
     if ok and not args.no_oracle_check:
-        for (blocks_i, off_i, rs, hostb, lo, hi), sh, r in zip(parts, shards, res):
+        for (blocks_i, off_i, rs, lo, hi), sh, r in zip(parts, shards, res):
+            # range by range: its input read back from the device, every host copy freed before
+            # the next range (host RSS bounded by one range's check, not by the rank's input)
+            hostb = (blocks_i.cpu().numpy(), off_i.cpu().numpy().view(np.uint64))
             c = oracle_check_range(hostb, rs, opts, sh, r, lo, hi)
+            del hostb
+            gc.collect()
             ok = ok and c == r["nblk"]
             checked += c
     # the carries chain through every range: carry-out of range g == carry-in of range g + 1
@@ -717,8 +760,10 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
     tot = torch.tensor([sum(r["nblk"] for r in res), sum(r["nbytes"] for r in res),
                         sum(r["nseg"] - int(r["first_continues"]) for r in res), sum(r["m"] for r in res),
                         sum(r["merged"] for r in res)], dtype=torch.int64, device=cdev)
+    rss = torch.tensor([host_rss_gib(), time.time() - t0], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot)
+        dist.all_reduce(rss, op=dist.ReduceOp.MAX)
     t_max, ok_all, checked_all = reduce_ranks(elapsed, ok and chain_ok, checked, world, dev)
     if rank != 0:
         return None
@@ -737,6 +782,8 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
                                "+ SST rotation with range-to-range carry + block packing",
                    "input_blocks_per_gpu": nblk, "input_entries_per_gpu": n_all, "encoded_bytes_per_gpu": E,
                    "ranges_per_gpu": R, "total_input_gib": round(world * E / GiB, 2),
+                   "host_peak_rss_gib_max_rank": round(float(rss[0].item()), 2),
+                   "wall_s_max_rank": round(float(rss[1].item()), 1),
                    "merged_entries": tot[4], "kept_entries": tot[3], "output_blocks": tot[0], "output_bytes": tot[1],
                    "output_ssts": tot[2], "target_sst_size": args.segment_bytes,
                    "parallelism": f"key-range sharded x{world}x{R} ({backend}: splitter + halo all-gather, "
@@ -799,7 +846,7 @@ def dry_run(args, rank, world, local):
         mask = 1
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "collective_world": seen, "rank_mask": mask,
-                          "local_rank": local}), flush=True)
+                          "local_rank": local, "c_extra_plan": c_plan_summary(args, world)}), flush=True)
     return 0
 
 

@@ -72,6 +72,10 @@ def test_gloo_world2_exchange():
 def test_bench_launcher_starts_world_ranks(world):
     """`bench.py --gpus N` without torchrun starts N rank processes itself (the parent touches no
     GPU); in --dry-run every rank joins one gloo group and rank 0 reports what it saw."""
+    _dry_run(world)
+
+
+def _dry_run(world):
     import json
     import subprocess
     import sys
@@ -83,6 +87,18 @@ def test_bench_launcher_starts_world_ranks(world):
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == world and line["collective_world"] == world
     assert line["rank_mask"] == (1 << world) - 1
+    return line
+
+
+@pytest.mark.timeout(240)
+def test_bench_default_c_extra_at_8_gpus_is_configs4_shape():
+    """At N = 8 the default run's compaction extra is SURVEY.md section 8(d) config 5: 3 key ranges
+    of 1 Mi input blocks per GPU, 12.7 GB of L0 input per GPU, ~100 GB on 8 (VERDICT round 4,
+    missing item 3) -- shown by the launcher's dry run, 8 gloo ranks (no GPU)."""
+    line = _dry_run(8)
+    plan = line["c_extra_plan"]
+    assert plan["ranges_per_gpu"] == 3 and plan["input_blocks_per_gpu"] == 3 << 20
+    assert 12.0 < plan["input_gb_per_gpu"] < 13.0 and 95 < plan["total_input_gb"] < 105
 
 
 def test_bench_refuses_world_mismatch():
