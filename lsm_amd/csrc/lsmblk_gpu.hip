@@ -3241,7 +3241,19 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.skip = c->skip;
   p.dbg = c->dbg_on ? c->dbg : nullptr;
   if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), 0, st, p);
+#ifndef LSMBLK_XPAD
+#define LSMBLK_XPAD 0
+#endif
+  uint32_t plan_lds = 0;
+  if (LSMBLK_XPAD) {
+    if (!c->ncu) {
+      int v = 0;
+      c->ncu = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && v > 0 ? uint32_t(v) : 256u;
+    }
+    const uint32_t nwg = (nseg + 3) / 4;
+    if ((nwg + c->ncu - 1) / c->ncu <= 2) plan_lds = 22528;  // (experiment) at most two walker workgroups per CU
+  }
+  LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), plan_lds, st, p);
   if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
