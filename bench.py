@@ -427,35 +427,37 @@ def oracle_check_compaction(host, rs, opts, buf, stats):
     return nblk if ok else 0
 
 
-def oracle_check_range(hostb, rs, opts, sh, res, lo=None, hi=None):
+def oracle_check_range(blocks_dev, off_dev, rs, opts, sh, res, lo=None, hi=None):
     """One range of the sharded compaction against the C oracle: the range's kept stream ==
     the oracle's decode of the range's input blocks + orc_merge_runs + compact_generate_sst's rules,
     restricted to the range's keys [lo, hi); its segments, carry-out and blocks ==
     compact_generate_sst resumed at the received carry-in (orc_shard_rotation) over that stream +
     the received halo.  Chained over the ranks (carry-out r == carry-in r+1, checked by the caller)
-    this is the whole single-stream compaction."""
+    this is the whole single-stream compaction.  Host memory: one range at a time, every
+    intermediate dropped as soon as the next one exists (a few copies of the range's KV at most)."""
     from oracle import oracle as O
     t = time.time()
-    rc, kv = O.decode_blocks(*hostb)
+    rc, kv = O.decode_blocks(blocks_dev.cpu().numpy(), off_dev.cpu().numpy().view(np.uint64))
     assert rc == 0 and kv.n == int(rs[-1])
     src = O.merge_runs(kv, rs)
-    kept = O.gather(kv, src[O.compact(kv, src, opts["watermark"], opts["bottom_level"], (), opts["block_size"],
-                                      1 << 62)["kept"]])
+    idx = src[O.compact(kv, src, opts["watermark"], opts["bottom_level"], (), opts["block_size"], 1 << 62,
+                        kept_only=True)["kept"]].astype(np.int64)
+    del src
     if lo is not None or hi is not None:  # the kept stream is sorted: [lo, hi) is an index interval
-        ko = kept.key_off.astype(np.int64)
+        ko = kv.key_off
 
         def first_at_least(bound):
-            a, b = 0, kept.n
+            a, b = 0, len(idx)
             while a < b:
                 m = (a + b) // 2
-                if bytes(kept.keys[ko[m]:ko[m + 1]]) < bound:
+                if bytes(kv.keys[ko[idx[m]]:ko[idx[m] + 1]]) < bound:
                     a = m + 1
                 else:
                     b = m
             return a
-        i0 = 0 if lo is None else first_at_least(lo)
-        i1 = kept.n if hi is None else first_at_least(hi)
-        kept = O.gather(kept, np.arange(i0, i1, dtype=np.int64))
+        idx = idx[0 if lo is None else first_at_least(lo):len(idx) if hi is None else first_at_least(hi)]
+    kept = O.gather(kv, idx)
+    del kv, idx
     m = sh.m
     ok = kept.n == m
     ek, eko, ev, evo, ets = batch.KVStream(sh.ext.keys, sh.ext.key_off, sh.ext.vals, sh.ext.val_off, sh.ext.ts,
@@ -463,12 +465,14 @@ def oracle_check_range(hostb, rs, opts, sh, res, lo=None, hi=None):
     ok = ok and np.array_equal(eko[:m + 1], kept.key_off) and np.array_equal(evo[:m + 1], kept.val_off)
     ok = ok and np.array_equal(ets[:m], kept.ts) and np.array_equal(ek[:kept.key_off[-1]], kept.keys)
     ok = ok and np.array_equal(ev[:kept.val_off[-1]], kept.vals)
+    del kept
     if ok:
         ext = O.KV(ek, eko, ev, evo, ets)
         rc, seg, cout = O.shard_rotation(ext, m, sh.last, *res["carry_in"], opts["block_size"], opts["target_sst_size"])
         ok = rc == 0 and cout == res["carry_out"] and seg.tolist() == res["seg_start"].tolist()
         if ok and len(seg):
             rc, blk, off = O.encode_span(ext, seg, opts["block_size"])
+            del ext, ek, ev
             ok = rc == 0 and np.array_equal(blk, res["blocks"].cpu().numpy())
             ok = ok and np.array_equal(off, res["blk_off"].cpu().numpy().view(np.uint64))
     log(f"[rank] oracle check of the range ({res['nblk']} output blocks, {res['nseg']} segments, carry "
@@ -605,7 +609,8 @@ def storage_slice(k, WR, nblk_range, nrun, seg_bytes, dev):
     overlapping runs of seg_bytes SSTs) holding half-slices 2k-1 and 2k of the key space cut into
     2 WR (the first and the last storage slice hold one half-slice).  Deterministic in k, so
     every rank that reads a slice builds the same blocks.  Returns the blocks, their offsets,
-    each run's first block, every block's first / last key and first entry, and the host KV."""
+    each run's first block, every block's first / last key and first entry, and the largest ts
+    (the host KV is dropped: the oracle check reads the range inputs back from the device)."""
     h0, h1 = max(2 * k - 1, 0), min(2 * k + 1, 2 * WR)
     blocks, off, rs, host, run_blk = build_runs(nblk_range * (h1 - h0) // 2, nrun, seg_bytes, 3000 + k, dev,
                                                 key_slice=(h0, 2 * WR, h1 - h0), with_run_blk=True)
@@ -614,8 +619,10 @@ def storage_slice(k, WR, nblk_range, nrun, seg_bytes, dev):
     keys, ko = host[0], host[1]
     first = [bytes(keys[ko[ent[b]]:ko[ent[b] + 1]]) for b in range(len(ent) - 1)]
     last = [bytes(keys[ko[ent[b + 1] - 1]:ko[ent[b + 1]]]) for b in range(len(ent) - 1)]
+    ts_max = int(host[4].max())
+    del host, keys, ko
     return dict(blocks=blocks, off=off.cpu().numpy().view(np.uint64).astype(np.int64), run_blk=run_blk,
-                first=first, last=last, ent=ent, host=host)
+                first=first, last=last, ent=ent, ts_max=ts_max)
 
 
 def range_input(sl_lo, sl_hi, lo, hi, nrun, dev):
@@ -678,7 +685,7 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
             sl = storage_slice(k, WR, nblk_range, nrun, args.segment_bytes, dev)
             f = sorted(sl["first"])
             sl["splitter"] = f[len(f) // 2]  # the median BlockMeta first key (k = 1 .. WR-1)
-            wm_local = max(wm_local, int(sl["host"][4].max()))
+            wm_local = max(wm_local, sl["ts_max"])
             slices[k] = sl
         return slices[k]
     for i in range(R):
@@ -740,9 +747,7 @@ def run_compaction_sharded(args, steps, warmup, rank, world, local, dev):
         for (blocks_i, off_i, rs, lo, hi), sh, r in zip(parts, shards, res):
             # range by range: its input read back from the device, every host copy freed before
             # the next range (host RSS bounded by one range's check, not by the rank's input)
-            hostb = (blocks_i.cpu().numpy(), off_i.cpu().numpy().view(np.uint64))
-            c = oracle_check_range(hostb, rs, opts, sh, r, lo, hi)
-            del hostb
+            c = oracle_check_range(blocks_i, off_i, rs, opts, sh, r, lo, hi)
             gc.collect()
             ok = ok and c == r["nblk"]
             checked += c

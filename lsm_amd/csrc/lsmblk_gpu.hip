@@ -3141,7 +3141,10 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     if (a.dbg && hipMemsetAsync(a.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     a.tag = c->epoch;
     a.poll = c->poll;
-    LSM_LAUNCH_SLOT(2, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), 0, st, a);
+#ifndef LSMBLK_XDECPAD
+#define LSMBLK_XDECPAD 0
+#endif
+    LSM_LAUNCH_SLOT(2, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), LSMBLK_XDECPAD, st, a);
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
   if (flags & LSMBLK_DECODE_VERIFY_CRC) {
@@ -3281,10 +3284,13 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
+#ifndef LSMBLK_XEMITPAD
+#define LSMBLK_XEMITPAD 0
+#endif
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, LSMBLK_XEMITPAD) != hipSuccess || per_cu < 1)
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
-  LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), LSMBLK_XEMITPAD, st, e);
   LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), 0, st, e);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }

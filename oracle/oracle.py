@@ -191,18 +191,25 @@ def gather(kv: KV, idx) -> KV:
     return KV(cat(kv.keys, kv.key_off, kl), ko, cat(kv.vals, kv.val_off, vl), vo, kv.ts[idx].copy())
 
 
-def compact(kv: KV, src, watermark, bottom, prefixes, block_size, target):
+def compact(kv: KV, src, watermark, bottom, prefixes, block_size, target, kept_only=False):
     """compact_generate_sst over the merged stream kv[src] -> dict(blocks, blk_off, sst_blk,
-    sst_ent, kept) (kept = merged positions added to an SST)."""
+    sst_ent, kept) (kept = merged positions added to an SST).  kept_only: only `kept` (no output
+    buffers: the rules alone, for a range check that needs just the kept stream)."""
     src = np.ascontiguousarray(src, np.uint32)
     n = len(src)
-    kl = int((kv.key_off[src.astype(np.int64) + 1] - kv.key_off[src]).sum()) if n else 0
-    vl = int((kv.val_off[src.astype(np.int64) + 1] - kv.val_off[src]).sum()) if n else 0
-    out_cap = kl + vl + 18 * n + 16
-    out = np.zeros(max(out_cap, 1), np.uint8)
-    blk_off = np.zeros(n + 2, np.uint64)
-    sst_blk = np.zeros(n + 2, np.uint32)
-    sst_ent = np.zeros(n + 2, np.uint32)
+    if kept_only:
+        out_cap, out, blk_off, sst_blk, sst_ent = 0, np.zeros(1, np.uint8), np.zeros(1, np.uint64), \
+            np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        bcap = scap = 0
+    else:
+        kl = int((kv.key_off[src.astype(np.int64) + 1] - kv.key_off[src]).sum()) if n else 0
+        vl = int((kv.val_off[src.astype(np.int64) + 1] - kv.val_off[src]).sum()) if n else 0
+        out_cap = kl + vl + 18 * n + 16
+        out = np.zeros(max(out_cap, 1), np.uint8)
+        blk_off = np.zeros(n + 2, np.uint64)
+        sst_blk = np.zeros(n + 2, np.uint32)
+        sst_ent = np.zeros(n + 2, np.uint32)
+        bcap = scap = n + 2
     kept = np.zeros(max(n, 1), np.uint32)
     pf = [bytes(p) for p in prefixes]
     pbufs = [ctypes.create_string_buffer(p, len(p)) for p in pf]
@@ -212,8 +219,11 @@ def compact(kv: KV, src, watermark, bottom, prefixes, block_size, target):
     c = kv._c()
     rc = lib().orc_compact(ctypes.byref(c), src.ctypes.data if n else None, n, watermark, int(bool(bottom)),
                            parr, plen, len(pf), block_size, target, out.ctypes.data, out_cap, blk_off.ctypes.data,
-                           len(blk_off), sst_blk.ctypes.data, sst_ent.ctypes.data, len(sst_blk), kept.ctypes.data,
+                           bcap, sst_blk.ctypes.data, sst_ent.ctypes.data, scap, kept.ctypes.data,
                            len(kept), ctypes.byref(nb), ctypes.byref(nbytes), ctypes.byref(nsst), ctypes.byref(nk))
+    if kept_only:
+        assert rc in (ORC_OK, ORC_E_CAPACITY) and nk.value <= len(kept), rc
+        return dict(kept=kept[:nk.value])
     assert rc == ORC_OK, rc
     return dict(blocks=out[:nbytes.value], blk_off=blk_off[:nb.value + 1], sst_blk=sst_blk[:nsst.value + 1],
                 sst_ent=sst_ent[:nsst.value + 1], kept=kept[:nk.value])
@@ -239,8 +249,12 @@ def encode_span(kv: KV, seg, block_size: int):
     seg = np.asarray(seg, np.int64)
     if len(seg) < 2:
         return 0, np.zeros(0, np.uint8), np.zeros(1, np.uint64)
-    sub = gather(kv, np.arange(seg[0], seg[-1]))
-    return encode_segments(sub, (seg - seg[0]).astype(np.uint32), block_size)
+    a, b = int(seg[0]), int(seg[-1])
+    ka, va = int(kv.key_off[a]), int(kv.val_off[a])
+    # entries [a, b) as views of the arenas (only the offsets are rebased, no byte copy)
+    sub = KV(kv.keys[ka:int(kv.key_off[b])], (kv.key_off[a:b + 1] - ka).astype(np.uint32),
+             kv.vals[va:int(kv.val_off[b])], (kv.val_off[a:b + 1] - va).astype(np.uint32), kv.ts[a:b])
+    return encode_segments(sub, (seg - a).astype(np.uint32), block_size)
 
 
 class Builder:
