@@ -247,6 +247,13 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
             "windows": q(tr[:, 3]), "blocks": q(tr[:, 7]),
             "helper_us": q((tr[:, 5] - tr[:, 4]) / 100), "helper_wait_frac": q(tr[:, 6] / np.maximum(1, tr[:, 5] - tr[:, 4])),
             "walk_end_us": q((tr[:, 1] - t0) / 100)}}), flush=True)
+        # where the slow walkers ran: walk time by XCD, by SE, by SIMD (HW_ID / XCC_ID in word 7)
+        walk = (tr[:, 1] - tr[:, 0]) / 100
+        hw = (tr[:, 7] >> 32) & 0xFFFFFF
+        xcc = (tr[:, 7] >> 56) & 0xF
+        groups = {"xcc": xcc, "se": (hw >> 13) & 3, "simd": (hw >> 4) & 3, "cu": (hw >> 8) & 0xF}
+        print(json.dumps({"plan_walk_us_by": {g: {int(v): [int((key == v).sum()), round(float(np.median(walk[key == v])), 1)]
+                                                  for v in np.unique(key)} for g, key in groups.items()}}), flush=True)
         return None
     if args.ablate is not None and not extra:
         if args.ablate >= 65536:  # plan masks: the plan kernel alone (emit not launched)

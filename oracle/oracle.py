@@ -183,11 +183,22 @@ def gather(kv: KV, idx) -> KV:
     vo[1:] = np.cumsum(vl)
 
     def cat(arena, off, ln):
-        if len(idx) == 0 or ln.sum() == 0:
-            return np.zeros(0, np.uint8)
+        total = int(ln.sum())
+        out = np.zeros(total, np.uint8)
+        if len(idx) == 0 or total == 0:
+            return out
         starts = off[idx].astype(np.int64)
-        rep = np.repeat(starts - np.concatenate([[0], np.cumsum(ln)[:-1]]), ln)
-        return arena[np.arange(int(ln.sum()), dtype=np.int64) + rep]
+        dst = np.concatenate([[0], np.cumsum(ln)])
+        # in chunks of entries: the per-byte int64 index arrays of one chunk only (a 4 GB arena
+        # gathered at once took 2 x 8 bytes of index per byte, ~50 GiB of host memory)
+        step = 1 << 20
+        for a in range(0, len(idx), step):
+            b = min(a + step, len(idx))
+            lo, hi = int(dst[a]), int(dst[b])
+            if hi > lo:
+                rep = np.repeat(starts[a:b] - dst[a:b], ln[a:b])
+                out[lo:hi] = arena[np.arange(lo, hi, dtype=np.int64) + rep]
+        return out
     return KV(cat(kv.keys, kv.key_off, kl), ko, cat(kv.vals, kv.val_off, vl), vo, kv.ts[idx].copy())
 
 
