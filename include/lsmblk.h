@@ -27,7 +27,12 @@
  *                                                           src/table/builder.rs:68-77)
  *       lsmblk_compact_filter_batch  compaction's per-entry keep/drop rules  (src/compact.rs:234-299)
  *     All pointers are DEVICE pointers; calls are asynchronous on `stream` (a hipStream_t
- *     passed as void*; NULL = the default stream).  Thread-safe per distinct context.
+ *     passed as void*; NULL = the default stream).  Concurrency: a context's calls are
+ *     serialised by its lock (any host thread) and its device work is ordered on the stream each
+ *     call is given; a context's workspace is reused by its next call, so work that must run
+ *     concurrently (several streams, several host threads at once) takes one context each.
+ *     Every device-side wait is bounded (LSMBLK_E_TIMEOUT) and every data-dependent walk is
+ *     bounded by its progress (LSMBLK_E_INTERNAL), so no call can leave a kernel running forever.
  *
  * Errors: every function returns 0 (LSMBLK_OK) or a negative LSMBLK_E_* code.  Where the
  * reference panics (empty key builder.rs:55, empty build :82-83, malformed decode

@@ -2101,178 +2101,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   raise_err(a.stats, err);
 }
 
-// One block per single-wave workgroup (experiment, LSMBLK_XEMIT1): no cross-block prefetch; the
-// workgroup's own loads are its block's metadata (scalar), the entry-offset bounds (scalar), then
-// the staging and per-entry loads.  Blocks bi = blockIdx.x, + gridDim.x, ... (grid <= blocks).
-__global__ __launch_bounds__(64) void emit1_kernel(EmitArgs a0) {
-  const EmitArgs a = resolve(a0);
-  __shared__ EmitLds L;
-  const uint32_t l = lane_id();
-  const uint64_t nblk = uni64(a.stats[0]);
-  uint32_t err = 0;
-  const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
-  const uint64_t lim = nblk < a.blk_cap ? nblk : (a.blk_cap ? a.blk_cap - 1 : 0);
-  cu32_t* const kfirst = kconst(a.blk_first);
-  cu64_t* const koff = kconst(a.blk_off);
-  for (uint64_t bi = blockIdx.x; bi < lim; bi += gridDim.x) {
-    const uint32_t s = kfirst[bi], e = kfirst[bi + 1], n = e - s;
-    const uint64_t O = koff[bi], size = koff[bi + 1] - O;
-    const uint32_t kb0 = uni(a.key_off[s]), kb1 = uni(a.key_off[e]), vb0 = uni(a.val_off[s]), vb1 = uni(a.val_off[e]);
-    const uint32_t klead = uint32_t((kaddr + kb0) & 15), vlead = uint32_t((vaddr + vb0) & 15);
-    const uint32_t olead = uint32_t(O & 15);
-    if (!(n <= kEmitMaxE && klead + (kb1 - kb0) + 8 <= kEmitKCap && vlead + (vb1 - vb0) + 24 <= kEmitICap &&
-          olead + size + 8 <= kEmitICap)) {
-      if (l == 0) a.big_flag[bi] = 1;
-      continue;
-    }
-    u32x4 kq[2], vq[5];
-    uint32_t pf_ko0 = 0, pf_ko1 = 0, pf_vo0 = 0, pf_vo1 = 0;
-    uint64_t pf_ts = 0;
-    {
-      const rsrc_t RK = make_rsrc(a.keys + kb0 - klead, klead + (kb1 - kb0));
-      const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
-      const rsrc_t RV = make_rsrc(a.vals + vb0 - vlead, vlead + (vb1 - vb0));
-      const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
-#pragma unroll
-      for (uint32_t i = 0; i < 2; ++i)
-        if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, kLdAux);
-#pragma unroll
-      for (uint32_t i = 0; i < 5; ++i)
-        if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, kLdAux);
-      if (l < n) {
-        pf_ko0 = a.key_off[s + l];
-        pf_ko1 = a.key_off[s + l + 1];
-        pf_vo0 = a.val_off[s + l];
-        pf_vo1 = a.val_off[s + l + 1];
-        pf_ts = a.ts[s + l];
-      }
-      const uint32_t nk2 = nk, nv2 = nv;
-#pragma unroll
-      for (uint32_t i = 0; i < 2; ++i)
-        if (l + 64 * i < nk2) *reinterpret_cast<u32x4*>(L.kimg + (l + 64 * i) * 16) = kq[i];
-#pragma unroll
-      for (uint32_t i = 0; i < 5; ++i)
-        if (l + 64 * i < nv2) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = vq[i];
-    }
-    const uint32_t fl = uint32_t(__builtin_amdgcn_readfirstlane(pf_ko1)) - kb0;  // first key length (n >= 1)
-    wave_sync();
-    const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;
-    for (uint32_t j = 4 * l; j < ncs; j += 256) *reinterpret_cast<u32x4*>(L.cent + j) = u32x4{~0u, ~0u, ~0u, ~0u};
-    uint32_t fkw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
-    uint32_t dc = 0;
-    uint32_t eh[2][4], et[2][4];
-#pragma unroll
-    for (uint32_t it = 0; it < 2; ++it) {
-      const uint32_t c = 64 * it;
-      if (c >= n) break;
-      const uint32_t k = c + l;
-      uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
-      if (k < n) {
-        uint32_t ko0, ko1, vo0, vo1;
-        if (it == 0) {
-          ko0 = pf_ko0; ko1 = pf_ko1; vo0 = pf_vo0; vo1 = pf_vo1;
-          L.ts[k] = pf_ts;
-        } else {
-          ko0 = a.key_off[s + k]; ko1 = a.key_off[s + k + 1];
-          vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1];
-          L.ts[k] = a.ts[s + k];
-        }
-        kp = ko0 - kb0;
-        kl = ko1 - ko0;
-        vp = vo0 - vb0;
-        vl = vo1 - vo0;
-        if (k != 0) {
-          const uint32_t m = fl < kl ? fl : kl;
-          uint32_t z = 16;
-#pragma unroll
-          for (int i = 3; i >= 0; --i) {
-            const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
-            z = x ? 4 * i + (__builtin_ctz(x) >> 3) : z;
-          }
-          p = z < 16 && z < m ? z : m;
-          bool done = z < 16 || m <= 16;
-          for (uint32_t q = 16; !done && q < m; q += 4) {
-            const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
-            if (x) {
-              const uint32_t zq = q + (__builtin_ctz(x) >> 3);
-              p = zq < m ? zq : m;
-              done = true;
-            }
-          }
-        }
-        const uint32_t vs = vlead + vp;
-        lds_read16(L.img, vs, eh[it]);
-        lds_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
-      }
-      const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
-      const uint32_t incl = wave_incl_scan<uint32_t>(dg);
-      const uint32_t pos = dc + incl - dg;
-      dc += __shfl(incl, 63, 64);
-      if (k < n) {
-        const uint32_t sfx = kl - p;
-        *reinterpret_cast<u32x4*>(L.erec + 4 * k) = u32x4{pos | (p << 16), (klead + kp + p) | (vl << 16), sfx, 0u};
-        const uint32_t vdb = olead + pos + 14 + sfx;
-        const uint32_t srcb = vlead + vp - vdb;
-        for (uint32_t cc = (vdb + 15) >> 4; 16 * cc + 16 <= vdb + vl; ++cc) L.cent[cc] = srcb + 16 * cc;
-      }
-    }
-    const uint32_t data_len = dc;
-    if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
-    wave_sync();
-    {
-      const int32_t top = int32_t((ncs + 63) & ~63u);
-      for (int32_t c0 = top; c0 > 0; c0 -= 64) {
-        const int32_t c = c0 - 64 + int32_t(l);
-        const uint32_t src = uint32_t(c) < ncs ? L.cent[c] : ~0u;
-        u32x4 v;
-        if (src != ~0u) v = *reinterpret_cast<const u32x4*>(L.img + src);
-        if (src != ~0u) *reinterpret_cast<u32x4*>(L.img + 16 * c) = v;
-      }
-    }
-    wave_sync();
-#pragma unroll
-    for (uint32_t it = 0; it < 2; ++it) {
-      const uint32_t k = 64 * it + l;
-      if (64 * it >= n) break;
-      if (k >= n) continue;
-      const u32x4 er = *reinterpret_cast<const u32x4*>(L.erec + 4 * k);
-      const uint32_t pos = er.x & 0xFFFF, p = er.x >> 16, ks = er.y & 0xFFFF, vl = er.y >> 16, sfx = er.z;
-      const uint32_t vd = pos + 14 + sfx;
-      const uint64_t tsv = L.ts[k];
-      uint8_t* o = L.img;
-      const uint32_t ox = olead + pos;
-      *reinterpret_cast<uint32_t*>(o + ox) = bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16);
-      for (uint32_t t = 0; t < sfx; t += 16) {
-        const uint32_t o2 = sfx >= 16 ? min(t, sfx - 16) : 0u;
-        uint32_t v[4];
-        lds_read16(L.kimg, ks + o2, v);
-        if (sfx >= 16) *reinterpret_cast<u32x4*>(o + ox + 4 + o2) = u32x4{v[0], v[1], v[2], v[3]};
-        else lds_st_short(o + ox + 4, sfx, v);
-      }
-      const uint64_t tbe = __builtin_bswap64(tsv);
-      *reinterpret_cast<u32x2*>(o + ox + 4 + sfx) = u32x2{uint32_t(tbe), uint32_t(tbe >> 32)};
-      *reinterpret_cast<uint16_t*>(o + ox + 12 + sfx) = uint16_t(bswap16(vl & 0xFFFF));
-      const uint32_t A = olead + vd;
-      if (vl >= 16) {
-        *reinterpret_cast<u32x4*>(o + A) = u32x4{eh[it][0], eh[it][1], eh[it][2], eh[it][3]};
-        *reinterpret_cast<u32x4*>(o + A + vl - 16) = u32x4{et[it][0], et[it][1], et[it][2], et[it][3]};
-      } else if (vl) {
-        lds_st_short(o + A, vl, eh[it]);
-      }
-    }
-    wave_sync();
-    for (uint32_t k = l; k < n; k += 64)
-      *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.erec[4 * k] & 0xFFFF));
-    if (l == 0) *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * n) = uint16_t(bswap16(n & 0xFFFF));
-    wave_sync();
-    if (O + size <= a.out_cap) flush_run_masked<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
-    wave_sync();
-  }
-  raise_err(a.stats, err);
-}
-
 // The blocks emit_kernel flagged as beyond its LDS image, one wave per block: wave j checks
 // blocks j, j + nw, j + 2 nw, ... 64 at a time (a flag per lane, then a ballot).
 __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
@@ -3460,15 +3288,6 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
 #ifndef LSMBLK_XEMITPAD
 #define LSMBLK_XEMITPAD 0
 #endif
-#ifndef LSMBLK_XEMIT1
-#define LSMBLK_XEMIT1 0
-#endif
-  if (LSMBLK_XEMIT1) {  // (experiment) one block per single-wave workgroup, grid = min(blocks bound, cap)
-    const uint64_t g1 = std::min<uint64_t>(blk_cap > 1 ? blk_cap - 1 : 1, uint64_t(LSMBLK_XEMIT1));
-    LSM_LAUNCH_SLOT(4, emit1_kernel, dim3(uint32_t(g1)), dim3(64), 0, st, e);
-    LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), 0, st, e);
-    return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
-  }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, LSMBLK_XEMITPAD) != hipSuccess || per_cu < 1)
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
