@@ -509,7 +509,6 @@ struct lsmblk_ctx {
   int device = 0;
   std::mutex mu;
   uint32_t* counters = nullptr;  // [0] decode ticket, [1] plan ticket, [2] emit big-block count
-  uint32_t ncu = 0;              // compute units of the device (first use)
   uint32_t* dec_agg = nullptr;   // (entries, key bytes, value bytes) per block
   uint64_t dec_cap = 0;
   void* crc_tabs = nullptr;      // CrcTabs: CRC-32 slicing + zero-extension tables (first CRC call)

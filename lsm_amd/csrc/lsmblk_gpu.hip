@@ -3142,10 +3142,7 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     if (a.dbg && hipMemsetAsync(a.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     a.tag = c->epoch;
     a.poll = c->poll;
-#ifndef LSMBLK_XDECPAD
-#define LSMBLK_XDECPAD 0
-#endif
-    LSM_LAUNCH_SLOT(2, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), LSMBLK_XDECPAD, st, a);
+    LSM_LAUNCH_SLOT(2, decode_lag_kernel, dim3(uint32_t(nblk + a.lag)), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
   if (flags & LSMBLK_DECODE_VERIFY_CRC) {
@@ -3245,19 +3242,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.skip = c->skip;
   p.dbg = c->dbg_on ? c->dbg : nullptr;
   if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-#ifndef LSMBLK_XPAD
-#define LSMBLK_XPAD 0
-#endif
-  uint32_t plan_lds = 0;
-  if (LSMBLK_XPAD) {
-    if (!c->ncu) {
-      int v = 0;
-      c->ncu = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && v > 0 ? uint32_t(v) : 256u;
-    }
-    const uint32_t nwg = (nseg + 3) / 4;
-    if ((nwg + c->ncu - 1) / c->ncu <= 2) plan_lds = 22528;  // (experiment) at most two walker workgroups per CU
-  }
-  LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), plan_lds, st, p);
+  LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), 0, st, p);
   if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
@@ -3285,13 +3270,10 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   int per_cu = 0;
-#ifndef LSMBLK_XEMITPAD
-#define LSMBLK_XEMITPAD 0
-#endif
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, LSMBLK_XEMITPAD) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
-  LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), LSMBLK_XEMITPAD, st, e);
+  LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), 0, st, e);
   LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), 0, st, e);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
