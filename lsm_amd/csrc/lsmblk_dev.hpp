@@ -370,6 +370,20 @@ struct alignas(16) CrcTabs {
   uint32_t unz[3][8][16];            // Z(., t)^-1, t = 1..3: undoes t appended zero bytes
   uint32_t z32[8][16];               // Z(., 32): joins a window's two fold chains
 };
+// crc_stream_kernel (the plain CRC pass): the stride step Z(., 256) as four byte tables (each
+// workgroup replicates them 32 times in LDS), the joins as nibble maps.
+struct alignas(16) CrcStreamTabs {
+  uint32_t a256[4][256];             // a256[k][v] = Z(v << 8k, 256)
+  uint32_t unz4[8][16];              // Z(., 4)^-1: a lane's four dword chains
+  uint32_t unzl[4][8][16];           // Z(., 16 << b)^-1, b = 0..3: the lane tree of a 16-lane row
+  uint32_t z4096[8][16];             // Z(., 4096): chunk after chunk
+  uint32_t unzt[16][8][16];          // Z(., t)^-1: t tail zero bytes (t = 0 unused)
+  uint32_t zinit[260];               // zinit[m] = Z(0xFFFFFFFF, 16 m), m = 0..256
+};
+struct alignas(16) CrcAllTabs {
+  CrcTabs t;
+  CrcStreamTabs s;
+};
 
 // 4 * (byte B of v & 15 << 2 ...): (byte B of v) & 0x3C as one SDWA instruction
 template <int B>
@@ -497,6 +511,45 @@ inline void crc_host_tables(CrcTabs& T) {
       col[bit] = x;
     }
     crc_nibble_tables(col, T.shift[j]);
+  }
+}
+// columns of Z(., bytes) (bytes > 0) or Z(., -bytes)^-1 (bytes < 0)
+inline void crc_shift_cols(int64_t bytes, uint32_t (&col)[32]) {
+  for (uint32_t bit = 0; bit < 32; ++bit) {
+    uint32_t x = 1u << bit;
+    if (bytes >= 0)
+      for (int64_t s = 0; s < 8 * bytes; ++s) x = crc_bit_step(x);
+    else
+      for (int64_t s = 0; s < -8 * bytes; ++s) x = crc_bit_unstep(x);
+    col[bit] = x;
+  }
+}
+inline void crc_stream_host_tables(CrcStreamTabs& T) {
+  uint32_t col[32];
+  crc_shift_cols(256, col);
+  for (uint32_t k = 0; k < 4; ++k)
+    for (uint32_t v = 0; v < 256; ++v) {
+      uint32_t y = 0;
+      for (uint32_t bit = 0; bit < 8; ++bit)
+        if ((v >> bit) & 1) y ^= col[8 * k + bit];
+      T.a256[k][v] = y;
+    }
+  crc_shift_cols(-4, col);
+  crc_nibble_tables(col, T.unz4);
+  for (uint32_t b = 0; b < 4; ++b) {
+    crc_shift_cols(-(int64_t(16) << b), col);
+    crc_nibble_tables(col, T.unzl[b]);
+  }
+  crc_shift_cols(4096, col);
+  crc_nibble_tables(col, T.z4096);
+  for (uint32_t t = 0; t < 16; ++t) {
+    crc_shift_cols(-int64_t(t), col);
+    crc_nibble_tables(col, T.unzt[t]);
+  }
+  uint32_t z = 0xFFFFFFFFu;
+  for (uint32_t m = 0; m < 260; ++m) {
+    T.zinit[m] = z;
+    for (int s = 0; s < 128; ++s) z = crc_bit_step(z);
   }
 }
 
@@ -690,10 +743,13 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
 // lsmblk_encode_segment_blocks for the encode that just ran on this context.
 int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
                           uint32_t* seg_blk, hipStream_t st);
-// CRC tables on the context (first use) and the crc_kernel launch over [blk_off[b], blk_off[b+1] - tail).
+// CRC tables on the context (first use) and the CRC launch over [blk_off[b], blk_off[b+1] - tail):
+// crc_stream_kernel, or crc_kernel<true> when agg takes the per-block counts as well, or
+// crc_kernel<false> for a few long ranges (sections: a wave per range, its 4 KiB chunks one after
+// another, keeps more waves busy than a 16-lane row per range).
 int ensure_crc_tabs(lsmblk_ctx* c);
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
-               uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg = nullptr);
+               uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg = nullptr, bool sections = false);
 // lsmblk_block_meta_batch with the context lock held.
 int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                       const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off,

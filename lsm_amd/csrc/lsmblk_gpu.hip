@@ -2365,6 +2365,164 @@ __global__ __launch_bounds__(256) void crc_kernel(CrcArgs a) {
   raise_err(a.stats, err);
 }
 
+// ---------------------------------------------------------------- streaming CRC (the plain pass)
+// crc_kernel folds each lane's contiguous 68-B window, so it stages every chunk in LDS and pays
+// eight nibble lookups per dword.  This kernel reads the blocks straight into registers
+// with coalesced 16-B loads and folds them where they land:
+//   * a wave takes 4 consecutive blocks, a 16-lane row each; a block of L bytes is cut into
+//     4 KiB chunks of the padded message 0^P || M || 0^T (T = -L mod 16, P a multiple of 16 that
+//     fills the first chunk), lane r of the row holding the 16-B pieces r, r + 16, ... of a chunk;
+//   * dword i of every piece of a lane is one chain whose consecutive dwords lie 256 B apart, so
+//     every chain step is c <- Z(c ^ d, 256), the same map for all chains: four byte tables,
+//     replicated 32 times in LDS so that lane l reads copy l mod 32 (bank l mod 32: conflict-free),
+//     4 lookups per dword instead of 8;
+//   * a chain ends 16 r + 4 i bytes past the chunk end: the lane joins its four chains by
+//     Z(., 4)^-1 (Horner), the row's lanes by a DPP tree over Z(., 16 << b)^-1;
+//   * chunk after chunk acc = Z(acc, 4096) ^ R_0(chunk), starting from the init carried through
+//     the first chunk's data, Z(0xFFFFFFFF, 4096 - P); the T tail zeros come off with Z(., T)^-1.
+// Bytes outside a block are never read: padding pieces load from past the descriptor's bound
+// (zeros), and the last piece -- the block's last 16 - T bytes and T zeros -- is loaded as the
+// block's last 16 bytes and shifted down by T (byte loads when the block is shorter).
+constexpr uint32_t kCsWaves = 16;
+constexpr uint32_t kCsOob = 0x80000000u;  // a piece offset past every descriptor bound (range < 2^31)
+
+struct CrcStreamArgs {
+  const uint8_t* blocks;
+  const uint64_t* blk_off;
+  uint64_t nblk;
+  uint32_t tail;
+  uint32_t* crc;
+  const CrcStreamTabs* tabs;
+  uint64_t* stats;
+};
+
+__global__ __launch_bounds__(1024) void crc_stream_kernel(CrcStreamArgs a) {
+  __shared__ uint32_t rep[4 * 256 * 32];  // rep[(k * 256 + v) * 32 + r] = a256[k][v]
+  __shared__ CrcStreamTabs S;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = lane_id(), g = l >> 4, lq = l & 15;
+  for (uint32_t i = t; i < sizeof(CrcStreamTabs) / 16; i += 64 * kCsWaves)
+    reinterpret_cast<u32x4*>(&S)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
+  for (uint32_t e = t; e < 4 * 256 * 32; e += 64 * kCsWaves) rep[e] = (&a.tabs->a256[0][0])[e >> 5];
+  if (blockIdx.x == 0 && t == 0) {
+    a.stats[0] = a.nblk;
+    a.stats[1] = a.nblk ? a.blk_off[a.nblk] - a.blk_off[0] : 0;
+  }
+  __syncthreads();
+  const uint8_t* const R8 = reinterpret_cast<const uint8_t*>(rep);
+  const uint32_t lane4 = (l & 31) << 2;
+  // c <- Z(x, 256): byte k of x addresses copy (l mod 32) of table k
+  auto step = [&](uint32_t x) -> uint32_t {
+    const uint32_t a0 = *reinterpret_cast<const uint32_t*>(R8 + (((x << 7) & 0x7F80u) | lane4));
+    const uint32_t a1 = *reinterpret_cast<const uint32_t*>(R8 + 32768 + (((x >> 1) & 0x7F80u) | lane4));
+    const uint32_t a2 = *reinterpret_cast<const uint32_t*>(R8 + 65536 + (((x >> 9) & 0x7F80u) | lane4));
+    const uint32_t a3 = *reinterpret_cast<const uint32_t*>(R8 + 98304 + (((x >> 17) & 0x7F80u) | lane4));
+    return xor3(a0, a1, a2) ^ a3;
+  };
+  uint32_t err = 0;
+  const uint64_t ngrp = (a.nblk + 3) / 4, nw = uint64_t(gridDim.x) * kCsWaves;
+  // lanes 0..4: blk_off[4 G + lane], the group's block offsets (loaded one group ahead)
+  auto offs = [&](uint64_t G) -> uint64_t {
+    return G < ngrp && l <= 4 && 4 * G + l <= a.nblk ? a.blk_off[4 * G + l] : 0ull;
+  };
+  uint64_t G = uni64(uint64_t(blockIdx.x) * kCsWaves + w);
+  uint64_t onext = offs(G);
+  for (; G < ngrp; G += nw) {
+    const uint64_t b0 = G * 4, nb = a.nblk - b0 < 4 ? a.nblk - b0 : 4;  // blocks of this wave
+    uint64_t Sx[5];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) Sx[k] = lane64(onext, k);
+    onext = offs(G + nw);
+    const bool have = g < nb;
+    const uint64_t s = g == 0 ? Sx[0] : g == 1 ? Sx[1] : g == 2 ? Sx[2] : Sx[3];
+    const uint64_t e = g == 0 ? Sx[1] : g == 1 ? Sx[2] : g == 2 ? Sx[3] : Sx[4];
+    const bool valid = have && e >= s + a.tail && e - s <= 0x7FFFFFF0ull;
+    if (have && !valid) err |= LSMBLK_ERR_MALFORMED;
+    const uint32_t L = valid ? uint32_t(e - s) - a.tail : 0u;
+    const uint32_t T = (0u - L) & 15u, nch = (L + T + 4095) >> 12, P = (nch << 12) - L - T;
+    const uint64_t S0 = Sx[0], Se = Sx[nb];
+    // one descriptor over the wave's blocks when they lie inside [S0, Se) (adjacent ranges do)
+    const bool wave_ok = Se >= S0 && Se - S0 <= 0x7FFFFFF0ull &&
+                         __ballot(valid && (s < S0 || s + L > Se)) == 0;
+    uint32_t maxnch = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) maxnch = max(maxnch, uint32_t(__builtin_amdgcn_readlane(nch, 16 * k)));
+    uint32_t acc = S.zinit[(4096 - P) >> 4];
+    for (uint32_t c = 0; c < maxnch; ++c) {
+      const bool live = c < nch;
+      const bool tailp = live && c + 1 == nch && lq == 15 && T != 0;
+      u32x4 q[16];
+      // piece j of this lane: padded position 4096 c + 256 j + 16 lq, data offset that - P; the
+      // last piece of a block with tail zeros loads the block's last 16 bytes (shifted below)
+      // (offsets by masks, not selects: selects let the compiler sink each load into branches)
+      auto issue = [&](const rsrc_t& R, uint32_t rel) {
+        const uint32_t m15 = tailp && L >= 16 ? ~0u : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) {
+          const uint32_t po = (c << 12) + 256 * j + 16 * lq, x = po - P;
+          const uint32_t in = live && po >= P && x + 16 <= L ? ~0u : 0u;
+          uint32_t off = kCsOob ^ ((kCsOob ^ (rel + x)) & in);
+          if (j == 15) off ^= (off ^ (rel + L - 16)) & m15;
+          q[j] = __builtin_amdgcn_raw_buffer_load_b128(R, off, 0, 0);
+        }
+      };
+      if (wave_ok) {
+        const rsrc_t R = make_rsrc_exact(const_cast<uint8_t*>(a.blocks + S0), uint32_t(Se - S0));
+        issue(R, uint32_t(s - S0));
+      } else {  // (non-adjacent or huge ranges: one descriptor per block, its row's lanes only)
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint64_t sk = lane64(s, 16 * k);
+          const uint32_t Lk = uint32_t(__builtin_amdgcn_readlane(L, 16 * k));
+          const rsrc_t R = make_rsrc_exact(const_cast<uint8_t*>(a.blocks + sk), Lk);
+          if (g == k) issue(R, 0);
+        }
+      }
+      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 16; ++j) {
+        if (j == 15) {  // (here, not before the loop: the fold of pieces 0..14 waits only for them)
+          if (tailp) {
+            uint32_t v[4] = {q[15].x, q[15].y, q[15].z, q[15].w};
+            if (L < 16) {  // the whole block is the last piece: its L bytes, then zeros
+              const rsrc_t R = make_rsrc_exact(const_cast<uint8_t*>(a.blocks + s), L);
+              v[0] = v[1] = v[2] = v[3] = 0;
+              for (uint32_t i = 0; i < L; ++i) v[i >> 2] |= uint32_t(__builtin_amdgcn_raw_buffer_load_b8(R, i, 0, 0)) << (8 * (i & 3));
+            } else {  // the block's last 16 bytes, down by T
+              for (uint32_t r = 0; r < 3; ++r)
+                if ((T >> 2) > r) v[0] = v[1], v[1] = v[2], v[2] = v[3], v[3] = 0;
+              const uint32_t sb = T & 3;
+              v[0] = __builtin_amdgcn_alignbyte(v[1], v[0], sb);
+              v[1] = __builtin_amdgcn_alignbyte(v[2], v[1], sb);
+              v[2] = __builtin_amdgcn_alignbyte(v[3], v[2], sb);
+              v[3] = __builtin_amdgcn_alignbyte(0u, v[3], sb);
+            }
+            q[15] = u32x4{v[0], v[1], v[2], v[3]};
+          }
+        }
+        c0 = step(c0 ^ q[j].x);
+        c1 = step(c1 ^ q[j].y);
+        c2 = step(c2 ^ q[j].z);
+        c3 = step(c3 ^ q[j].w);
+      }
+      // chain i of row lane r ends 16 r + 4 i bytes past the chunk end
+      uint32_t x = crc_apply(S.unz4, c3) ^ c2;
+      x = crc_apply(S.unz4, x) ^ c1;
+      x = crc_apply(S.unz4, x) ^ c0;
+      x ^= crc_apply(S.unzl[0], LSM_DPP(x, 0x101, 0xF));  // row_shl:1
+      x ^= crc_apply(S.unzl[1], LSM_DPP(x, 0x102, 0xF));  // row_shl:2
+      x ^= crc_apply(S.unzl[2], LSM_DPP(x, 0x104, 0xF));  // row_shl:4
+      x ^= crc_apply(S.unzl[3], LSM_DPP(x, 0x108, 0xF));  // row_shl:8
+      if (live) acc = c == 0 ? acc ^ x : crc_apply(S.z4096, acc) ^ x;  // (row lane 0's x is the chunk's)
+    }
+    if (have && lq == 0) {
+      const uint32_t r = crc_apply(S.unzt[T], acc);
+      a.crc[b0 + g] = L ? ~r : 0u;
+    }
+  }
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
+  raise_err(a.stats, err);
+}
+
 }  // namespace lsmblk_impl
 
 // ---------------------------------------------------------------- SST BlockMeta section
@@ -3123,11 +3281,18 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   a.bagg = a.bbase = a.tagg = a.tinc = a.dbg = nullptr;
   a.lag = a.lag_bytes = 0;
   a.tag = a.poll = 0;
-  if (!(flags & LSMBLK_DECODE_VERIFY_CRC) && !c->dec_two_pass) {
-    // lagged decode: E is read from HBM once, one launch (decode_lag_kernel).  (The CRC-verifying
-    // read keeps the two-pass decode: the lagged decode with the CRC pass beside it on a second
-    // stream took 5.07 ms against 4.00 -- the persistent CRC grid and the lagged decode's
-    // dispatch-order schedule get in each other's way.)
+  if (!c->dec_two_pass) {
+    // lagged decode: E is read from HBM once, one launch (decode_lag_kernel).  The CRC-verifying
+    // read runs the streaming CRC pass and the checksum test first, on the same stream (round 4:
+    // the two-pass decode with the count folded into the old CRC pass, 4.0 ms at U; the lagged
+    // decode beside that CRC pass on a second stream, 5.07 ms -- the persistent CRC grid and the
+    // lagged decode's dispatch-order schedule got in each other's way).
+    if (flags & LSMBLK_DECODE_VERIFY_CRC) {
+      if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st)))
+        return rc;
+      LSM_LAUNCH(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
+                 c->vcrc, c->meta_cstats, stats);
+    }
     if ((rc = next_epoch(c, st))) return rc;
     a.bagg = c->lag_gran;
     a.bbase = a.bagg + 3 * c->lag_blk_cap;
@@ -3146,8 +3311,8 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
   }
   if (flags & LSMBLK_DECODE_VERIFY_CRC) {
-    // one pass over E: the CRC of every block and its (entries, key bytes, value bytes), in
-    // place of the count pass's second read of E
+    // (two-pass A/B) one pass over E: the CRC of every block and its (entries, key bytes, value
+    // bytes), in place of the count pass's second read of E
     if ((rc = lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, c->vcrc, c->meta_cstats, st, c->dec_agg)))
       return rc;
     LSM_LAUNCH(crc_verify_kernel, dim3(uint32_t((nblk + 255) / 256)), dim3(256), 0, st, blocks, blk_off, nblk,
@@ -3375,7 +3540,8 @@ int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_
   if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
   // section CRC over [meta_off[s] + 4, meta_off[s+1] - 4): blocks = meta + 4, tail = 8
   if (hipMemsetAsync(c->meta_cstats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  if ((rc = lsmblk_impl::launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st))) return rc;
+  if ((rc = lsmblk_impl::launch_crc(c, meta + 4, meta_off, nseg, 8, c->meta_crc, c->meta_cstats, st, nullptr, true)))
+    return rc;
   LSM_LAUNCH(meta_crc_put_kernel, dim3(sg), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
@@ -3433,17 +3599,21 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
 namespace lsmblk_impl {
 int ensure_crc_tabs(lsmblk_ctx* c) {
   if (c->crc_tabs) return LSMBLK_OK;
-  CrcTabs h;
-  crc_host_tables(h);
-  if (hipMalloc(reinterpret_cast<void**>(&c->crc_tabs), sizeof(CrcTabs)) != hipSuccess) {
+  static CrcAllTabs h;  // (built once per process: the stream tables take ~40 M bit steps)
+  static std::once_flag once;
+  std::call_once(once, [] {
+    crc_host_tables(h.t);
+    crc_stream_host_tables(h.s);
+  });
+  if (hipMalloc(reinterpret_cast<void**>(&c->crc_tabs), sizeof(CrcAllTabs)) != hipSuccess) {
     c->crc_tabs = nullptr;
     return LSMBLK_E_NOMEM;
   }
-  return hipMemcpy(c->crc_tabs, &h, sizeof(CrcTabs), hipMemcpyHostToDevice) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  return hipMemcpy(c->crc_tabs, &h, sizeof(CrcAllTabs), hipMemcpyHostToDevice) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
-               uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg) {
+               uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg, bool sections) {
   CrcArgs a;
   a.agg = agg;
   a.blocks = blocks;
@@ -3453,9 +3623,25 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
   a.crc = crc;
   a.tabs = static_cast<const CrcTabs*>(c->crc_tabs);
   a.stats = stats;
-  // persistent: as many workgroups as are resident at once (4 KiB tables + 4 x 4 KiB staging)
   int cus = 256, per_cu = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+#ifndef LSMBLK_XCRC_OLD
+  if (!agg && !sections) {  // the plain pass: one 16-wave workgroup per CU (the replicated tables fill the LDS)
+    CrcStreamArgs b;
+    b.blocks = blocks;
+    b.blk_off = blk_off;
+    b.nblk = nblk;
+    b.tail = tail;
+    b.crc = crc;
+    b.tabs = &static_cast<const CrcAllTabs*>(c->crc_tabs)->s;
+    b.stats = stats;
+    const uint64_t want = (nblk + 4 * kCsWaves - 1) / (4 * kCsWaves);
+    const uint32_t grid = uint32_t(want < uint64_t(cus) ? (want ? want : 1) : uint64_t(cus));
+    LSM_LAUNCH(crc_stream_kernel, dim3(grid), dim3(64 * kCsWaves), 0, st, b);
+    return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  }
+#endif
+  // persistent: as many workgroups as are resident at once (4 KiB tables + 4 x 4 KiB staging)
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, agg ? crc_kernel<true> : crc_kernel<false>, 256, 0) !=
           hipSuccess ||
       per_cu < 1)
