@@ -442,6 +442,23 @@ __device__ __forceinline__ void copy_run(const rsrc_t& RS, uint32_t so, uint32_t
   }
 }
 
+// copy_run one 16-B piece at a time (few registers: for copies inside another loop's live range)
+__device__ __forceinline__ void copy_run1(const rsrc_t& RS, uint32_t so, uint32_t lim, const rsrc_t& RD, uint32_t dof,
+                                          uint32_t len) {
+  if (len < 16) {
+    copy_run(RS, so, lim, RD, dof, len);
+    return;
+  }
+  const uint32_t last = len - 16;
+  for (uint32_t o = 0;; o += 16) {
+    const uint32_t x = min(o, last);
+    const u32x4 q = gload16(RS, so + x);
+    const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+    st16(RD, dof + x, v);
+    if (x == last) break;
+  }
+}
+
 // The same copy by the whole wave (len >= 16, wave-uniform arguments): lane j moves pieces
 // j, j + 64, ... so a wave instruction moves 1 KiB of contiguous bytes.  Values of
 // kCoop bytes or more go this way: one long value no longer keeps 63 lanes idle.
@@ -535,14 +552,24 @@ __device__ __forceinline__ void copy_store(const rsrc_t& RD, const CopyBatch<B>&
     }
 }
 
+// after(lo, hi), if given, runs after each round's stores with the round's piece range [lo, hi)
+// (hi = ~0u on the last round; once with [0, ~0u) when no lane has a run): lanes whose first
+// piece number falls in it can store the bytes next to those pieces while their lines are hot.
+struct NoAfter {
+  __device__ void operator()(uint32_t, uint32_t, uint32_t) const {}
+};
+template <class After = NoAfter>
 __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, uint32_t so, const rsrc_t& RD,
-                                               uint32_t dof, uint32_t len, uint32_t* sc) {
+                                               uint32_t dof, uint32_t len, uint32_t* sc, const After& after = After()) {
   const uint32_t l = lane_id();
   const uint32_t np = longrun ? (len + 15) >> 4 : 0u;
   const uint32_t incl = wave_incl_scan32(np);
   const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-  if (total == 0) return;
   const uint32_t first = incl - np;  // this lane's first piece number
+  if (total == 0) {
+    after(first, 0u, ~0u);
+    return;
+  }
   wave_sync();                       // the scratch's previous readers are done
   reinterpret_cast<u32x4*>(sc)[l] = u32x4{so, dof, len - 16, first};  // read only for lanes with a run
   uint32_t carry = 0;  // owner + 1 of the previous row's last piece
@@ -550,6 +577,7 @@ __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, u
     CopyBatch<kBigB> c;
     copy_issue(RS, g0, total, np, first, sc, carry, c);
     copy_store(RD, c);
+    after(first, g0, g0 + 64 * kBigB >= total ? ~0u : g0 + 64 * kBigB);
   }
 }
 
@@ -1774,24 +1802,34 @@ __device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, 
     const uint64_t pos = dc + incl - dg;
     dc += __shfl(incl, 63, 64);
     uint32_t vdst = 0;
+    const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
+    uint64_t tsv = 0;
     if (k < n) {
-      const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
       vdst = at + 14 + sfx;
-      if (!(diag_mask(a.skip) & 16)) {
-      // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value
-      __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
-      copy_run(RK, kp + p, klim, RO, at + 4, sfx);
-      const uint64_t tsv = a.ts[s + k];
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bswap32(uint32_t(tsv >> 32)), __builtin_bswap32(uint32_t(tsv))},
-                                            RO, at + 4 + sfx, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(vl & 0xFFFF)), RO, at + 12 + sfx, 0, 0);
-      if (vl < kCoop) copy_run(RV, vp, vlim, RO, vdst, vl);
-      // builder.rs:71: offsets.push(data.len() as u16), BE
-      __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO,
-                                            ob + uint32_t(data_len) + 2 * k, 0, 0);
-      }
+      tsv = a.ts[s + k];
+      // builder.rs:71: offsets.push(data.len() as u16), BE (the table's stores are contiguous)
+      if (!(diag_mask(a.skip) & 16))
+        __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO,
+                                              ob + uint32_t(data_len) + 2 * k, 0, 0);
     }
-    if (!(diag_mask(a.skip) & 32)) copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc);
+    // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value.
+    // A record's fields (and a short value) are stored right after the copy round that stores the
+    // first piece of its long value (or the next long value), so the partial lines they share with
+    // the value pieces around them are written close together in time: written up front, the
+    // fields' lines were evicted from L2 half-written before the pieces came (M: WRITE_SIZE 1.165x
+    // the encoded bytes).
+    auto fields = [&](uint32_t first, uint32_t lo, uint32_t hi) {
+      if (k < n && first >= lo && first < hi && !(diag_mask(a.skip) & 16)) {
+        __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
+        copy_run1(RK, kp + p, klim, RO, at + 4, sfx);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bswap32(uint32_t(tsv >> 32)), __builtin_bswap32(uint32_t(tsv))},
+                                              RO, at + 4 + sfx, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(vl & 0xFFFF)), RO, at + 12 + sfx, 0, 0);
+        if (vl < kCoop) copy_run1(RV, vp, vlim, RO, vdst, vl);
+      }
+    };
+    if (!(diag_mask(a.skip) & 32)) copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc, fields);
+    else fields(0u, 0u, ~0u);
   }
   if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
   if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
@@ -3439,7 +3477,11 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
     per_cu = 3;
   const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
   LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), 0, st, e);
-  LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * 5), dim3(256), 0, st, e);
+  // (every workgroup resident at once: the flagged blocks are strided over the whole grid)
+  int big_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&big_cu, emit_big_kernel, 256, 0) != hipSuccess || big_cu < 1)
+    big_cu = 4;
+  LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * uint32_t(big_cu)), dim3(256), 0, st, e);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
