@@ -558,7 +558,7 @@ __device__ __forceinline__ void copy_store(const rsrc_t& RD, const CopyBatch<B>&
 struct NoAfter {
   __device__ void operator()(uint32_t, uint32_t, uint32_t) const {}
 };
-template <class After = NoAfter>
+template <uint32_t B = kBigB, class After = NoAfter>
 __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, uint32_t so, const rsrc_t& RD,
                                                uint32_t dof, uint32_t len, uint32_t* sc, const After& after = After()) {
   const uint32_t l = lane_id();
@@ -573,11 +573,11 @@ __device__ __forceinline__ void copy_long_runs(bool longrun, const rsrc_t& RS, u
   wave_sync();                       // the scratch's previous readers are done
   reinterpret_cast<u32x4*>(sc)[l] = u32x4{so, dof, len - 16, first};  // read only for lanes with a run
   uint32_t carry = 0;  // owner + 1 of the previous row's last piece
-  for (uint32_t g0 = 0; g0 < total; g0 += 64 * kBigB) {
-    CopyBatch<kBigB> c;
+  for (uint32_t g0 = 0; g0 < total; g0 += 64 * B) {
+    CopyBatch<B> c;
     copy_issue(RS, g0, total, np, first, sc, carry, c);
     copy_store(RD, c);
-    after(first, g0, g0 + 64 * kBigB >= total ? ~0u : g0 + 64 * kBigB);
+    after(first, g0, g0 + 64 * B >= total ? ~0u : g0 + 64 * B);
   }
 }
 
@@ -623,6 +623,11 @@ __device__ __forceinline__ void dec_big_entry(const DecodeArgs& a, const DecTabl
   }
 }
 
+#ifndef LSMBLK_XDBB
+#define LSMBLK_XDBB 8
+#endif
+constexpr uint32_t kDecBigB = LSMBLK_XDBB;  // (experiment) pieces per lane per copy round, large-block decode
+
 // Outputs of the n entries whose tables are in L (block entries Eb - E0 .. + n), large block.
 __device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const rsrc_t& R, uint32_t lead,
                                 const BlockHdr& h, uint32_t n, uint64_t Eb, uint64_t K0, uint64_t V0, uint32_t K,
@@ -643,7 +648,7 @@ __device__ void dec_big_outputs(const DecodeArgs& a, const DecTables& L, const r
       vl = L.vout[k + 1] - L.vout[k];
       if (vl < kCoop) copy_run(R, vsrc, lim, RV, vdst, vl);
     }
-    copy_long_runs(live && vl >= kCoop, R, vsrc, RV, vdst, vl, sc);
+    copy_long_runs<kDecBigB>(live && vl >= kCoop, R, vsrc, RV, vdst, vl, sc);
   }
 }
 
@@ -1749,91 +1754,33 @@ __device__ __forceinline__ void lds_st_short(uint8_t* p, uint32_t len, const uin
   }
 }
 
+#ifndef LSMBLK_XEBB
+#define LSMBLK_XEBB 4
+#endif
+constexpr uint32_t kEmitBigB = LSMBLK_XEBB;  // (experiment) pieces per lane per copy round in emit_big
+
 // Blocks beyond the LDS image (config M's 64 KiB blocks, oversize entries, > kEmitMaxE
-// entries): one pass, entry lanes write their records straight to HBM.  LCP against the
-// first key in 16-B compares; suffix and value as 16-B unaligned buffer loads/stores with
-// batched loads (copy_run); header, ts and value_len as single unaligned stores; the offset
-// slot at data_len + 2k, data_len = size - 2n - 2 known from the plan (checked at the end).
-__device__ void emit_big(const EmitArgs& a, uint32_t s, uint32_t n, uint64_t O, uint64_t size, uint32_t& err,
-                         uint32_t* sc) {
-  const uint32_t l = lane_id();
-  const uint32_t kg = uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15), vg = uint32_t(reinterpret_cast<uintptr_t>(a.vals) & 15);
-  const uint32_t klim = kg + uni(a.key_off[a.n]), vlim = vg + uni(a.val_off[a.n]);  // valid descriptor bytes
-  const rsrc_t RK = make_rsrc(a.keys - kg, klim), RV = make_rsrc(a.vals - vg, vlim);
-  const uint32_t ob = uint32_t(O & 15);
-  const uint64_t room = O < a.out_cap ? a.out_cap - O : 0;  // never store past out_cap
-  const rsrc_t RO = make_rsrc_exact(a.out + (O - ob), ob + uint32_t(size < room ? size : room));
-  const uint32_t fp = kg + uni(a.key_off[s]), fl = uni(a.key_off[s + 1]) - (fp - kg);
-  const uint64_t data_len = size - 2ull * n - 2;
-  uint64_t dc = 0;
-  for (uint32_t c = 0; c < n; c += 64) {
-    const uint32_t k = c + l;
-    uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
-    if (k < n) {
-      kp = kg + a.key_off[s + k];
-      kl = a.key_off[s + k + 1] - (kp - kg);
-      vp = vg + a.val_off[s + k];
-      vl = a.val_off[s + k + 1] - (vp - vg);
-      if (k != 0 && !(diag_mask(a.skip) & 128)) {  // builder.rs:62 common_prefix(first_key, key)
-        const uint32_t m = fl < kl ? fl : kl;
-        p = m;
-        for (uint32_t q = 0; q < m; q += 16) {
-          uint32_t z = 16;  // first differing byte in [q, q + 16)
-          if (fp + q + 16 <= klim && kp + q + 16 <= klim) {
-            const u32x4 x = gload16(RK, fp + q), y = gload16(RK, kp + q);
-            const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
-            for (uint32_t i = 0; i < 4 && z == 16; ++i)
-              if (d[i]) z = 4 * i + (__builtin_ctz(d[i]) >> 3);
-          } else {
-            for (uint32_t i = 0; i < 16 && z == 16 && q + i < m; ++i)
-              if (__builtin_amdgcn_raw_buffer_load_b8(RK, fp + q + i, 0, 0) !=
-                  __builtin_amdgcn_raw_buffer_load_b8(RK, kp + q + i, 0, 0))
-                z = i;
-          }
-          if (z < 16) {
-            p = min(q + z, m);
-            break;
-          }
-        }
-      }
-    }
-    const uint64_t dg = k < n ? uint64_t(kl) + vl + 14 - p : 0;
-    const uint64_t incl = wave_incl_scan<uint64_t>(dg);
-    const uint64_t pos = dc + incl - dg;
-    dc += __shfl(incl, 63, 64);
-    uint32_t vdst = 0;
-    const uint32_t sfx = kl - p, at = ob + uint32_t(pos);
-    uint64_t tsv = 0;
-    if (k < n) {
-      vdst = at + 14 + sfx;
-      tsv = a.ts[s + k];
-      // builder.rs:71: offsets.push(data.len() as u16), BE (the table's stores are contiguous)
-      if (!(diag_mask(a.skip) & 16))
-        __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO,
-                                              ob + uint32_t(data_len) + 2 * k, 0, 0);
-    }
-    // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value.
-    // A record's fields (and a short value) are stored right after the copy round that stores the
-    // first piece of its long value (or the next long value), so the partial lines they share with
-    // the value pieces around them are written close together in time: written up front, the
-    // fields' lines were evicted from L2 half-written before the pieces came (M: WRITE_SIZE 1.165x
-    // the encoded bytes).
-    auto fields = [&](uint32_t first, uint32_t lo, uint32_t hi) {
-      if (k < n && first >= lo && first < hi && !(diag_mask(a.skip) & 16)) {
-        __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
-        copy_run1(RK, kp + p, klim, RO, at + 4, sfx);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bswap32(uint32_t(tsv >> 32)), __builtin_bswap32(uint32_t(tsv))},
-                                              RO, at + 4 + sfx, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(vl & 0xFFFF)), RO, at + 12 + sfx, 0, 0);
-        if (vl < kCoop) copy_run1(RV, vp, vlim, RO, vdst, vl);
-      }
-    };
-    if (!(diag_mask(a.skip) & 32)) copy_long_runs(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc, fields);
-    else fields(0u, 0u, ~0u);
-  }
-  if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
-  if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(size) - 2, 0, 0);
-}
+// entries), one wave per block, 64 entries (a chunk) at a time: entry lanes write their records
+// straight to HBM.  LCP against the first key in 16-B compares; suffix and value as 16-B
+// unaligned buffer loads/stores (long values by the wave's packed copy); header, ts and
+// value_len as single unaligned stores; the offset slot at data_len + 2k, data_len = size - 2n - 2
+// known from the plan (checked at the end).
+//
+// The chunks of a wave's blocks are software-pipelined (emit_big_kernel): a chunk's entry offsets
+// (level 1) are loaded while the chunk before it is processed, and its first 16 key bytes and the
+// block's first key (level 2, the LCP's operands) right after that chunk's first copy round --
+// without it each chunk waited two round trips before its copies (M: 0.40 of 1.93 ms with the
+// copies ablated, none of it overlapped).
+struct BigBlk {
+  uint64_t bi, O, size;
+  uint32_t s, n;
+};
+struct BigL1 {  // lane k: key_off[s + k], key_off[s + k + 1], val_off[s + k], val_off[s + k + 1]
+  uint32_t ko0, ko1, vo0, vo1;
+};
+struct BigL2 {  // lane k: its key's first 16 bytes; the block's first key's first 16 bytes
+  u32x4 own, first;
+};
 
 // Block metadata of one emit unit: two levels of dependent loads (block tables, then the
 // entry offsets of its first/last entry).
@@ -2148,18 +2095,168 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   const uint64_t nw = uint64_t(gridDim.x) * 4;
   const uint32_t l = lane_id();
   __shared__ alignas(16) uint32_t scratch[4][kCopyScratch];
+  uint32_t* const sc = scratch[wave_id()];
   uint32_t err = 0;
-  for (uint64_t base = blockIdx.x * 4 + wave_id(); base < lim; base += nw * 64) {
-    const uint64_t mine = base + nw * l;
-    uint64_t big = __ballot(mine < lim && a.big_flag[mine]);
-    while (big) {
-      const uint32_t i = uint32_t(__builtin_ctzll(big));
-      big &= big - 1;
-      const uint64_t bi = base + nw * i;
-      const uint32_t s = uni(a.blk_first[bi]), e = uni(a.blk_first[bi + 1]);
-      const uint64_t O = uni64(a.blk_off[bi]), size = uni64(a.blk_off[bi + 1]) - O;
-      emit_big(a, s, e - s, O, size, err, scratch[wave_id()]);
+  const uint32_t kg = uint32_t(reinterpret_cast<uintptr_t>(a.keys) & 15), vg = uint32_t(reinterpret_cast<uintptr_t>(a.vals) & 15);
+  const uint32_t klim = kg + uni(a.key_off[a.n]), vlim = vg + uni(a.val_off[a.n]);  // valid descriptor bytes
+  const rsrc_t RK = make_rsrc(a.keys - kg, klim), RV = make_rsrc(a.vals - vg, vlim);
+  // this wave's flagged blocks, in order
+  uint64_t wbase = uint64_t(blockIdx.x) * 4 + wave_id(), cbase = 0, bits = 0;
+  auto next_block = [&](BigBlk& B) -> bool {
+    while (bits == 0) {
+      if (wbase >= lim) return false;
+      const uint64_t mine = wbase + nw * l;
+      bits = __ballot(mine < lim && a.big_flag[mine]);
+      cbase = wbase;
+      wbase += nw * 64;
     }
+    const uint32_t i = uint32_t(__builtin_ctzll(bits));
+    bits &= bits - 1;
+    B.bi = cbase + nw * i;
+    B.s = uni(a.blk_first[B.bi]);
+    B.n = uni(a.blk_first[B.bi + 1]) - B.s;
+    B.O = uni64(a.blk_off[B.bi]);
+    B.size = uni64(a.blk_off[B.bi + 1]) - B.O;
+    return true;
+  };
+  auto issue_l1 = [&](const BigBlk& B, uint32_t c) -> BigL1 {
+    BigL1 x{0u, 0u, 0u, 0u};
+    const uint32_t k = c + l;
+    if (k < B.n) {
+      x.ko0 = a.key_off[B.s + k];
+      x.ko1 = a.key_off[B.s + k + 1];
+      x.vo0 = a.val_off[B.s + k];
+      x.vo1 = a.val_off[B.s + k + 1];
+    }
+    return x;
+  };
+  // fp: descriptor byte of the block's first key (a 16-B load only where it stays in the keys)
+  auto issue_l2 = [&](const BigL1& x, uint32_t fp) -> BigL2 {
+    BigL2 y{u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+    const uint32_t kp = kg + x.ko0;
+    if (kp + 16 <= klim) y.own = gload16(RK, kp);
+    if (fp + 16 <= klim) y.first = gload16(RK, fp);
+    return y;
+  };
+  BigBlk B;
+  if (!next_block(B)) {
+    raise_err(a.stats, err);
+    return;
+  }
+  BigL1 x = issue_l1(B, 0);
+  uint32_t fp = kg + uint32_t(__builtin_amdgcn_readlane(x.ko0, 0));        // key_off[s]
+  uint32_t fl = uint32_t(__builtin_amdgcn_readlane(x.ko1, 0)) - (fp - kg);  // its length
+  BigL2 y = issue_l2(x, fp);
+  uint32_t c = 0;
+  uint64_t dc = 0;
+  for (;;) {
+    // the next chunk: its entry offsets in flight during this one
+    BigBlk NB = B;
+    uint32_t nc = c + 64;
+    bool more = true;
+    if (nc >= B.n) {
+      more = next_block(NB);
+      nc = 0;
+    }
+    BigL1 nx{0u, 0u, 0u, 0u};
+    if (more) nx = issue_l1(NB, nc);
+    BigL2 ny{u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+    uint32_t nfp = fp, nfl = fl;
+    bool ny_done = !more;
+    auto issue_next_l2 = [&]() {
+      if (ny_done) return;
+      if (nc == 0) {
+        nfp = kg + uint32_t(__builtin_amdgcn_readlane(nx.ko0, 0));
+        nfl = uint32_t(__builtin_amdgcn_readlane(nx.ko1, 0)) - (nfp - kg);
+      }
+      ny = issue_l2(nx, nfp);
+      ny_done = true;
+    };
+    // this chunk
+    const uint32_t s = B.s, n = B.n, k = c + l;
+    const uint32_t ob = uint32_t(B.O & 15);
+    const uint64_t room = B.O < a.out_cap ? a.out_cap - B.O : 0;  // never store past out_cap
+    const rsrc_t RO = make_rsrc_exact(a.out + (B.O - ob), ob + uint32_t(B.size < room ? B.size : room));
+    const uint64_t data_len = B.size - 2ull * n - 2;
+    uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
+    uint64_t tsv = 0;
+    if (k < n) {
+      tsv = a.ts[s + k];  // (used after the copy rounds)
+      kp = kg + x.ko0;
+      kl = x.ko1 - x.ko0;
+      vp = vg + x.vo0;
+      vl = x.vo1 - x.vo0;
+      if (k != 0 && !(diag_mask(a.skip) & 128)) {  // builder.rs:62 common_prefix(first_key, key)
+        const uint32_t m = fl < kl ? fl : kl;
+        p = m;
+        uint32_t q = 0;
+        if (fp + 16 <= klim && kp + 16 <= klim) {  // the first 16 bytes from the prefetch
+          const uint32_t d[4] = {y.first.x ^ y.own.x, y.first.y ^ y.own.y, y.first.z ^ y.own.z, y.first.w ^ y.own.w};
+          uint32_t z = 16;
+          for (uint32_t i = 0; i < 4 && z == 16; ++i)
+            if (d[i]) z = 4 * i + (__builtin_ctz(d[i]) >> 3);
+          q = z < 16 || m <= 16 ? m : 16u;
+          if (z < 16) p = min(z, m);
+        }
+        for (; q < m; q += 16) {
+          uint32_t z = 16;  // first differing byte in [q, q + 16)
+          if (fp + q + 16 <= klim && kp + q + 16 <= klim) {
+            const u32x4 xa = gload16(RK, fp + q), ya = gload16(RK, kp + q);
+            const uint32_t d[4] = {xa.x ^ ya.x, xa.y ^ ya.y, xa.z ^ ya.z, xa.w ^ ya.w};
+            for (uint32_t i = 0; i < 4 && z == 16; ++i)
+              if (d[i]) z = 4 * i + (__builtin_ctz(d[i]) >> 3);
+          } else {
+            for (uint32_t i = 0; i < 16 && z == 16 && q + i < m; ++i)
+              if (__builtin_amdgcn_raw_buffer_load_b8(RK, fp + q + i, 0, 0) !=
+                  __builtin_amdgcn_raw_buffer_load_b8(RK, kp + q + i, 0, 0))
+                z = i;
+          }
+          if (z < 16) {
+            p = min(q + z, m);
+            break;
+          }
+        }
+      }
+    }
+    const uint64_t dg = k < n ? uint64_t(kl) + vl + 14 - p : 0;
+    const uint64_t incl = wave_incl_scan<uint64_t>(dg);
+    const uint64_t pos = dc + incl - dg;
+    dc += __shfl(incl, 63, 64);
+    const uint32_t sfx = kl - p, at = ob + uint32_t(pos), vdst = at + 14 + sfx;
+    // builder.rs:71: offsets.push(data.len() as u16), BE (the table's stores are contiguous)
+    if (k < n && !(diag_mask(a.skip) & 16))
+      __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(uint32_t(pos) & 0xFFFF)), RO, ob + uint32_t(data_len) + 2 * k, 0, 0);
+    // builder.rs:63-70: BE u16 prefix, BE u16 suffix len, suffix, BE u64 ts, BE u16 value len, value.
+    // A record's fields (and a short value) are stored right after the copy round that stores the
+    // first piece of its long value (or the next long value), so the partial lines they share with
+    // the value pieces around them are written close together in time: written up front, the
+    // fields' lines were evicted from L2 half-written before the pieces came (M: WRITE_SIZE 1.165x
+    // the encoded bytes).  The next chunk's level-2 loads go out after the first round.
+    auto fields = [&](uint32_t first, uint32_t lo, uint32_t hi) {
+      if (k < n && first >= lo && first < hi && !(diag_mask(a.skip) & 16)) {
+        __builtin_amdgcn_raw_buffer_store_b32(bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16), RO, at, 0, 0);
+        copy_run1(RK, kp + p, klim, RO, at + 4, sfx);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bswap32(uint32_t(tsv >> 32)), __builtin_bswap32(uint32_t(tsv))},
+                                              RO, at + 4 + sfx, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(vl & 0xFFFF)), RO, at + 12 + sfx, 0, 0);
+        if (vl < kCoop) copy_run1(RV, vp, vlim, RO, vdst, vl);
+      }
+      issue_next_l2();
+    };
+    if (!(diag_mask(a.skip) & 32)) copy_long_runs<kEmitBigB>(k < n && vl >= kCoop, RV, vp, RO, vdst, vl, sc, fields);
+    else fields(0u, 0u, ~0u);
+    if (c + 64 >= n) {  // the block's last chunk
+      if (dc != data_len) err |= LSMBLK_ERR_INTERNAL;
+      if (l == 0) __builtin_amdgcn_raw_buffer_store_b16(uint16_t(bswap16(n & 0xFFFF)), RO, ob + uint32_t(B.size) - 2, 0, 0);
+      dc = 0;
+    }
+    if (!more) break;
+    B = NB;
+    c = nc;
+    x = nx;
+    y = ny;
+    fp = nfp;
+    fl = nfl;
   }
   raise_err(a.stats, err);
 }
