@@ -8,6 +8,7 @@
 //   pwpf   persistent waves, block stride NW, next block's loads issued before this block's stores
 //   slab   persistent waves, each a contiguous slab of blocks
 //   blkk K one single-wave workgroup per K consecutive blocks, one block ahead prefetched
+//   pwx    persistent waves, consecutive blocks on consecutive workgroups (XCDs)
 // build: hipcc --offload-arch=gfx950 -O3 tools/copy_probe3.hip -o tools/copy_probe3
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -64,6 +65,31 @@ __global__ __launch_bounds__(256) void slab(const u32x4* __restrict__ a, u32x4* 
     u32x4 v[4];
     for (int j = 0; j < 4; ++j) v[j] = a[blk * kB + lane() + 64 * j];
     for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(v[j], b + blk * kB + lane() + 64 * j);
+  }
+}
+
+// persistent, consecutive blocks on consecutive workgroups (so on consecutive XCDs, as in
+// dispatch order): wave wv of workgroup g takes blocks g + G wv + k NW
+template <bool PF>
+__global__ __launch_bounds__(256) void pwx(const u32x4* __restrict__ a, u32x4* __restrict__ b, uint64_t nblk) {
+  const uint64_t G = gridDim.x, nw = G * 4;
+  uint64_t blk = uint64_t(blockIdx.x) + G * (threadIdx.x >> 6);
+  if (blk >= nblk) return;
+  u32x4 v[4];
+  for (int j = 0; j < 4; ++j) v[j] = a[blk * kB + lane() + 64 * j];
+  for (;;) {
+    const uint64_t nx = blk + nw;
+    u32x4 w[4];
+    if (PF && nx < nblk)
+      for (int j = 0; j < 4; ++j) w[j] = a[nx * kB + lane() + 64 * j];
+    for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(v[j], b + blk * kB + lane() + 64 * j);
+    if (nx >= nblk) break;
+    if (PF) {
+      for (int j = 0; j < 4; ++j) v[j] = w[j];
+    } else {
+      for (int j = 0; j < 4; ++j) v[j] = a[nx * kB + lane() + 64 * j];
+    }
+    blk = nx;
   }
 }
 
@@ -124,6 +150,8 @@ int main() {
       snprintf(nm, 64, "pw   WG/CU %d", wg);   rep(nm, timeit(pw<false>, dim3(cus * wg), dim3(256), a, b, nblk));
       snprintf(nm, 64, "pwpf WG/CU %d", wg);   rep(nm, timeit(pw<true>, dim3(cus * wg), dim3(256), a, b, nblk));
       snprintf(nm, 64, "slab WG/CU %d", wg);   rep(nm, timeit(slab, dim3(cus * wg), dim3(256), a, b, nblk));
+      snprintf(nm, 64, "pwx  WG/CU %d", wg);   rep(nm, timeit(pwx<false>, dim3(cus * wg), dim3(256), a, b, nblk));
+      snprintf(nm, 64, "pwxpf WG/CU %d", wg);  rep(nm, timeit(pwx<true>, dim3(cus * wg), dim3(256), a, b, nblk));
     }
   }
   return 0;
