@@ -105,27 +105,30 @@ def test_tiny_and_empty_ranges():
     check_each_range_against_resumed_oracle(kept, res, bases, 4096, 16 << 10)
 
 
-def test_ranges_read_only_their_blocks_decode_merge_encode():
-    """The §8 e pipeline from SST blocks: each range decodes only the blocks of every run that
-    overlap it (straddling blocks read by both neighbours), merges its own keys, and the ranges
-    together give the single-stream compaction."""
-    rng = np.random.default_rng(5)
-    kv, rs = case(900, versions=2, nkeys=8000, nrun=4)
-    bs, target = 4096, 48 << 10
+def range_inputs(kv, rs, splitters, bs):
+    """Every run encoded as SST blocks; per key range, the KV input decoded from only the blocks of
+    each run that overlap the range (BlockMeta first / last keys; straddling blocks go to both
+    neighbours) and its run starts."""
     runs = []
     for r in range(len(rs) - 1):
         sub = O.gather(kv, np.arange(rs[r], rs[r + 1]))
+        if sub.n == 0:
+            runs.append(None)
+            continue
         seg = synth.segments_by_bytes(sub.key_off, sub.val_off, 64 << 10)
         blocks, off = batch.encode_kv(to_dev(sub), seg, bs)
         dec = batch.decode_blocks(blocks, off)
         keys, ko, _, _, _ = dec.to_numpy()
         runs.append((blocks, off.cpu().numpy().view(np.uint64), keys, ko))
-    splitters = pick_splitters(kv, rng, 3)
     inputs = []
     for g in range(len(splitters) + 1):
         lo, hi = shard.range_of(g, splitters)
         parts, rstarts = [], [0]
-        for blocks, off, keys, ko in runs:
+        for run in runs:
+            if run is None:
+                rstarts.append(rstarts[-1])
+                continue
+            blocks, off, keys, ko = run
             # block first / last keys from the decoded run (BlockMeta's first_key / last_key)
             dec = batch.decode_blocks(blocks, torch.from_numpy(off.view(np.int64)).cuda(), with_blk_ent=True)[1]
             ent = dec.cpu().numpy().view(np.uint64)
@@ -148,6 +151,18 @@ def test_ranges_read_only_their_blocks_decode_merge_encode():
         ts_all = np.concatenate([c[4] for c in cat]) if cat else np.zeros(0, np.uint64)
         inputs.append((batch.KVStream.from_numpy(k_all, ko_all, v_all, vo_all, ts_all),
                        np.array(rstarts, np.uint32)))
+    return inputs
+
+
+def test_ranges_read_only_their_blocks_decode_merge_encode():
+    """The §8 e pipeline from SST blocks: each range decodes only the blocks of every run that
+    overlap it (straddling blocks read by both neighbours), merges its own keys, and the ranges
+    together give the single-stream compaction."""
+    rng = np.random.default_rng(5)
+    kv, rs = case(900, versions=2, nkeys=8000, nrun=4)
+    bs, target = 4096, 48 << 10
+    splitters = pick_splitters(kv, rng, 3)
+    inputs = range_inputs(kv, rs, splitters, bs)
     wm = int(kv.ts.max()) // 3
     opts = batch.compact_opts(wm, True, block_size=bs, target_sst_size=target)
     res, _ = run_ranges(None, None, opts, splitters, inputs)
@@ -264,3 +279,29 @@ def test_two_level_sharded_small_vs_iterator():
     for sp in ([b"d"], [b"k", b"q"], [b"m\x00", b"r"], [b"q"]):
         res, _ = run_ranges(to_dev(kv), rs, opts, sp)
         assert b"".join(r["blocks"].cpu().numpy().tobytes() for r in res) == b"".join(blk for sst, _ in want for blk in sst)
+
+
+@pytest.mark.parametrize("seed,b_frac", [(0, 0.6), (1, 1.0), (2, 0.3)])
+def test_two_level_ranges_read_only_their_blocks(seed, b_frac):
+    """The two-level merge with every range decoding only the blocks of each run that overlap it
+    (ADVICE round 4): no range holds all of b, so b's last key -- where TwoMergeIterator's stream
+    ends -- reaches the ranges through compact_local's b-end exchange (the same message as
+    compact_dist's all-gather), and the ranges give the single-stream two-level compaction."""
+    rng = np.random.default_rng(930 + seed)
+    kv, rs = two_level_input(940 + seed, 6000, b_frac)
+    bs, target = 4096, 32 << 10
+    wm = int(kv.ts.max()) // 2
+    single = batch.compact_runs(to_dev(kv), rs, wm, True, block_size=bs, target_sst_size=target, merge_mode=TWO)
+    want_blocks = single["blocks"].cpu().numpy().tobytes()
+    want_starts = single["sst_start"].cpu().numpy().view(np.uint32).astype(np.int64)[:-1].tolist()
+    sp = pick_splitters(kv, rng, 4)
+    if rs[-1] > rs[-2]:
+        sp = sorted(set(sp) | {kv.entry(int(rs[-1]) - 1)[0]})  # a range starting exactly at b's last key
+    opts = batch.compact_opts(wm, True, block_size=bs, target_sst_size=target, merge_mode=TWO)
+    res, _ = run_ranges(None, None, opts, sp, range_inputs(kv, rs, sp, bs))
+    assert b"".join(r["blocks"].cpu().numpy().tobytes() for r in res) == want_blocks
+    bases = np.concatenate([[0], np.cumsum([r["m"] for r in res])]).tolist()
+    assert bases[-1] == single["stats"][5]
+    assert shard.sst_starts(res, bases) == want_starts
+    for a, b in zip(res, res[1:]):
+        assert a["carry_out"] == b["carry_in"]
