@@ -76,12 +76,18 @@ def parse(argv=None):
                    help="diagnostics: in --dry-run, this rank raises inside compact_dist (the N>1 extra's path)")
     p.add_argument("--dry-run-fail-rank", type=int, default=None,
                    help="launcher self-test: this rank exits with status 3 before joining the group")
+    p.add_argument("--encode-mode", default="packed", choices=["slots", "packed", "slots-unfused"],
+                   help="re-encode output: per-segment slots (LSMBLK_ENCODE_SEG_SLOTS, the plan walk fused "
+                        "with emit), all segments packed (lsmblk_encode_batch), or slots through the separate "
+                        "plan walk + emit launches (A/B)")
     p.add_argument("--decode-two-pass", action="store_true",
                    help="diagnostics (A/B): count + tile scan + decode (three launches) instead of the lagged decode")
     p.add_argument("--decode-lag", type=int, default=None,
                    help="diagnostics (A/B): blocks the lagged decode counts ahead of its decodes (default 10240)")
     p.add_argument("--ablate-lag", action="store_true", help="diagnostics: the lagged decode's ablation masks")
     p.add_argument("--trace-plan", action="store_true", help="diagnostics: the plan walk's per-segment trace")
+    p.add_argument("--trace-fused", action="store_true",
+                   help="diagnostics: the fused walk + emit launch's per-walker trace and emitter record waits")
     p.add_argument("--ablate-only", action="store_true", help="diagnostics: time only mask 0 and --ablate")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
@@ -205,16 +211,20 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     out_kv = batch.KVStream(batch._aligned_empty(K + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
                             batch._aligned_empty(V + 16, dev), torch.empty(n + 1, dtype=torch.int32, device=dev),
                             torch.empty(n, dtype=torch.int64, device=dev), n)
-    out_cap, blk_cap = E + 16, nblk + 2
+    slots = args.encode_mode != "packed"
+    # per-segment slots need the closed-form bound (include/lsmblk.h): keys + values + 18 B per entry
+    out_cap, blk_cap = (K + V + 18 * n + 16 if slots else E + 16), nblk + 2
     out_blocks = batch._aligned_empty(out_cap, dev)
     out_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
     seg_t = torch.from_numpy(seg.view(np.int32)).to(dev)
+    seg_out = torch.zeros(2 * (len(seg) - 1), dtype=torch.int64, device=dev) if slots else None
     st_dec = torch.zeros(4, dtype=torch.int64, device=dev)
     st_enc = torch.zeros(4, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     ctx = batch._ctx(local, stream)
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
     check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
+    check(lib().lsmblk_debug_set(ctx, 8, 1 if args.encode_mode == "slots-unfused" else 0))
     if args.decode_lag is not None:
         check(lib().lsmblk_debug_set(ctx, 4, args.decode_lag))
 
@@ -224,7 +234,8 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
         batch.decode_into(blocks, blk_off, nblk, out_kv, st_dec, n, K + 16, V + 16)
         if ev is not None:
             ev[1].record(stream)
-        batch.encode_into(out_kv, seg_t, len(seg) - 1, bs, out_blocks, out_cap, out_off, blk_cap, st_enc)
+        batch.encode_into(out_kv, seg_t, len(seg) - 1, bs, out_blocks, out_cap, out_off, blk_cap, st_enc,
+                          seg_out=seg_out)
         if ev is not None:
             ev[2].record(stream)
 
@@ -255,6 +266,32 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
         print(json.dumps({"plan_walk_us_by": {g: {int(v): [int((key == v).sum()), round(float(np.median(walk[key == v])), 1)]
                                                   for v in np.unique(key)} for g, key in groups.items()}}), flush=True)
         return None
+    if args.trace_fused and not extra:  # the fused walk + emit launch: per-walker trace, emitter waits
+        import ctypes
+        step()
+        torch.cuda.synchronize()
+        check(lib().lsmblk_debug_set(ctx, 5, 1))
+        t0 = time.time()
+        batch.encode_into(out_kv, seg_t, len(seg) - 1, bs, out_blocks, out_cap, out_off, blk_cap, st_enc,
+                          seg_out=seg_out)
+        NW = 16 + 8 * 32768
+        w = (ctypes.c_uint64 * NW)()
+        check(lib().lsmblk_debug_counters(ctx, w, NW))
+        check(lib().lsmblk_debug_set(ctx, 5, 0))
+        a = np.frombuffer(w, dtype=np.uint64).astype(np.int64)
+        tr = a[16:].reshape(-1, 8)
+        tr = tr[tr[:, 0] > 0]
+        t_0 = tr[:, 0].min()
+        q = lambda x: {p: round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)}
+        print(json.dumps({"fused_trace": {
+            "walkers": int(len(tr)), "walk_start_us": q((tr[:, 0] - t_0) / 100), "walk_us": q((tr[:, 1] - tr[:, 0]) / 100),
+            "walk_end_us": q((tr[:, 1] - t_0) / 100), "walker_helper_wait_frac": q(tr[:, 2] / np.maximum(1, tr[:, 1] - tr[:, 0])),
+            "windows": q(tr[:, 3]), "blocks": q(tr[:, 4]),
+            "us_per_window": q((tr[:, 1] - tr[:, 0]) / 100 / np.maximum(1, tr[:, 3])),
+            "emit_items": int(a[2]), "emit_waited_items": int(a[1]), "emit_wait_us_total": round(a[0] / 100, 1),
+            "emit_wait_us_per_item": round(a[0] / 100 / max(1, a[2]), 3),
+            "last_emitter_end_us": round((a[3] - t_0) / 100, 1)}}), flush=True)
+        return None
     if args.ablate is not None and not extra:
         if args.ablate >= 65536:  # plan masks: the plan kernel alone (emit not launched)
             res = {}
@@ -278,15 +315,18 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
         return None
     elapsed, (dec_ms, enc_ms) = timed(step, steps, warmup, world, dev)
 
-    # correctness of the last step: re-encoded bytes == input bytes
+    # correctness of the last step: re-encoded bytes == input bytes (the slots packed first)
     sd, se = st_dec.cpu().tolist(), st_enc.cpu().tolist()
+    pk_blocks, pk_off = out_blocks, out_off  # (step() keeps writing out_blocks: never rebound)
+    if slots and se[3] == 0 and se[0] == nblk:
+        pk_blocks, pk_off = batch.slots_to_packed(out_blocks, out_off[:nblk + 1], seg_out)
     ok = (sd[3] == 0 and se[3] == 0 and sd[0] == n and se[0] == nblk and se[1] == E
-          and torch.equal(out_blocks[:E], blocks) and torch.equal(out_off[:nblk + 1], blk_off))
+          and torch.equal(pk_blocks[:E], blocks) and torch.equal(pk_off[:nblk + 1], blk_off))
     if not ok:
         log(f"ROUND TRIP MISMATCH dec_stats={sd} enc_stats={se}")
     checked = 0
     if ok and not args.no_oracle_check:
-        checked = oracle_check_blocks(host, seg, bs, blocks, blk_off, out_kv, n, out_blocks, out_off, nblk)
+        checked = oracle_check_blocks(host, seg, bs, blocks, blk_off, out_kv, n, pk_blocks, pk_off, nblk)
         ok = checked == nblk
     t_max, ok_all, checked_all = reduce_ranks(elapsed, ok, checked, world, dev)
 
@@ -315,6 +355,9 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
                    "blocks_per_gpu": nblk, "entries_per_gpu": n, "encoded_bytes_per_gpu": E,
                    "decoded_bytes_per_gpu": D, "block_size": bs, "segments_per_gpu": len(seg) - 1,
                    "parallelism": f"block-sharded x{world} (no data-path collective)",
+                   "encode_output": {"slots": "per-segment slots (LSMBLK_ENCODE_SEG_SLOTS; walk fused with emit)",
+                                     "packed": "segments packed (lsmblk_encode_batch)",
+                                     "slots-unfused": "per-segment slots, separate walk + emit launches"}[args.encode_mode],
                    "rccl_world": world, "roundtrip_bit_exact": bool(ok_all),
                    "oracle_checked_blocks": int(checked_all)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -331,12 +374,12 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
         return result
     result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
     result["read_path_verify"] = read_path_verify(blocks, blk_off, nblk, out_kv, n, K, V, st_dec, dev, stream)
-    result["framing_meta"] = framing_meta(out_blocks, out_off, nblk, seg_t, st_enc, dev, stream)
+    result["framing_meta"] = framing_meta(pk_blocks, pk_off, nblk, seg_t, st_enc, dev, stream)
     result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
     if not args.no_pcie and world == 1:
-        del out_kv, out_blocks
+        del out_kv, out_blocks, pk_blocks, pk_off
         torch.cuda.empty_cache()
         result["pcie_inclusive"] = pcie_inclusive(blocks, blk_off, nblk, kv, seg, bs, dev)
     return result
@@ -865,7 +908,7 @@ def dry_run(args, rank, world, local):
 # ---------------------------------------------------------------------------------------------
 def main():
     args = parse()
-    if args.ablate is not None or args.trace_plan:  # ablation masks and traces: the diagnostics build only
+    if args.ablate is not None or args.trace_plan or args.trace_fused:  # ablation masks, traces: diagnostics build
         from lsm_amd import _build
         os.environ.setdefault("LSMBLK_SO_OVERRIDE", _build.DIAG_SO)
     if "RANK" not in os.environ and args.gpus > 1:

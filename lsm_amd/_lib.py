@@ -24,6 +24,8 @@ LSMBLK_E_OVERFLOW = -7
 LSMBLK_E_INTERNAL = -8
 LSMBLK_E_CHECKSUM = -9
 LSMBLK_DECODE_VERIFY_CRC = 1
+LSMBLK_ENCODE_SEG_SLOTS = 1
+LSMBLK_DEBUG_ENCODE_UNFUSED = 8
 LSMBLK_SHARD_LAST = 1
 LSMBLK_MERGE_RUNS = 0
 LSMBLK_MERGE_TWO_LEVEL = 1
@@ -94,6 +96,7 @@ SIGNATURES = [
     ("lsmblk_decode_batch", I, [P, P, P, U64, ctypes.POINTER(KVStreamC), P, P]),
     ("lsmblk_decode_batch_ex", I, [P, P, P, U64, U32, U32, ctypes.POINTER(KVStreamC), P, P, P]),
     ("lsmblk_encode_batch", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, P, U64, P, U64, P, P]),
+    ("lsmblk_encode_batch_ex", I, [P, ctypes.POINTER(KVStreamC), P, U32, U32, U32, P, U64, P, U64, P, P, P]),
     ("lsmblk_crc32_batch", I, [P, P, P, U64, U32, P, P, P]),
     ("lsmblk_encode_segment_blocks", I, [P, P, U32, P, P, P]),
     ("lsmblk_block_meta_batch", I, [P, P, P, U64, U32, P, U32, P, U64, P, P, P]),

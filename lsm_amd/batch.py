@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from ._lib import (CompactOptsC, KVStreamC, KeyRangeC, LSMBLK_DECODE_VERIFY_CRC, LSMBLK_E_CAPACITY,
-                   LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
+                   LSMBLK_ENCODE_SEG_SLOTS, LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
 
 STATS_WORDS = 4
 _ctx_lock = threading.Lock()
@@ -298,8 +298,10 @@ def encode_bound(kv: KVStream, key_bytes: int, val_bytes: int):
 
 
 def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: int, out, out_cap,
-                blk_off, blk_cap, stats, stream=None):
-    """Asynchronous encode into preallocated buffers (no host sync)."""
+                blk_off, blk_cap, stats, stream=None, seg_out=None):
+    """Asynchronous encode into preallocated buffers (no host sync).  With seg_out (int64[2 nseg])
+    the output is per-segment slots (LSMBLK_ENCODE_SEG_SLOTS, include/lsmblk.h): every segment's
+    blocks at its own slot, seg_out[s] = (slot, bytes); slots_to_packed packs them."""
     dev = _dev_index(seg_start)
     kv.check(dev, "kv")
     _need(seg_start, torch.int32, "seg_start", dev, nseg + 1)
@@ -307,9 +309,54 @@ def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: in
     _need(blk_off, torch.int64, "blk_off", dev, blk_cap)
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     c = kv._c()
-    _native("lsmblk_encode_batch", dev, stream, ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
-            _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
-            _stream_ptr(stream, dev), what="lsmblk_encode_batch")
+    if seg_out is None:
+        _native("lsmblk_encode_batch", dev, stream, ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
+                _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
+                _stream_ptr(stream, dev), what="lsmblk_encode_batch")
+        return
+    _need(seg_out, torch.int64, "seg_out", dev, 2 * nseg)
+    _native("lsmblk_encode_batch_ex", dev, stream, ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
+            LSMBLK_ENCODE_SEG_SLOTS, _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, seg_out.data_ptr(),
+            stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_encode_batch_ex")
+
+
+def encode_kv_slots(kv: KVStream, seg_start, block_size: int, stream=None):
+    """Per-segment slot output (LSMBLK_ENCODE_SEG_SLOTS) -> (out u8 tensor, blk_off int64
+    tensor[nblk+1], seg_out int64 tensor[nseg, 2] of (slot, bytes))."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    seg_start = _u32_table(seg_start, dev)
+    nseg = seg_start.numel() - 1
+    kb, vb = kv.byte_sizes()
+    out_cap, blk_cap = encode_bound(kv, kb, vb)
+    out = _aligned_empty(out_cap, dev)
+    blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    seg_out = torch.zeros(max(2 * nseg, 1), dtype=torch.int64, device=dev)
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    encode_into(kv, seg_start, nseg, block_size, out, out_cap, blk_off, blk_cap, stats, stream, seg_out=seg_out)
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "encode_kv_slots")
+    nblk = stats[0].item()
+    return out, blk_off[:nblk + 1], seg_out[:2 * nseg].view(-1, 2)
+
+
+def slots_to_packed(out: torch.Tensor, blk_off: torch.Tensor, seg_out: torch.Tensor):
+    """The slot output of encode_kv_slots / encode_into(seg_out=...) packed as lsmblk_encode_batch
+    writes it: (blocks, blk_off[nblk+1]).  Test and bench helper (copies every segment)."""
+    so = seg_out.view(-1, 2)
+    starts, lens = so[:, 0].contiguous(), so[:, 1].contiguous()
+    dense = torch.cumsum(lens, 0) - lens
+    sl, ll = starts.tolist(), lens.tolist()
+    parts = [out[a:a + b] for a, b in zip(sl, ll) if b]
+    blocks = torch.cat(parts) if parts else out[:0]
+    nblk = blk_off.numel() - 1
+    b = blk_off[:nblk]
+    seg = torch.searchsorted(starts, b, right=True) - 1
+    packed = torch.empty(nblk + 1, dtype=torch.int64, device=out.device)
+    packed[:nblk] = b - starts[seg] + dense[seg]
+    packed[nblk] = int(lens.sum().item())
+    return blocks, packed
 
 
 def encode_kv(kv: KVStream, seg_start, block_size: int, stream=None):

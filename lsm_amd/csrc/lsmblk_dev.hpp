@@ -575,7 +575,19 @@ struct lsmblk_ctx {
   uint32_t* blk_first = nullptr;
   uint32_t* ent = nullptr;       // per (segment-local) block: its encoded size (plan walk)
   uint32_t* big_list = nullptr;  // n+1 u32: emit_big_kernel's per-block flags (bytes)
+  uint32_t* blk_sz = nullptr;    // n+1: every block's size (per-segment slot output)
   uint64_t rec_cap = 0;
+  // fused walk + emit (encode_fused_kernel): 4 uncached granules per block record, R(w, i) < n +
+  // walkers; per walker its block count (uncached granule, and plain); per record a big-block flag
+  uint64_t* frec = nullptr;
+  uint64_t frec_cap = 0;
+  uint64_t* fdone = nullptr;
+  uint64_t fdone_cap = 0;
+  uint32_t* fwnb = nullptr;
+  uint64_t fwnb_cap = 0;
+  uint8_t* fbig = nullptr;
+  uint64_t fbig_cap = 0;
+  bool fuse_off = false;         // diagnostics: slot output through plan_walk + emit (A/B)
   uint64_t* lag_gran = nullptr;  // lagged decode granules (uncached): 3 aggregate + 3 base per block,
   uint64_t lag_blk_cap = 0;      //   then 3 aggregate + 3 inclusive per 64-block tile; blocks covered
   uint32_t rot_poison = 0;       // diagnostics builds only: LSMBLK_DEBUG_ROT_POISON
@@ -739,7 +751,8 @@ namespace lsmblk_impl {
 // stream that also holds the previous rank's crossing block and the halo), not all of it.
 int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
                   const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
-                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span = false);
+                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span = false,
+                  uint32_t flags = 0, uint64_t* seg_out = nullptr);
 // lsmblk_encode_segment_blocks for the encode that just ran on this context.
 int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nseg_max, const uint64_t* enc_stats,
                           uint32_t* seg_blk, hipStream_t st);

@@ -1296,6 +1296,11 @@ struct PlanArgs {
   uint64_t* dbg;           // optional realtime trace per segment (LSMBLK_DEBUG_COUNTERS)
   uint32_t skip;           // ablation (timing only, emit not launched): 1 << 16 helpers skip the key
                            // loads and LCPs, 1 << 17 walkers skip the scans (one block per window)
+  // per-segment slot output (LSMBLK_ENCODE_SEG_SLOTS; encode_fused_kernel has the layout): segment
+  // g's blocks at seg_slot(g) on; seg_out[2 g] = that slot, [2 g + 1] = its bytes; blk_sz = the
+  // blocks' sizes (a segment's last block does not end where the next one starts)
+  uint64_t* seg_out;
+  uint32_t* blk_sz;
 };
 
 __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
@@ -1303,6 +1308,15 @@ __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
   if (a.dn) a.n = uni64(*a.dn);
   if (a.dnseg) a.nseg = uni(*a.dnseg);
   return a;
+}
+
+// First byte of segment g's slot in the per-segment output (LSMBLK_ENCODE_SEG_SLOTS): the keys and
+// values of the segments before it plus 18 bytes per entry, an upper bound of their encoded size
+// (encode_fused_kernel).
+__device__ __forceinline__ uint64_t seg_slot(const uint32_t* key_off, const uint32_t* val_off, const uint32_t* seg_start,
+                                             uint32_t g) {
+  const uint32_t b = seg_start[0], s = seg_start[g];
+  return uint64_t(key_off[s] - key_off[b]) + uint64_t(val_off[s] - val_off[b]) + 18ull * (s - b);
 }
 
 constexpr uint32_t kAlcpUnsorted = 0x80000000u;
@@ -1469,61 +1483,38 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
   }
 }
 
-// (fused: three workgroups of 8 waves per CU, so that up to 3 K segments walk at once)
-__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4))) void plan_walk_kernel(PlanArgs a0) {
-  const PlanArgs a = resolve(a0);
-  static_assert(kRing >= 2 * kChunk && (kRing & (kRing - 1)) == 0, "plan ring size");
-  __shared__ uint32_t crec[4][kRing], calcp[4][kRing];
+// The walker's side of the ring hand-off: its window start, and the producer's count.
+struct WalkRing {
+  const uint32_t* CR;   // rec per entry, slot (e - S0) % kRing
+  const uint32_t* CA;   // alcp per entry
+  uint32_t* cons;       // walker's window start (relative to S0)
+  const uint32_t* prod; // entries produced (relative to S0)
+  uint32_t S0;          // the ring's base entry (the first entry of the walker's first segment)
+  uint32_t known = 0;   // entries the producer has finished (relative to S0)
+  bool stalled = false; // a poll gave up: the walk goes on over stale data, the call reports TIMEOUT
+};
+
+// The greedy block walk of one segment [s0, s1) over the helper's ring (SsTableBuilder::add over
+// BlockBuilder::add: src/table/builder.rs:48-65, src/block/builder.rs:54-73).  Every block, in
+// order, goes to sink(first entry, end entry, encoded size, blocks before it in the segment,
+// bytes before it in the segment) (wave-uniform arguments); returns (blocks, bytes).
+template <class Sink>
+__device__ __forceinline__ void walk_segment(const PlanArgs& a, const PlanKeys& K, WalkRing& R, uint32_t s0, uint32_t s1,
+                                             uint32_t& err, uint32_t& nb, uint64_t& bytes, Sink&& sink, uint64_t* tr,
+                                             uint64_t& waited, uint64_t& windows) {
   const uint32_t l = lane_id();
-  // waves 0-3 walk segments, wave 4 + w produces (rec, alcp) into walker w's ring
-  __shared__ uint32_t hand_g[4], hand_prod[4], hand_cons[4];
-  const uint32_t wv = wave_id(), ww = wv & 3;
-  if (wv < 4) {
-    const uint32_t t = take_ticket(a.ticket);
-    if (l == 0) {
-      hand_g[wv] = t;
-      hand_prod[wv] = 0;
-      hand_cons[wv] = 0;
-    }
-  }
-  __syncthreads();
-  const uint32_t g = uni(hand_g[ww]);
-  uint32_t* CR = crec[ww];
-  uint32_t* CA = calcp[ww];
-  if (g >= a.nseg) return;
-  uint32_t err = 0;
-  uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
-  if ((!a.span && g == 0 && s0 != 0) || (!a.span && g == a.nseg - 1 && uint64_t(s1) != a.n) || s0 > s1 ||
-      uint64_t(s1) > a.n) {
-    err |= LSMBLK_ERR_SEGMENTS;
-    s1 = s0 = (s0 > a.n ? uint32_t(a.n) : s0);
-    if (s1 < s0) s1 = s0;
-  }
-  const PlanKeys K = plan_keys(a);
-  uint64_t* const tr = kDiag && a.dbg && g < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(g) : nullptr;  // (diagnostics)
-  if (wv >= 4) {
-    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
-    const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
-                          (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
-    raise_err(a.stats, werr);
-    return;
-  }
-  // (rec, alcp) of entry e at LDS slot (e - s0) % kRing, written by the helper wave; `need` waits
+  // (rec, alcp) of entry e at LDS slot (e - S0) % kRing, written by the helper wave; `need` waits
   // until the window's entries are in and tells the helper where the window starts.
-  uint32_t known = 0;  // entries of the ring the producer has finished (relative to s0)
-  bool stalled = false;
-  uint64_t waited = 0, windows = 0;
-  if (tr && l == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
   auto need = [&](uint32_t j0, uint32_t wend) {
-    __hip_atomic_store(&hand_cons[ww], j0 - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(R.cons, j0 - R.S0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (tr) ++windows;
-    if (wend - s0 > known && !stalled) {
+    if (wend - R.S0 > R.known && !R.stalled) {
       const uint64_t w0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
       uint32_t spins = 0;
-      while ((known = __hip_atomic_load(&hand_prod[ww], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < wend - s0) {
+      while ((R.known = __hip_atomic_load(R.prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < wend - R.S0) {
         if (++spins > kSpinMax) {
           err |= LSMBLK_ERR_TIMEOUT;
-          stalled = true;  // walk on over stale ring data: the call fails with TIMEOUT
+          R.stalled = true;  // walk on over stale ring data: the call fails with TIMEOUT
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1532,8 +1523,11 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
   };
-  uint32_t nb = 0;
-  uint64_t bytes = 0;
+  const uint32_t* const CR = R.CR;
+  const uint32_t* const CA = R.CA;
+  const uint32_t S0 = R.S0;
+  nb = 0;
+  bytes = 0;
   const uint64_t bs = a.block_size;
   const bool narrow = bs < (1ull << 30);
   for (uint32_t s = s0; s < s1;) {
@@ -1545,12 +1539,9 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       const uint32_t wend = s1 - j0 < 64 ? s1 : j0 + 64;
       need(j0, wend);
       if (diag_mask(a.skip) & (1u << 17)) {  // ablation: consume the window as one block, no scans
-        const uint32_t x = (j0 + l - s0) & (kRing - 1);
+        const uint32_t x = (j0 + l - S0) & (kRing - 1);
         const uint32_t rr = j0 + l < s1 ? CR[x] + CA[x] : 0u;
-        if (l == 0) {
-          a.rec_first[s0 + nb] = s;
-          a.sz[s0 + nb] = __builtin_amdgcn_readfirstlane(rr);
-        }
+        sink(s, wend, uint32_t(__builtin_amdgcn_readfirstlane(rr)), nb, bytes);
         ++nb;
         s = wend;
         break;
@@ -1559,7 +1550,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       const bool valid = e < s1;
       uint32_t r = 0, al = kAlcpLcp;
       if (valid) {
-        const uint32_t x = (e - s0) & (kRing - 1);
+        const uint32_t x = (e - S0) & (kRing - 1);
         r = CR[x];
         if (e != s) al = CA[x];
       }
@@ -1603,10 +1594,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       if (m) {
         uint32_t f = uint32_t(__builtin_ctzll(m));
         const uint64_t size = lane64(before, f);
-        if (l == 0) {
-          a.rec_first[s0 + nb] = s;
-          a.sz[s0 + nb] = uint32_t(size);
-        }
+        sink(s, j0 + f, uint32_t(size), nb, bytes);
         ++nb;
         bytes += size;
         s = j0 + f;
@@ -1633,10 +1621,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
           }
           const uint32_t f2 = uint32_t(__builtin_ctzll(m2));
           const uint32_t size2 = uint32_t(__builtin_amdgcn_readlane(before2, f2));
-          if (l == 0) {
-            a.rec_first[s0 + nb] = s;
-            a.sz[s0 + nb] = size2;
-          }
+          sink(s, j0 + f2, size2, nb, bytes);
           ++nb;
           bytes += size2;
           s = j0 + f2;
@@ -1648,6 +1633,191 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       carry += incl_all;
     }
   }
+}
+
+// plan_produce for the fused walk + emit launch, software-pipelined over chunks: a chunk's 8 key
+// loads go out, then the next chunk's 20 entry-offset loads, and only then does the chunk wait for
+// its keys (vmcnt(20)) -- one memory round trip per chunk instead of two.  (Beside emit's stream the
+// round trips are long: the unpipelined helper held its walker to ~2.5 us per window.)  Both sets
+// are issued by inline asm so that the compiler neither sinks the key loads into the per-entry
+// branch (it did) nor waits for the offsets there; registers loaded by asm are landed by explicit
+// waits and then redefined for the compiler.
+struct ProdOffs {
+  uint32_t kp[kProdBatch], kn[kProdBatch], pp[kProdBatch], v0[kProdBatch], v1[kProdBatch];
+};
+// the 5 offset loads of entry lane l's i-th entry of chunk [c, cend) (indices clamped: always issued)
+__device__ __forceinline__ void prod_offs_issue(const rsrc_t& RKO, const rsrc_t& RVO, uint32_t c, uint32_t cend,
+                                                ProdOffs& P) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (uint32_t i = 0; i < kProdBatch; ++i) {
+    uint32_t e = c + 64 * i + l;
+    e = e < cend ? e : cend - 1;
+    const uint32_t oe = 4 * e, op = 4 * (e > 0 ? e - 1 : 0u);
+    asm volatile(
+        "buffer_load_dword %0, %5, %7, 0 offen\n\t"
+        "buffer_load_dword %1, %5, %7, 0 offen offset:4\n\t"
+        "buffer_load_dword %2, %6, %7, 0 offen\n\t"
+        "buffer_load_dword %3, %5, %8, 0 offen\n\t"
+        "buffer_load_dword %4, %5, %8, 0 offen offset:4"
+        : "=&v"(P.kp[i]), "=&v"(P.kn[i]), "=&v"(P.pp[i]), "=&v"(P.v0[i]), "=&v"(P.v1[i])
+        : "v"(oe), "v"(op), "s"(RKO), "s"(RVO));
+  }
+}
+__device__ __forceinline__ void prod_offs_land(ProdOffs& P) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (uint32_t i = 0; i < kProdBatch; ++i)
+    asm volatile("" : "+v"(P.kp[i]), "+v"(P.kn[i]), "+v"(P.pp[i]), "+v"(P.v0[i]), "+v"(P.v1[i]));
+}
+__device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t s0, uint32_t s1, uint32_t* CR,
+                                  uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t& err) {
+  static_assert(kChunk == 64 * kProdBatch && kProdBatch == 4, "one load batch of 4 entries per lane per chunk");
+  const uint32_t l = lane_id();
+  const uint32_t klim = K.glead + uni(a.key_off[a.n]);
+  if (s0 >= s1) return;
+  const uint32_t nb4 = uint32_t(min(uint64_t(a.n + 1) * 4, uint64_t(0xFFFFFFF0u)));
+  const rsrc_t RKO = make_rsrc(a.key_off, nb4), RVO = make_rsrc(a.val_off, nb4);
+  ProdOffs P;
+  asm volatile("s_nop 4" ::: "memory");  // (VALU-written descriptor SGPRs before a VMEM read of them, inside asm)
+  prod_offs_issue(RKO, RVO, s0, s1 - s0 < kChunk ? s1 : s0 + kChunk, P);
+  prod_offs_land(P);
+  for (uint32_t c = s0; c < s1; c += kChunk) {
+    const uint32_t cend = s1 - c < kChunk ? s1 : c + kChunk;
+    if (c - s0 + kChunk > kRing) {  // ring space: the walker's window must have passed c + kChunk - kRing
+      const uint32_t need = c - s0 + kChunk - kRing;
+      uint32_t spins = 0;
+      while (__hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+        if (++spins > kSpinMax) {
+          err |= LSMBLK_ERR_TIMEOUT;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    u32x4 xk[kProdBatch], xp[kProdBatch];
+#pragma unroll
+    for (uint32_t i = 0; i < kProdBatch; ++i) {
+      const uint32_t ok = K.glead + P.kp[i], op = K.glead + P.pp[i];
+      asm volatile(
+          "buffer_load_dwordx4 %0, %2, %4, 0 offen\n\t"
+          "buffer_load_dwordx4 %1, %3, %4, 0 offen"
+          : "=&v"(xk[i]), "=&v"(xp[i])
+          : "v"(ok), "v"(op), "s"(K.gk));
+    }
+    // the next chunk's offsets (after the last chunk: its own again -- always 20 loads)
+    const uint32_t cn = c + kChunk < s1 ? c + kChunk : c;
+    ProdOffs Pn;
+    prod_offs_issue(RKO, RVO, cn, s1 - cn < kChunk ? s1 : cn + kChunk, Pn);
+    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // this chunk's keys (issued before the 20)
+#pragma unroll
+    for (uint32_t i = 0; i < kProdBatch; ++i) asm volatile("" : "+v"(xk[i]), "+v"(xp[i]));
+#pragma unroll
+    for (uint32_t i = 0; i < kProdBatch; ++i) {
+      const uint32_t e = c + 64 * i + l;
+      if (e >= cend) continue;
+      const uint32_t kp = P.kp[i], pp = P.pp[i], kl = P.kn[i] - kp, x = (e - s0) & (kRing - 1);
+      if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
+      uint32_t al = 0;
+      if (e != s0) {  // LCP with the predecessor, bit 31 = out of order (as plan_produce)
+        const uint32_t pl = kp - pp, m = pl < kl ? pl : kl;
+        uint32_t lcp = m, w0 = 0, w1 = 0;
+        if (K.glead + kp + 16 <= klim && K.glead + pp + 16 <= klim) {
+          const uint32_t Pw[4] = {xp[i].x, xp[i].y, xp[i].z, xp[i].w}, Qw[4] = {xk[i].x, xk[i].y, xk[i].z, xk[i].w};
+          uint32_t t[4];
+#pragma unroll
+          for (uint32_t d = 0; d < 4; ++d) t[d] = uint32_t(__builtin_ctzg(Pw[d] ^ Qw[d], 32)) >> 3;  // 4: equal
+          const uint32_t z16 = t[0] < 4 ? t[0] : t[1] < 4 ? 4 + t[1] : t[2] < 4 ? 8 + t[2] : 12 + t[3];
+          const uint32_t zd = z16 >> 2;
+          if (z16 < m) {
+            lcp = z16;
+            w0 = zd == 0 ? Pw[0] : zd == 1 ? Pw[1] : zd == 2 ? Pw[2] : Pw[3];
+            w1 = zd == 0 ? Qw[0] : zd == 1 ? Qw[1] : zd == 2 ? Qw[2] : Qw[3];
+          }
+          if (!(z16 < m || m <= 16)) {  // equal first 16 bytes: the rest by dwords
+            for (uint32_t d = 4; 4 * d < m; ++d) {
+              const uint32_t y0 = K.dword(pp + 4 * d), y1 = K.dword(kp + 4 * d);
+              if (y0 != y1) {
+                const uint32_t z = 4 * d + (__builtin_ctz(y0 ^ y1) >> 3);
+                if (z < m) {
+                  lcp = z;
+                  w0 = y0;
+                  w1 = y1;
+                }
+                break;
+              }
+            }
+          }
+        } else {
+          lcp = key_lcp(K, pp, pl, kp, kl, w0, w1);
+        }
+        const uint32_t sh = 8 * (lcp & 3);
+        const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
+        al = (lcp < kAlcpLcp ? lcp : kAlcpLcp) | (sorted ? 0u : kAlcpUnsorted);
+      }
+      CR[x] = kl + (P.v1[i] - P.v0[i]);
+      CA[x] = al;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (l == 0) __hip_atomic_store(prod, cend - s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prod_offs_land(Pn);
+    P = Pn;
+  }
+}
+
+// (fused: three workgroups of 8 waves per CU, so that up to 3 K segments walk at once)
+__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4))) void plan_walk_kernel(PlanArgs a0) {
+  const PlanArgs a = resolve(a0);
+  static_assert(kRing >= 2 * kChunk && (kRing & (kRing - 1)) == 0, "plan ring size");
+  __shared__ uint32_t crec[4][kRing], calcp[4][kRing];
+  const uint32_t l = lane_id();
+  // waves 0-3 walk segments, wave 4 + w produces (rec, alcp) into walker w's ring
+  __shared__ uint32_t hand_g[4], hand_prod[4], hand_cons[4];
+  const uint32_t wv = wave_id(), ww = wv & 3;
+  if (wv < 4) {
+    const uint32_t t = take_ticket(a.ticket);
+    if (l == 0) {
+      hand_g[wv] = t;
+      hand_prod[wv] = 0;
+      hand_cons[wv] = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t g = uni(hand_g[ww]);
+  uint32_t* CR = crec[ww];
+  uint32_t* CA = calcp[ww];
+  if (g >= a.nseg) return;
+  uint32_t err = 0;
+  uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
+  if ((!a.span && g == 0 && s0 != 0) || (!a.span && g == a.nseg - 1 && uint64_t(s1) != a.n) || s0 > s1 ||
+      uint64_t(s1) > a.n) {
+    err |= LSMBLK_ERR_SEGMENTS;
+    s1 = s0 = (s0 > a.n ? uint32_t(a.n) : s0);
+    if (s1 < s0) s1 = s0;
+  }
+  const PlanKeys K = plan_keys(a);
+  uint64_t* const tr = kDiag && a.dbg && g < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(g) : nullptr;  // (diagnostics)
+  if (wv >= 4) {
+    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
+    const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
+                          (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
+    raise_err(a.stats, werr);
+    return;
+  }
+  uint64_t waited = 0, windows = 0;
+  if (tr && l == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+  WalkRing R{CR, CA, &hand_cons[ww], &hand_prod[ww], s0};
+  uint32_t nb = 0;
+  uint64_t bytes = 0;
+  walk_segment(a, K, R, s0, s1, err, nb, bytes,
+               [&](uint32_t first, uint32_t, uint32_t size, uint32_t i, uint64_t) {
+                 if (l == 0) {
+                   a.rec_first[s0 + i] = first;
+                   a.sz[s0 + i] = size;
+                 }
+               },
+               tr, waited, windows);
   if (tr && l == 0) {
     tr[1] = __builtin_amdgcn_s_memrealtime();
     tr[2] = waited;
@@ -1670,7 +1840,11 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     const uint64_t inc[2] = {excl[0] + agg[0], excl[1] + agg[1]};
     publish<2>(a.inc, g, inc, a.tag, 2, a.poll);
   }
-  const uint64_t B0 = excl[0], O0 = excl[1];
+  const uint64_t B0 = excl[0], O0 = a.seg_out ? seg_slot(a.key_off, a.val_off, a.seg_start, g) : excl[1];
+  if (a.seg_out && l == 0) {
+    a.seg_out[2ull * g] = O0;
+    a.seg_out[2ull * g + 1] = bytes;
+  }
   uint64_t oc = O0;
   for (uint32_t c = 0; c < nb; c += 64) {
     const uint32_t i = c + l;
@@ -1683,6 +1857,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     if (i < nb) {
       const uint64_t bi = B0 + i;
       a.blk_first[bi] = first;
+      if (a.blk_sz) a.blk_sz[bi] = sz;
       if (bi < a.blk_cap) a.blk_off[bi] = oc + incl - sz;
     }
     oc += __shfl(incl, 63, 64);
@@ -1692,7 +1867,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     a.blk_first[Bt] = a.span ? s1 : uint32_t(a.n);
     if (Bt < a.blk_cap) a.blk_off[Bt] = Ot;
     a.stats[0] = Bt;
-    a.stats[1] = Ot;
+    a.stats[1] = excl[1] + bytes;  // (the encoded bytes; in slot mode Ot is where they end)
     if (Bt + 1 > a.blk_cap || Ot > a.out_cap) err |= LSMBLK_ERR_CAPACITY;
   }
   raise_err(a.stats, err);
@@ -1714,6 +1889,9 @@ struct EmitArgs {
   // per block: 1 = beyond the LDS image, left by emit_kernel for emit_big_kernel (a flag per
   // block, not a list: appending through one shared counter cost 0.6 ms on 64 Ki big blocks)
   uint8_t* big_flag;
+  // optional: every block's encoded size (per-segment slot output, LSMBLK_ENCODE_SEG_SLOTS: a
+  // segment's last block does not end where the next block starts); else blk_off[bi + 1] - blk_off[bi]
+  const uint32_t* blk_sz;
   uint32_t skip;  // ablation mask (timing experiments only): 16 entry-lane byte writes,
                   // 32 bulk value copy, 64 flush, 128 LCP
   const uint64_t* dn;  // optional: n read from device memory (overrides n)
@@ -1791,6 +1969,185 @@ struct EmitMeta {
   uint32_t kb0, kb1, vb0, vb1;
 };
 
+// One fast-path block of emit (wave-uniform): entries [s, s + n), output [O, O + size), its keys
+// staged at kimg[klead], its values at img[vlead], fl = its first key's length.
+struct EmitBlk {
+  uint32_t s, n;
+  uint64_t O, size;
+  uint32_t kb0, vb0, klead, vlead, olead, fl;
+};
+// The first 64 entries' offsets and ts of a block, loaded by entry lane k one block ahead.
+struct EmitPf {
+  uint32_t ko0 = 0, ko1 = 0, vo0 = 0, vo1 = 0;
+  uint64_t ts = 0;
+};
+
+// Phase 1 of emit_kernel for block B (staged and landed): returns the block's data length, ncs =
+// its image chunks; eh / et = the first / last 16 bytes of the value of entries l, l + 64.
+__device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, const EmitBlk& B, const EmitPf& pf,
+                                                uint32_t (&eh)[2][4], uint32_t (&et)[2][4], uint32_t& ncs, uint32_t& err) {
+  const uint32_t l = lane_id();
+  const uint32_t s = B.s, n = B.n, kb0 = B.kb0, vb0 = B.vb0, klead = B.klead, vlead = B.vlead, olead = B.olead, fl = B.fl;
+  const uint64_t size = B.size;
+  // Phase 1, entry lanes: LCP against the first key, record positions (wave scan), tables,
+  // and the value bytes of each value's two partial edge chunks (captured in registers: the
+  // in-place move below overwrites the staged values).
+  ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
+  for (uint32_t j = 4 * l; j < ncs; j += 256) *reinterpret_cast<u32x4*>(L.cent + j) = u32x4{~0u, ~0u, ~0u, ~0u};
+  uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
+  uint32_t dc = 0;
+#pragma unroll
+  for (uint32_t it = 0; it < 2; ++it) {
+    const uint32_t c = 64 * it;
+    if (c >= n) break;
+    const uint32_t k = c + l;
+    uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
+    if (k < n) {
+      uint32_t ko0, ko1, vo0, vo1;
+      if (it == 0) {  // prefetched one block ahead
+        ko0 = pf.ko0; ko1 = pf.ko1; vo0 = pf.vo0; vo1 = pf.vo1;
+        L.ts[k] = pf.ts;
+      } else {
+        ko0 = a.key_off[s + k]; ko1 = a.key_off[s + k + 1];
+        vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1];
+        L.ts[k] = a.ts[s + k];
+      }
+      kp = ko0 - kb0;
+      kl = ko1 - ko0;
+      vp = vo0 - vb0;
+      vl = vo1 - vo0;
+      if (k != 0 && !(diag_mask(a.skip) & 128)) {
+        // the first 16 bytes by selects, no branches: z = the first differing byte (16 if none);
+        // bytes read past either key do not matter, p is capped at m (the key image has 16 B
+        // of slack before the value image, which is LDS too)
+        const uint32_t m = fl < kl ? fl : kl;
+        uint32_t z = 16;
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+          const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
+          z = x ? 4 * i + (__builtin_ctz(x) >> 3) : z;
+        }
+        p = z < 16 && z < m ? z : m;  // (z == 16: m unless the loop below finds a difference)
+        bool done = z < 16 || m <= 16;
+        for (uint32_t q = 16; !done && q < m; q += 4) {
+          const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
+          if (x) {
+            const uint32_t zq = q + (__builtin_ctz(x) >> 3);
+            p = zq < m ? zq : m;
+            done = true;
+          }
+        }
+      }
+      const uint32_t vs = vlead + vp;
+      lds_read16(L.img, vs, eh[it]);
+      lds_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
+    }
+    const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
+    const uint32_t incl = wave_incl_scan<uint32_t>(dg);
+    const uint32_t pos = dc + incl - dg;
+    dc += __shfl(incl, 63, 64);
+    if (k < n) {
+      const uint32_t sfx = kl - p;
+      *reinterpret_cast<u32x4*>(L.erec + 4 * k) = u32x4{pos | (p << 16), (klead + kp + p) | (vl << 16), sfx, 0u};
+      // the image chunks lying wholly inside this value -> their source bytes in the staged
+      // values (every other chunk keeps ~0)
+      {
+        const uint32_t vdb = olead + pos + 14 + sfx;  // image byte of the value
+        const uint32_t srcb = vlead + vp - vdb;       // + image byte = staged byte (mod 2^32)
+        for (uint32_t cc = (vdb + 15) >> 4; 16 * cc + 16 <= vdb + vl; ++cc) L.cent[cc] = srcb + 16 * cc;
+      }
+    }
+  }
+  if (uint64_t(dc) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
+  return dc;
+}
+
+// Phases 2b-3 of emit_kernel, the offsets table and the flush of block B's image.
+__device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const EmitBlk& B, uint32_t data_len,
+                                            uint32_t ncs, const uint32_t (&eh)[2][4], const uint32_t (&et)[2][4]) {
+  const uint32_t l = lane_id();
+  const uint32_t n = B.n, olead = B.olead;
+  const uint64_t O = B.O, size = B.size;
+  // Phase 2a (ascending): image chunk -> source byte of a chunk lying wholly inside one
+  // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
+  // kEB chunk groups per batch: every LDS read of the batch is issued before its uses.
+  // (EMIT_DIRECT_CENT: the entry lanes wrote the map in phase 1)
+  wave_sync();
+  // Phase 2b (descending): move whole-value chunks to their place in the encoded block.
+  // A value only moves up (its destination follows its own header and every earlier
+  // record), so a chunk's source lies below the chunk's end: walking batches of chunks from
+  // the top, with all of a batch's reads before its writes, never overwrites a source still
+  // unread.
+  if (!(diag_mask(a.skip) & 32)) {
+    const int32_t top = int32_t((ncs + 63) & ~63u);
+    for (int32_t c0 = top; c0 > 0; c0 -= int32_t(64 * kEB)) {
+      uint32_t src[kEB];
+      u32x4 v[kEB];
+#pragma unroll
+      for (uint32_t j = 0; j < kEB; ++j) {
+        const int32_t c = c0 - int32_t(64 * (j + 1)) + int32_t(l);
+        src[j] = (c0 >= int32_t(64 * (j + 1)) && uint32_t(c) < ncs) ? L.cent[c] : ~0u;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kEB; ++j)
+        if (src[j] != ~0u) v[j] = *reinterpret_cast<const u32x4*>(L.img + src[j]);
+#pragma unroll
+      for (uint32_t j = 0; j < kEB; ++j)
+        if (src[j] != ~0u) *reinterpret_cast<u32x4*>(L.img + 16 * (c0 - int32_t(64 * (j + 1)) + int32_t(l))) = v[j];
+    }
+  }
+  wave_sync();
+  // Phase 3, entry lanes: header, key suffix, ts, value_len, and the value bytes of the
+  // partial edge chunks (from the registers captured in phase 1).
+  if (!(diag_mask(a.skip) & 16)) {
+#pragma unroll
+    for (uint32_t it = 0; it < 2; ++it) {
+      const uint32_t k = 64 * it + l;
+      if (64 * it >= n) break;
+      if (k >= n) continue;
+      const u32x4 er = *reinterpret_cast<const u32x4*>(L.erec + 4 * k);
+      const uint32_t pos = er.x & 0xFFFF, p = er.x >> 16, ks = er.y & 0xFFFF, vl = er.y >> 16, sfx = er.z;
+      const uint32_t vd = pos + 14 + sfx;
+      const uint64_t tsv = L.ts[k];
+      // unaligned LDS stores (the image is not swizzled): every field is one or two stores
+      uint8_t* o = L.img;
+      const uint32_t ox = olead + pos;
+      *reinterpret_cast<uint32_t*>(o + ox) = bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16);
+      for (uint32_t t = 0; t < sfx; t += 16) {
+        const uint32_t o2 = sfx >= 16 ? min(t, sfx - 16) : 0u;
+        uint32_t v[4];
+        lds_read16(L.kimg, ks + o2, v);
+        if (sfx >= 16) *reinterpret_cast<u32x4*>(o + ox + 4 + o2) = u32x4{v[0], v[1], v[2], v[3]};
+        else lds_st_short(o + ox + 4, sfx, v);
+      }
+      const uint64_t tbe = __builtin_bswap64(tsv);
+      *reinterpret_cast<u32x2*>(o + ox + 4 + sfx) = u32x2{uint32_t(tbe), uint32_t(tbe >> 32)};
+      *reinterpret_cast<uint16_t*>(o + ox + 12 + sfx) = uint16_t(bswap16(vl & 0xFFFF));
+      // value bytes outside whole chunks: a value of >= 16 bytes rewrites its first and last
+      // 16 (the bytes inside whole chunks are rewritten with what the move put there)
+      const uint32_t A = olead + vd;
+      if (vl >= 16) {
+        *reinterpret_cast<u32x4*>(o + A) = u32x4{eh[it][0], eh[it][1], eh[it][2], eh[it][3]};
+        *reinterpret_cast<u32x4*>(o + A + vl - 16) = u32x4{et[it][0], et[it][1], et[it][2], et[it][3]};
+      } else if (vl) {
+        lds_st_short(o + A, vl, eh[it]);
+      }
+    }
+  }
+  wave_sync();
+  // offsets table + entry count (u16 BE, `as u16`)
+  for (uint32_t k = l; k < n; k += 64)
+    *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.erec[4 * k] & 0xFFFF));
+  if (l == 0) *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * n) = uint16_t(bswap16(n & 0xFFFF));
+  wave_sync();
+  // flush the image: 16-B chunks; only the two end chunks can be partial
+  // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
+  if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run_masked<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
+  wave_sync();
+}
+
 // Persistent waves, software-pipelined one block ahead: while block i is processed, the
 // metadata, the key/value staging loads and the first 64 entries' offsets/ts of block i+1
 // are already in flight (the wave is latency-bound otherwise: ~3 dependent global round
@@ -1816,7 +2173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     m.e = kfirst[bi + 1];
     m.n = m.e - m.s;
     m.O = koff[bi];
-    m.size = koff[bi + 1] - m.O;
+    m.size = a.blk_sz ? uint64_t(kconst(a.blk_sz)[bi]) : koff[bi + 1] - m.O;
   };
   auto meta2 = [&](EmitMeta& m) {
     m.kb0 = uni(a.key_off[m.s]);
@@ -1831,8 +2188,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
            vlead + (m.vb1 - m.vb0) + 24 <= kEmitICap && uint32_t(m.O & 15) + m.size + 8 <= kEmitICap;
   };
   u32x4 kq[2], vq[5];
-  uint32_t pf_ko0 = 0, pf_ko1 = 0, pf_vo0 = 0, pf_vo1 = 0;
-  uint64_t pf_ts = 0;
+  EmitPf pf;
   auto issue = [&](const EmitMeta& m) {  // staging + first-chunk entry loads of block m
     const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
     const rsrc_t RK = make_rsrc(a.keys + m.kb0 - klead, klead + (m.kb1 - m.kb0));
@@ -1846,11 +2202,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     for (uint32_t i = 0; i < 5; ++i)
       if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, kLdAux);
     if (l < m.n) {
-      pf_ko0 = a.key_off[m.s + l];
-      pf_ko1 = a.key_off[m.s + l + 1];
-      pf_vo0 = a.val_off[m.s + l];
-      pf_vo1 = a.val_off[m.s + l + 1];
-      pf_ts = a.ts[m.s + l];
+      pf.ko0 = a.key_off[m.s + l];
+      pf.ko1 = a.key_off[m.s + l + 1];
+      pf.vo0 = a.val_off[m.s + l];
+      pf.vo1 = a.val_off[m.s + l + 1];
+      pf.ts = a.ts[m.s + l];
     }
   };
 
@@ -1887,7 +2243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint32_t olead = uint32_t(O & 15);
     // first key length at kimg[klead]: made uniform before the next block's level-2 loads are
     // issued (read after them, its wait would also cover the first of them: vmcnt is in order)
-    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf_ko1) - kb0;
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf.ko1) - kb0;
     {  // land the staged keys (plain) and values (swizzled block image at vlead)
       const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
       const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
@@ -1914,80 +2270,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       r_vb1 = a.val_off[nxt.e];
     }
     wave_sync();
-    // Phase 1, entry lanes: LCP against the first key, record positions (wave scan), tables,
-    // and the value bytes of each value's two partial edge chunks (captured in registers: the
-    // in-place move below overwrites the staged values).
-    const uint32_t ncs = (olead + uint32_t(size) + 15) >> 4;  // image chunks of the encoded block
-    for (uint32_t j = 4 * l; j < ncs; j += 256) *reinterpret_cast<u32x4*>(L.cent + j) = u32x4{~0u, ~0u, ~0u, ~0u};
-    uint32_t fkw[4];  // first 16 bytes of the first key (LDS broadcast reads)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fkw[i] = lds_dword_at(L.kimg, klead + 4 * i);
-    uint32_t dc = 0;
+    const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl};
     uint32_t eh[2][4], et[2][4];  // first / last 16 bytes of the value of entries l, l + 64
-#pragma unroll
-    for (uint32_t it = 0; it < 2; ++it) {
-      const uint32_t c = 64 * it;
-      if (c >= n) break;
-      const uint32_t k = c + l;
-      uint32_t kp = 0, kl = 0, vp = 0, vl = 0, p = 0;
-      if (k < n) {
-        uint32_t ko0, ko1, vo0, vo1;
-        if (it == 0) {  // prefetched one block ahead
-          ko0 = pf_ko0; ko1 = pf_ko1; vo0 = pf_vo0; vo1 = pf_vo1;
-          L.ts[k] = pf_ts;
-        } else {
-          ko0 = a.key_off[s + k]; ko1 = a.key_off[s + k + 1];
-          vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1];
-          L.ts[k] = a.ts[s + k];
-        }
-        kp = ko0 - kb0;
-        kl = ko1 - ko0;
-        vp = vo0 - vb0;
-        vl = vo1 - vo0;
-        if (k != 0 && !(diag_mask(a.skip) & 128)) {
-          // the first 16 bytes by selects, no branches: z = the first differing byte (16 if none);
-          // bytes read past either key do not matter, p is capped at m (the key image has 16 B
-          // of slack before the value image, which is LDS too)
-          const uint32_t m = fl < kl ? fl : kl;
-          uint32_t z = 16;
-#pragma unroll
-          for (int i = 3; i >= 0; --i) {
-            const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
-            z = x ? 4 * i + (__builtin_ctz(x) >> 3) : z;
-          }
-          p = z < 16 && z < m ? z : m;  // (z == 16: m unless the loop below finds a difference)
-          bool done = z < 16 || m <= 16;
-          for (uint32_t q = 16; !done && q < m; q += 4) {
-            const uint32_t x = lds_dword_at(L.kimg, klead + q) ^ lds_dword_at(L.kimg, klead + kp + q);
-            if (x) {
-              const uint32_t zq = q + (__builtin_ctz(x) >> 3);
-              p = zq < m ? zq : m;
-              done = true;
-            }
-          }
-        }
-        const uint32_t vs = vlead + vp;
-        lds_read16(L.img, vs, eh[it]);
-        lds_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
-      }
-      const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
-      const uint32_t incl = wave_incl_scan<uint32_t>(dg);
-      const uint32_t pos = dc + incl - dg;
-      dc += __shfl(incl, 63, 64);
-      if (k < n) {
-        const uint32_t sfx = kl - p;
-        *reinterpret_cast<u32x4*>(L.erec + 4 * k) = u32x4{pos | (p << 16), (klead + kp + p) | (vl << 16), sfx, 0u};
-        // the image chunks lying wholly inside this value -> their source bytes in the staged
-        // values (every other chunk keeps ~0)
-        {
-          const uint32_t vdb = olead + pos + 14 + sfx;  // image byte of the value
-          const uint32_t srcb = vlead + vp - vdb;       // + image byte = staged byte (mod 2^32)
-          for (uint32_t cc = (vdb + 15) >> 4; 16 * cc + 16 <= vdb + vl; ++cc) L.cent[cc] = srcb + 16 * cc;
-        }
-      }
-    }
-    const uint32_t data_len = dc;
-    if (uint64_t(data_len) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
+    uint32_t ncs;
+    const uint32_t data_len = emit_phase1(a, L, B, pf, eh, et, ncs, err);
     // the level-2 loads have landed on every path (on the !has_next path there were none):
     // without this the waitcnt pass keeps them pending past the branch below and waits for
     // the next block's whole prefetch before the chunk moves reuse their registers
@@ -2004,82 +2290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       if (has_next) issue(nxt);
     }
     wave_sync();
-    // Phase 2a (ascending): image chunk -> source byte of a chunk lying wholly inside one
-    // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
-    // kEB chunk groups per batch: every LDS read of the batch is issued before its uses.
-    // (EMIT_DIRECT_CENT: the entry lanes wrote the map in phase 1)
-    wave_sync();
-    // Phase 2b (descending): move whole-value chunks to their place in the encoded block.
-    // A value only moves up (its destination follows its own header and every earlier
-    // record), so a chunk's source lies below the chunk's end: walking batches of chunks from
-    // the top, with all of a batch's reads before its writes, never overwrites a source still
-    // unread.
-    if (!(diag_mask(a.skip) & 32)) {
-      const int32_t top = int32_t((ncs + 63) & ~63u);
-      for (int32_t c0 = top; c0 > 0; c0 -= int32_t(64 * kEB)) {
-        uint32_t src[kEB];
-        u32x4 v[kEB];
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j) {
-          const int32_t c = c0 - int32_t(64 * (j + 1)) + int32_t(l);
-          src[j] = (c0 >= int32_t(64 * (j + 1)) && uint32_t(c) < ncs) ? L.cent[c] : ~0u;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j)
-          if (src[j] != ~0u) v[j] = *reinterpret_cast<const u32x4*>(L.img + src[j]);
-#pragma unroll
-        for (uint32_t j = 0; j < kEB; ++j)
-          if (src[j] != ~0u) *reinterpret_cast<u32x4*>(L.img + 16 * (c0 - int32_t(64 * (j + 1)) + int32_t(l))) = v[j];
-      }
-    }
-    wave_sync();
-    // Phase 3, entry lanes: header, key suffix, ts, value_len, and the value bytes of the
-    // partial edge chunks (from the registers captured in phase 1).
-    if (!(diag_mask(a.skip) & 16)) {
-#pragma unroll
-      for (uint32_t it = 0; it < 2; ++it) {
-        const uint32_t k = 64 * it + l;
-        if (64 * it >= n) break;
-        if (k >= n) continue;
-        const u32x4 er = *reinterpret_cast<const u32x4*>(L.erec + 4 * k);
-        const uint32_t pos = er.x & 0xFFFF, p = er.x >> 16, ks = er.y & 0xFFFF, vl = er.y >> 16, sfx = er.z;
-        const uint32_t vd = pos + 14 + sfx;
-        const uint64_t tsv = L.ts[k];
-        // unaligned LDS stores (the image is not swizzled): every field is one or two stores
-        uint8_t* o = L.img;
-        const uint32_t ox = olead + pos;
-        *reinterpret_cast<uint32_t*>(o + ox) = bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16);
-        for (uint32_t t = 0; t < sfx; t += 16) {
-          const uint32_t o2 = sfx >= 16 ? min(t, sfx - 16) : 0u;
-          uint32_t v[4];
-          lds_read16(L.kimg, ks + o2, v);
-          if (sfx >= 16) *reinterpret_cast<u32x4*>(o + ox + 4 + o2) = u32x4{v[0], v[1], v[2], v[3]};
-          else lds_st_short(o + ox + 4, sfx, v);
-        }
-        const uint64_t tbe = __builtin_bswap64(tsv);
-        *reinterpret_cast<u32x2*>(o + ox + 4 + sfx) = u32x2{uint32_t(tbe), uint32_t(tbe >> 32)};
-        *reinterpret_cast<uint16_t*>(o + ox + 12 + sfx) = uint16_t(bswap16(vl & 0xFFFF));
-        // value bytes outside whole chunks: a value of >= 16 bytes rewrites its first and last
-        // 16 (the bytes inside whole chunks are rewritten with what the move put there)
-        const uint32_t A = olead + vd;
-        if (vl >= 16) {
-          *reinterpret_cast<u32x4*>(o + A) = u32x4{eh[it][0], eh[it][1], eh[it][2], eh[it][3]};
-          *reinterpret_cast<u32x4*>(o + A + vl - 16) = u32x4{et[it][0], et[it][1], et[it][2], et[it][3]};
-        } else if (vl) {
-          lds_st_short(o + A, vl, eh[it]);
-        }
-      }
-    }
-    wave_sync();
-    // offsets table + entry count (u16 BE, `as u16`)
-    for (uint32_t k = l; k < n; k += 64)
-      *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * k) = uint16_t(bswap16(L.erec[4 * k] & 0xFFFF));
-    if (l == 0) *reinterpret_cast<uint16_t*>(L.img + olead + data_len + 2 * n) = uint16_t(bswap16(n & 0xFFFF));
-    wave_sync();
-    // flush the image: 16-B chunks; only the two end chunks can be partial
-    // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
-    if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run_masked<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
-    wave_sync();
+    emit_finish(a, L, B, data_len, ncs, eh, et);
     if (!has_next) break;
     cur = nxt;
   }
@@ -2116,7 +2327,7 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
     B.s = uni(a.blk_first[B.bi]);
     B.n = uni(a.blk_first[B.bi + 1]) - B.s;
     B.O = uni64(a.blk_off[B.bi]);
-    B.size = uni64(a.blk_off[B.bi + 1]) - B.O;
+    B.size = a.blk_sz ? uint64_t(uni(a.blk_sz[B.bi])) : uni64(a.blk_off[B.bi + 1]) - B.O;
     return true;
   };
   auto issue_l1 = [&](const BigBlk& B, uint32_t c) -> BigL1 {
@@ -2259,6 +2470,349 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
     fl = nfl;
   }
   raise_err(a.stats, err);
+}
+
+// ================================================================ encode: fused walk + emit
+// LSMBLK_ENCODE_SEG_SLOTS (per-segment output) with blocks no larger than emit's LDS image: the
+// plan walk and emit run in one launch.  Segment g's blocks go back to back to its own slot,
+//   slot(g) = (key_off[s_g] - key_off[s_0]) + (val_off[s_g] - val_off[s_0]) + 18 (s_g - s_0),
+// the bytes of every earlier segment's keys and values plus 18 per entry: an upper bound of those
+// segments' encoded size (an entry costs 2 + 2 + 8 + 2 header bytes + its 2-byte offset slot + its
+// key and value minus the shared prefix, a block 2 more for its count, and a block holds at least
+// one entry).  So no block's position depends on another segment's walk, and a block can be
+// emitted as soon as its segment's walker has found it -- the walk leaves the critical path.
+//   * Workgroups [0, walk_wgs): two walkers and their two helpers (plan_walk_kernel's waves; their
+//     rings in the workgroup's LDS).  Walker w walks segments [w spw, (w + 1) spw) one after
+//     another and publishes every block as a record of four tagged granules {first entry, end
+//     entry, output offset, size} at R(w, i) = s_(w spw) - s_0 + w + i (a walker has at most one
+//     block per entry), then its block count (wdone[w]).
+//   * The other workgroups: emit_kernel's waves.  Emitter e takes walker (e mod nwalk)'s blocks
+//     i = e / nwalk, + r, + 2 r, ... (r emitters per walker) until the walker's count says there
+//     are no more; the record of its next block is loaded while a block is emitted (landed by the
+//     landing's vmcnt(0)).
+// Emitters wait only on walkers and walkers only on their helpers, all in lower-indexed (earlier
+// dispatched) workgroups; every wait is bounded (TIMEOUT).  emit_kernel measured the same at 12
+// and 16 waves per CU, so the walkers take one of a CU's four slots.
+struct FuseArgs {
+  PlanArgs p;
+  EmitArgs e;
+  uint64_t* rec;       // uncached: 4 granules per block record
+  uint64_t* wdone;     // uncached: per walker, its block count (flag 2)
+  uint32_t* wnb;       // per walker, its block count (plain: slot_tables_kernel)
+  uint64_t* seg_out;   // per segment: slot start, encoded bytes
+  uint8_t* bigr;       // per record: the block is beyond the LDS image (emit_big_kernel)
+  uint32_t nwalk;      // walkers (2 per walker workgroup)
+  uint32_t spw;        // segments per walker
+  uint32_t walk_wgs;   // workgroups [0, walk_wgs) walk
+  uint32_t per_walker; // emitters per walker (r)
+};
+static_assert(4 * kRing * 4 + 16 <= sizeof(EmitLds) * kEmitWaves, "two walkers' rings fit emit's LDS");
+
+__device__ __forceinline__ uint32_t walker_first_seg(const FuseArgs& f, uint32_t w) {
+  return uint32_t(min(uint64_t(w) * f.spw, uint64_t(f.p.nseg)));
+}
+// Record index of walker w's first block.
+__device__ __forceinline__ uint32_t walker_rbase(const FuseArgs& f, uint32_t w) {
+  return f.p.seg_start[walker_first_seg(f, w)] - f.p.seg_start[0] + w;
+}
+
+__device__ void fuse_walk(const FuseArgs& f, uint32_t* ring) {
+  const PlanArgs& a = f.p;
+  const uint32_t l = lane_id(), wv = wave_id(), ww = wv & 1;
+  uint32_t* CR = ring + ww * kRing;
+  uint32_t* CA = ring + (2 + ww) * kRing;
+  uint32_t* prod = ring + 4 * kRing + ww;
+  uint32_t* cons = ring + 4 * kRing + 2 + ww;
+  const uint32_t w = 2 * blockIdx.x + ww;
+  const uint32_t g0 = walker_first_seg(f, w), g1 = uint32_t(min(uint64_t(g0) + f.spw, uint64_t(a.nseg)));
+  uint32_t err = 0;
+  // the walker's segments must be a non-decreasing run inside the stream (seg_start[0] = 0,
+  // seg_start[nseg] = n); otherwise neither wave walks and the call fails with SEGMENTS
+  bool ok = uni(a.seg_start[0]) == 0;
+  for (uint32_t g = g0; g < g1; ++g) {
+    const uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
+    if ((g == 0 && s0 != 0) || (g == a.nseg - 1 && uint64_t(s1) != a.n) || s0 > s1 || uint64_t(s1) > a.n) ok = false;
+  }
+  const uint32_t S0 = ok ? uni(a.seg_start[g0]) : 0u, S1 = ok ? uni(a.seg_start[g1]) : 0u;
+  const PlanKeys K = plan_keys(a);
+  if (wv >= 2) {
+    plan_produce_pipe(a, K, S0, S1, CR, CA, prod, cons, err);
+    const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
+                          (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
+    raise_err(a.stats, werr);
+    return;
+  }
+  if (!ok) err |= LSMBLK_ERR_SEGMENTS;
+  WalkRing R{CR, CA, cons, prod, S0};
+  const uint32_t rb = walker_rbase(f, w);
+  const uint64_t tagb = uint64_t(a.tag) << 2;
+  uint32_t nbw = 0;
+  uint64_t waited = 0, windows = 0;
+  // (diagnostics: per-walker realtime trace, bench.py --trace-fused)
+  uint64_t* const tr = kDiag && a.dbg && w < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(w) : nullptr;
+  if (tr && l == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t g = g0; ok && g < g1; ++g) {
+    const uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
+    const uint64_t slot = seg_slot(a.key_off, a.val_off, a.seg_start, g);
+    uint32_t nb = 0;
+    uint64_t bytes = 0;
+    walk_segment(a, K, R, s0, s1, err, nb, bytes,
+                 [&](uint32_t first, uint32_t end, uint32_t size, uint32_t i, uint64_t before) {
+                   const uint64_t v = l == 0 ? first : (l == 1 ? end : (l == 2 ? slot + before : size));
+                   if (l < 4) gstore(f.rec + 4ull * (rb + nbw + i) + l, (v << 16) | tagb | 1, a.poll);
+                 },
+                 tr, waited, windows);
+    if (l == 0) {
+      f.seg_out[2ull * g] = slot;
+      f.seg_out[2ull * g + 1] = bytes;
+    }
+    nbw += nb;
+  }
+  if (l == 0) {
+    f.wnb[w] = nbw;
+    gstore(f.wdone + w, (uint64_t(nbw) << 16) | tagb | 2, a.poll);
+    if (tr) {
+      tr[1] = __builtin_amdgcn_s_memrealtime();
+      tr[2] = waited;
+      tr[3] = windows;
+      tr[4] = nbw;
+    }
+  }
+  raise_err(a.stats, err);
+}
+
+__device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
+  const EmitArgs& a = f.e;
+  const uint32_t l = lane_id();
+  const uint32_t eidx = (blockIdx.x - f.walk_wgs) * kEmitWaves + wave_id();
+  const uint32_t w = eidx % f.nwalk, r = f.per_walker;
+  uint32_t it = eidx / f.nwalk;  // this emitter's first block of walker w
+  if (it >= r) return;           // (grid rounding)
+  // walker w's entries bound its blocks: records [rb, rb + cap) are its own
+  const uint32_t g0 = walker_first_seg(f, w), g1 = uint32_t(min(uint64_t(g0) + f.spw, uint64_t(f.p.nseg)));
+  const uint32_t S0 = uni(f.p.seg_start[g0]), S1 = uni(f.p.seg_start[g1]);
+  // (a segment table the walkers refuse -- SEGMENTS -- gives the emitters no records to poll)
+  const bool sane = uni(f.p.seg_start[0]) == 0 && S0 <= S1 && uint64_t(S1) <= f.p.n;
+  const uint32_t cap = sane ? S1 - S0 : 0u, rb = S0 + w;
+  const uint64_t want1 = (uint64_t(f.p.tag) << 2) | 1, want2 = (uint64_t(f.p.tag) << 2) | 2;
+  uint32_t err = 0;
+  const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
+  // record of block x of walker w: lanes 0-3 its granules, lane 4 the walker's block count
+  auto rec_issue = [&](uint32_t x, uint32_t pm) -> uint64_t {
+    uint64_t g = 0;
+    if (x < cap) {
+      if (l < 4) g = gload(f.rec + 4ull * (rb + x) + l, pm);
+      else if (l == 4) g = gload(f.wdone + w, pm);
+    }
+    return g;
+  };
+  uint64_t* const dbg = kDiag ? f.p.dbg : nullptr;  // (diagnostics: record-wait ticks, bench.py --trace-fused)
+  uint64_t wait_t = 0, nwait = 0, nitems = 0;
+  // 1: m is block x; 0: walker w has no block x (the emitter is done); -1: timeout
+  auto rec_resolve = [&](uint64_t g, uint32_t x, EmitMeta& m) -> int {
+    if (x >= cap) return 0;
+    const uint64_t t0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (dbg) ++nitems;
+    for (uint32_t spins = 0;; ++spins) {
+      const uint64_t okm = __ballot((l < 4 && (g & 0xFFFF) == want1) || (l == 4 && (g & 0xFFFF) == want2));
+      if ((okm & 0xF) == 0xF) {
+        m.bi = x;
+        m.s = uint32_t(lane64(g, 0) >> 16);
+        m.e = uint32_t(lane64(g, 1) >> 16);
+        m.n = m.e - m.s;
+        m.O = lane64(g, 2) >> 16;
+        m.size = lane64(g, 3) >> 16;
+        if (dbg && spins) {
+          wait_t += __builtin_amdgcn_s_memrealtime() - t0;
+          ++nwait;
+        }
+        return 1;
+      }
+      if ((okm & 0x10) && x >= uint32_t(lane64(g, 4) >> 16)) return 0;
+      if (spins > kSpinLimit) return -1;
+      __builtin_amdgcn_s_sleep(1);
+      g = rec_issue(x, f.p.poll);
+    }
+  };
+  auto meta2 = [&](EmitMeta& m) {
+    m.kb0 = uni(a.key_off[m.s]);
+    m.kb1 = uni(a.key_off[m.e]);
+    m.vb0 = uni(a.val_off[m.s]);
+    m.vb1 = uni(a.val_off[m.e]);
+  };
+  auto is_fast = [&](const EmitMeta& m) {
+    const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
+    return m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
+           vlead + (m.vb1 - m.vb0) + 24 <= kEmitICap && uint32_t(m.O & 15) + m.size + 8 <= kEmitICap;
+  };
+  u32x4 kq[2], vq[5];
+  EmitPf pf;
+  auto issue = [&](const EmitMeta& m) {  // staging + first-chunk entry loads of block m
+    const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
+    const rsrc_t RK = make_rsrc(a.keys + m.kb0 - klead, klead + (m.kb1 - m.kb0));
+    const uint32_t nk = (klead + (m.kb1 - m.kb0) + 15) >> 4;
+    const rsrc_t RV = make_rsrc(a.vals + m.vb0 - vlead, vlead + (m.vb1 - m.vb0));
+    const uint32_t nv = (vlead + (m.vb1 - m.vb0) + 15) >> 4;
+#pragma unroll
+    for (uint32_t i = 0; i < 2; ++i)
+      if (l + 64 * i < nk) kq[i] = __builtin_amdgcn_raw_buffer_load_b128(RK, (l + 64 * i) * 16, 0, kLdAux);
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+      if (l + 64 * i < nv) vq[i] = __builtin_amdgcn_raw_buffer_load_b128(RV, (l + 64 * i) * 16, 0, kLdAux);
+    if (l < m.n) {
+      pf.ko0 = a.key_off[m.s + l];
+      pf.ko1 = a.key_off[m.s + l + 1];
+      pf.vo0 = a.val_off[m.s + l];
+      pf.vo1 = a.val_off[m.s + l + 1];
+      pf.ts = a.ts[m.s + l];
+    }
+  };
+  // from block x on (x advanced), the first on the fast path; the others are flagged for
+  // emit_big_kernel.  Waits for each record (before the loop, and after a flagged block).
+  auto find_fast = [&](uint32_t& x, EmitMeta& m) -> bool {
+    for (;; x += r) {
+      const int st = rec_resolve(rec_issue(x, 0), x, m);
+      if (st <= 0) {
+        if (st < 0) err |= LSMBLK_ERR_TIMEOUT;
+        return false;
+      }
+      meta2(m);
+      if (is_fast(m)) return true;
+      if (l == 0) f.bigr[rb + x] = 1;
+    }
+  };
+  EmitMeta cur;
+  if (!find_fast(it, cur)) {
+    raise_err(a.stats, err);
+    return;
+  }
+  issue(cur);
+  uint32_t in = it + r;        // the next block: its record loads in flight
+  uint64_t pg = rec_issue(in, 0);
+  for (;;) {
+    const uint32_t s = cur.s, n = cur.n;
+    const uint64_t O = cur.O, size = cur.size;
+    const uint32_t kb0 = cur.kb0, kb1 = cur.kb1, vb0 = cur.vb0, vb1 = cur.vb1;
+    const uint32_t klead = uint32_t((kaddr + kb0) & 15), vlead = uint32_t((vaddr + vb0) & 15);
+    const uint32_t olead = uint32_t(O & 15);
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(pf.ko1) - kb0;
+    {  // land the staged keys (plain) and values (block image at vlead)
+      const uint32_t nk = (klead + (kb1 - kb0) + 15) >> 4;
+      const uint32_t nv = (vlead + (vb1 - vb0) + 15) >> 4;
+#pragma unroll
+      for (uint32_t i = 0; i < 2; ++i)
+        if (l + 64 * i < nk) *reinterpret_cast<u32x4*>(L.kimg + (l + 64 * i) * 16) = kq[i];
+#pragma unroll
+      for (uint32_t i = 0; i < 5; ++i)
+        if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = vq[i];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): the staging and the next record
+    EmitMeta nxt;
+    const int st = rec_resolve(pg, in, nxt);
+    bool has_next = st > 0;
+    if (st < 0) err |= LSMBLK_ERR_TIMEOUT;
+    uint32_t r_kb0 = 0, r_kb1 = 0, r_vb0 = 0, r_vb1 = 0;
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) {
+      r_kb0 = a.key_off[nxt.s];
+      r_kb1 = a.key_off[nxt.e];
+      r_vb0 = a.val_off[nxt.s];
+      r_vb1 = a.val_off[nxt.e];
+    }
+    wave_sync();
+    const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl};
+    uint32_t eh[2][4], et[2][4];
+    uint32_t ncs;
+    const uint32_t data_len = emit_phase1(a, L, B, pf, eh, et, ncs, err);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
+    if (has_next) {
+      nxt.kb0 = uni(r_kb0);
+      nxt.kb1 = uni(r_kb1);
+      nxt.vb0 = uni(r_vb0);
+      nxt.vb1 = uni(r_vb1);
+      if (!is_fast(nxt)) {
+        if (l == 0) f.bigr[rb + in] = 1;
+        in += r;
+        has_next = find_fast(in, nxt);
+      }
+      if (has_next) {
+        issue(nxt);
+        in += r;
+        pg = rec_issue(in, 0);
+      }
+    }
+    wave_sync();
+    emit_finish(a, L, B, data_len, ncs, eh, et);
+    if (!has_next) break;
+    cur = nxt;
+  }
+  if (dbg && l == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(dbg + 0), (unsigned long long)wait_t);
+    atomicAdd(reinterpret_cast<unsigned long long*>(dbg + 1), (unsigned long long)nwait);
+    atomicAdd(reinterpret_cast<unsigned long long*>(dbg + 2), (unsigned long long)nitems);
+    atomicMax(reinterpret_cast<unsigned long long*>(dbg + 3), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+  raise_err(a.stats, err);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_fused_kernel(FuseArgs f) {
+  __shared__ EmitLds lds[kEmitWaves];
+  if (blockIdx.x < f.walk_wgs) {
+    // the walk is the serial part: its waves win the issue arbitration against the emitters
+    // sharing their SIMDs
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t* ring = reinterpret_cast<uint32_t*>(lds);
+    if (threadIdx.x < 4) ring[4 * kRing + threadIdx.x] = 0;  // the hand-off counters
+    __syncthreads();
+    fuse_walk(f, ring);
+  } else {
+    fuse_emit(f, lds[threadIdx.x >> 6]);
+  }
+}
+
+// After encode_fused_kernel: the dense block tables of the slot output -- blk_first, blk_off (every
+// block's position), blk_sz, the big-block flags -- stats[0] / [1], and the capacity checks.
+// Workgroup w takes walker w's blocks: dense indices B_w + i (a walker's segments are consecutive).
+// blk_off[nblk] = the end of the last segment's data.
+__global__ __launch_bounds__(256) void slot_tables_kernel(FuseArgs f, uint32_t* blk_first, uint32_t* blk_sz,
+                                                          uint8_t* big_flag, uint64_t* blk_off, uint64_t blk_cap,
+                                                          uint64_t out_cap) {
+  __shared__ uint64_t part[4];
+  const uint32_t w = blockIdx.x, tid = threadIdx.x, l = lane_id();
+  uint64_t acc = 0;
+  for (uint32_t v = tid; v < w; v += 256) acc += f.wnb[v];
+  acc = wave_sum<uint64_t>(acc);
+  if (l == 0) part[tid >> 6] = acc;
+  __syncthreads();
+  const uint64_t B = part[0] + part[1] + part[2] + part[3];
+  const uint32_t nb = f.wnb[w], rb = walker_rbase(f, w);
+  for (uint32_t i = tid; i < nb; i += 256) {
+    const uint64_t* g = f.rec + 4ull * (rb + i);
+    const uint64_t bi = B + i;
+    blk_first[bi] = uint32_t(g[0] >> 16);
+    blk_sz[bi] = uint32_t(g[3] >> 16);
+    big_flag[bi] = f.bigr[rb + i];
+    f.bigr[rb + i] = 0;
+    if (bi < blk_cap) blk_off[bi] = g[2] >> 16;
+  }
+  if (tid == 0) {
+    uint32_t err = 0;
+    uint64_t bytes = 0;
+    const uint32_t g0 = walker_first_seg(f, w), g1 = uint32_t(min(uint64_t(g0) + f.spw, uint64_t(f.p.nseg)));
+    for (uint32_t g = g0; g < g1; ++g) {
+      bytes += f.seg_out[2ull * g + 1];
+      if (f.seg_out[2ull * g] + f.seg_out[2ull * g + 1] > out_cap) err |= LSMBLK_ERR_CAPACITY;
+    }
+    if (bytes) atomicAdd(reinterpret_cast<unsigned long long*>(f.p.stats + 1), (unsigned long long)bytes);
+    if (w == f.nwalk - 1) {
+      const uint64_t nblk = B + nb, gl = f.p.nseg - 1;
+      blk_first[nblk] = uint32_t(f.p.n);
+      if (nblk < blk_cap) blk_off[nblk] = f.seg_out[2 * gl] + f.seg_out[2 * gl + 1];
+      f.p.stats[0] = nblk;
+      if (nblk + 1 > blk_cap) err |= LSMBLK_ERR_CAPACITY;
+    }
+    if (err) atomicOr(reinterpret_cast<unsigned long long*>(f.p.stats + 3), (unsigned long long)err);
+  }
 }
 
 // read_block's check (src/table.rs:226-230): the BE u32 after every block must equal the
@@ -3172,6 +3726,8 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
     if ((rc = grow(&c->ent, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
     if ((rc = grow(&c->big_list, &cap, entries + 1, 1))) return rc;
+    cap = c->rec_cap;
+    if ((rc = grow(&c->blk_sz, &cap, entries + 1, 1))) return rc;
     c->rec_cap = cap;
   }
   return LSMBLK_OK;
@@ -3187,6 +3743,8 @@ int next_epoch(lsmblk_ctx* c, hipStream_t st) {
     if (c->lag_blk_cap) {
       if (hipMemsetAsync(c->lag_gran, 0, lag_words(c->lag_blk_cap) * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     }
+    if (c->frec_cap && hipMemsetAsync(c->frec, 0, c->frec_cap * 4 * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    if (c->fdone_cap && hipMemsetAsync(c->fdone, 0, c->fdone_cap * 8, st) != hipSuccess) return LSMBLK_E_HIP;
     c->epoch = 0;
   }
   ++c->epoch;
@@ -3229,6 +3787,11 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   (void)hipFree(c->rec_first);
   (void)hipFree(c->ent);
   (void)hipFree(c->big_list);
+  (void)hipFree(c->blk_sz);
+  (void)hipFree(c->frec);
+  (void)hipFree(c->fdone);
+  (void)hipFree(c->fwnb);
+  (void)hipFree(c->fbig);
   (void)hipFree(c->blk_first);
   (void)hipFree(c->crc_tabs);
   (void)hipFree(c->meta_rec);
@@ -3279,6 +3842,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
   } else if (key == LSMBLK_DEBUG_DECODE_LAG && value >= 2 * kTile && value <= (1u << 24)) {
     c->dec_lag = value;
     c->dec_lag_bytes = 0;  // exactly this lag (experiments)
+  } else if (key == LSMBLK_DEBUG_ENCODE_UNFUSED) {
+    c->fuse_off = value != 0;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->timing) c->klog_n = 0;  // the log restarts with the timing
     c->timing = value != 0;
@@ -3487,14 +4052,22 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
 int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* seg_start, uint32_t nseg,
                         uint32_t block_size, uint8_t* out, uint64_t out_cap, uint64_t* blk_off, uint64_t blk_cap,
                         uint64_t* stats, void* stream) {
+  return lsmblk_encode_batch_ex(c, in, seg_start, nseg, block_size, 0, out, out_cap, blk_off, blk_cap, nullptr, stats,
+                                stream);
+}
+
+int lsmblk_encode_batch_ex(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_t* seg_start, uint32_t nseg,
+                           uint32_t block_size, uint32_t flags, uint8_t* out, uint64_t out_cap, uint64_t* blk_off,
+                           uint64_t blk_cap, uint64_t* seg_out, uint64_t* stats, void* stream) {
   if (!c || !in || !seg_start || !blk_off || !stats || !aligned16(out)) return LSMBLK_E_INVAL;
   if (in->n >= 0xFFFFFFFFull || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
-  if (block_size == 0) return LSMBLK_E_INVAL;
+  if (block_size == 0 || (flags & ~uint32_t(LSMBLK_ENCODE_SEG_SLOTS))) return LSMBLK_E_INVAL;
+  if ((flags & LSMBLK_ENCODE_SEG_SLOTS) && !seg_out) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   return lsmblk_impl::encode_locked(c, in, nullptr, seg_start, nullptr, nseg, block_size, out, out_cap, blk_off,
-                                    blk_cap, stats, reinterpret_cast<hipStream_t>(stream));
+                                    blk_cap, stats, reinterpret_cast<hipStream_t>(stream), false, flags, seg_out);
 }
 
 }  // extern "C"
@@ -3502,8 +4075,11 @@ int lsmblk_encode_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
 namespace lsmblk_impl {
 int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn, const uint32_t* seg_start,
                   const uint32_t* dnseg, uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
-                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span) {
+                  uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, hipStream_t st, bool span, uint32_t flags,
+                  uint64_t* seg_out) {
   const KLogRange lr(c, &c->enc_log0, &c->enc_log1);
+  const bool slots = (flags & LSMBLK_ENCODE_SEG_SLOTS) != 0;
+  if (slots && (!seg_out || span || dn || dnseg)) return LSMBLK_E_INVAL;
   // in->n (and nseg) are upper bounds when dn (dnseg) point at the device-side values
   int rc = reserve_locked(c, 0, in->n, nseg);
   if (rc) return rc;
@@ -3513,6 +4089,23 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
     if (in->n != 0) return LSMBLK_E_INVAL;
     if (blk_cap >= 1 && hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
     return LSMBLK_OK;
+  }
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  // the fused walk + emit: per-segment slots, blocks no larger than emit's LDS image
+  const bool fused = slots && block_size <= 4096 && !c->fuse_off;
+  uint32_t walk_wgs = 0, nwalk = 0;
+  if (fused) {
+    walk_wgs = uint32_t(std::min<uint64_t>(uint64_t(cus), (uint64_t(nseg) + 1) / 2));
+    walk_wgs += walk_wgs & 1;  // walkers a multiple of 4: emitters split evenly over them
+    nwalk = 2 * walk_wgs;
+    const uint64_t recs = in->n + nwalk + 1;
+    const uint64_t fc = c->frec_cap, dc = c->fdone_cap;
+    if ((rc = grow(&c->frec, &c->frec_cap, recs, 4, kStatusFlags))) return rc;
+    if ((rc = grow(&c->fdone, &c->fdone_cap, nwalk, 1, kStatusFlags))) return rc;
+    if ((rc = grow(&c->fwnb, &c->fwnb_cap, nwalk, 1))) return rc;
+    if ((rc = grow(&c->fbig, &c->fbig_cap, recs, 1))) return rc;
+    if (c->frec_cap != fc || c->fdone_cap != dc) c->epoch = 0;  // fresh granules: a new epoch sequence
   }
   if ((rc = next_epoch(c, st))) return rc;
   if (hipMemsetAsync(c->counters, 0, 2048, st) != hipSuccess) return LSMBLK_E_HIP;
@@ -3541,16 +4134,8 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.span = span ? 1u : 0u;
   p.skip = c->skip;
   p.dbg = c->dbg_on ? c->dbg : nullptr;
-  if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
-  LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), 0, st, p);
-  if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
-    return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
-  }
-  // the big-block flags are cleared before emit (the start of emit_kernel to the end of
-  // emit_big_kernel is what bench.py's roofline divides by)
-  const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;  // blocks <= entries, <= blk_cap
-  if (nblk_max && hipMemsetAsync(c->big_list, 0, nblk_max, st) != hipSuccess) return LSMBLK_E_HIP;
-  if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
+  p.seg_out = slots ? seg_out : nullptr;
+  p.blk_sz = slots ? c->blk_sz : nullptr;
   EmitArgs e;
   e.keys = in->keys;
   e.key_off = in->key_off;
@@ -3565,15 +4150,45 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   e.n = in->n;
   e.stats = stats;
   e.big_flag = reinterpret_cast<uint8_t*>(c->big_list);
+  e.blk_sz = slots ? c->blk_sz : nullptr;
   e.skip = c->skip;
   e.dn = dn;
-  int cus = 256;
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
-    per_cu = 3;
-  const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
-  LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  if (fused) {
+    if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    FuseArgs f;
+    f.p = p;
+    f.e = e;
+    f.rec = c->frec;
+    f.wdone = c->fdone;
+    f.wnb = c->fwnb;
+    f.seg_out = seg_out;
+    f.bigr = c->fbig;
+    f.nwalk = nwalk;
+    f.spw = uint32_t((uint64_t(nseg) + nwalk - 1) / nwalk);
+    f.walk_wgs = walk_wgs;
+    // three emit workgroups per CU beside the walkers' one, split evenly over the walkers
+    f.per_walker = std::max<uint32_t>(1u, uint32_t(3ull * kEmitWaves * uint64_t(cus) / nwalk));
+    const uint32_t emit_wgs = f.per_walker * nwalk / kEmitWaves;
+    LSM_LAUNCH_SLOT(4, encode_fused_kernel, dim3(walk_wgs + emit_wgs), dim3(256), 0, st, f);
+    LSM_LAUNCH(slot_tables_kernel, dim3(nwalk), dim3(256), 0, st, f, c->blk_first, c->blk_sz,
+               reinterpret_cast<uint8_t*>(c->big_list), blk_off, blk_cap, out_cap);
+  } else {
+    if (p.dbg && hipMemsetAsync(p.dbg, 0, kDbgWords * 8, st) != hipSuccess) return LSMBLK_E_HIP;
+    LSM_LAUNCH_SLOT(3, plan_walk_kernel, dim3((nseg + 3) / 4), dim3(kWalkThreads), 0, st, p);
+    if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
+      return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+    }
+    // the big-block flags are cleared before emit (the start of emit_kernel to the end of
+    // emit_big_kernel is what bench.py's roofline divides by)
+    const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;  // blocks <= entries, <= blk_cap
+    if (nblk_max && hipMemsetAsync(c->big_list, 0, nblk_max, st) != hipSuccess) return LSMBLK_E_HIP;
+    if (hipGetLastError() != hipSuccess) return LSMBLK_E_HIP;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_kernel, 256, 0) != hipSuccess || per_cu < 1)
+      per_cu = 3;
+    const uint32_t grid = uint32_t(cus) * uint32_t(per_cu);
+    LSM_LAUNCH_SLOT(4, emit_kernel, dim3(grid), dim3(256), 0, st, e);
+  }
   // (every workgroup resident at once: the flagged blocks are strided over the whole grid)
   int big_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&big_cu, emit_big_kernel, 256, 0) != hipSuccess || big_cu < 1)

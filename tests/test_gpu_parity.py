@@ -44,8 +44,37 @@ def assert_kv_equal(dkv: batch.KVStream, ref: O.KV):
     np.testing.assert_array_equal(vals, ref.vals[:ref.val_off[-1]])
 
 
+def seg_slots(kv: O.KV, seg):
+    """slot(s) of LSMBLK_ENCODE_SEG_SLOTS (include/lsmblk.h), in numpy."""
+    s = np.asarray(seg, dtype=np.int64)
+    ko, vo = kv.key_off.astype(np.int64), kv.val_off.astype(np.int64)
+    return (ko[s[:-1]] - ko[s[0]]) + (vo[s[:-1]] - vo[s[0]]) + 18 * (s[:-1] - s[0])
+
+
+def slot_check(kv: O.KV, seg, block_size, ref_blocks, ref_off):
+    """LSMBLK_ENCODE_SEG_SLOTS through the fused walk + emit launch and through plan_walk + emit
+    (LSMBLK_DEBUG_ENCODE_UNFUSED): every segment at its slot, the segments packed == the oracle's
+    blocks and offsets."""
+    from lsm_amd._lib import LSMBLK_DEBUG_ENCODE_UNFUSED, lib
+    ctx = batch._ctx(0)
+    for unfused in (0, 1):
+        assert lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_UNFUSED, unfused) == 0
+        try:
+            out, off, so = batch.encode_kv_slots(to_dev(kv), seg, block_size)
+        finally:
+            lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_UNFUSED, 0)
+        np.testing.assert_array_equal(so[:, 0].cpu().numpy(), seg_slots(kv, seg))
+        blocks, poff = batch.slots_to_packed(out, off, so)
+        np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), ref_off)
+        got = blocks.cpu().numpy()
+        assert len(got) == len(ref_blocks)
+        mism = np.flatnonzero(got != ref_blocks)
+        assert mism.size == 0, f"slots (unfused={unfused}): first mismatching byte {mism[:8]} of {len(got)}"
+
+
 def roundtrip_check(kv: O.KV, seg, block_size, shift=0):
-    """GPU encode == oracle encode; GPU decode(oracle blocks) == oracle decode."""
+    """GPU encode == oracle encode (packed, and per-segment slots); GPU decode(oracle blocks) ==
+    oracle decode."""
     rc, ref_blocks, ref_off = O.encode_segments(kv, seg, block_size)
     assert rc == 0
     blocks, blk_off = batch.encode_kv(to_dev(kv), seg, block_size)
@@ -55,6 +84,7 @@ def roundtrip_check(kv: O.KV, seg, block_size, shift=0):
     assert len(got) == len(ref_blocks)
     mism = np.flatnonzero(got != ref_blocks)
     assert mism.size == 0, f"first mismatching byte {mism[:8]} of {len(got)}"
+    slot_check(kv, seg, block_size, ref_blocks, ref_off)
     rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
     assert rc == 0
     db, do = dev_blocks(ref_blocks, ref_off, shift)
@@ -660,3 +690,59 @@ def test_decode_lag_setting_bounds():
     assert lib().lsmblk_debug_set(ctx, 4, (1 << 24) + 1) != 0
     assert lib().lsmblk_debug_set(ctx, 4, 10240) == 0
     assert lib().lsmblk_debug_set(ctx, 4, 0) == 0  # the default (scaled by the block size)
+
+
+@pytest.mark.parametrize("cfg,n,seg_bytes", [("U", 400_000, 2 << 20), ("Z", 400_000, 2 << 20), ("U", 200_000, 64 << 10),
+                                             ("M", 30_000, 8 << 20)])
+def test_slot_encode_large_matches_packed_and_writes_only_its_segments(cfg, n, seg_bytes):
+    """LSMBLK_ENCODE_SEG_SLOTS at sizes where the fused launch has many walkers, several segments
+    per walker and every emitter busy (and M's big blocks through emit_big_kernel): the packed
+    segments equal lsmblk_encode_batch's output, nothing between the segments is written, the
+    stats and blk_off[nblk] follow the header, and a second call (next epoch) gives the same."""
+    kv = O.KV(*synth.GENERATORS[cfg](n, seed=33))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, seg_bytes)
+    bs = synth.BLOCK_SIZE[cfg]
+    d = to_dev(kv)
+    blocks, blk_off = batch.encode_kv(d, seg, bs)
+    kb, vb = d.byte_sizes()
+    out_cap, blk_cap = batch.encode_bound(d, kb, vb)
+    nseg = len(seg) - 1
+    seg_t = torch.from_numpy(np.asarray(seg, np.uint32).view(np.int32)).cuda()
+    for rep in range(2):
+        out = batch._aligned_empty(out_cap, "cuda")
+        out.fill_(0xA5)
+        off = torch.zeros(blk_cap, dtype=torch.int64, device="cuda")
+        so = torch.full((2 * nseg,), -1, dtype=torch.int64, device="cuda")
+        st = torch.zeros(4, dtype=torch.int64, device="cuda")
+        batch.encode_into(d, seg_t, nseg, bs, out, out_cap, off, blk_cap, st, seg_out=so)
+        torch.cuda.synchronize()
+        nblk, nbytes, _, err = st.cpu().tolist()
+        assert err == 0 and nblk == blk_off.numel() - 1 and nbytes == blocks.numel()
+        so2 = so.view(-1, 2)
+        np.testing.assert_array_equal(so2[:, 0].cpu().numpy(), seg_slots(kv, seg))
+        assert int(off[nblk].item()) == int(so2[-1, 0].item() + so2[-1, 1].item())
+        pb, po = batch.slots_to_packed(out, off[:nblk + 1], so)
+        assert torch.equal(po, blk_off) and torch.equal(pb, blocks), f"rep {rep}"
+        untouched = torch.ones(out_cap, dtype=torch.bool, device="cuda")
+        for a, b in so2.cpu().tolist():
+            untouched[a:a + b] = False
+        assert bool((out[untouched] == 0xA5).all())
+
+
+def test_slot_encode_refuses_missing_seg_out_and_bad_flags():
+    from lsm_amd._lib import lib
+    import ctypes
+    kv = O.KV(*synth.gen_uniform(1000, seed=1))
+    d = to_dev(kv)
+    c = d._c()
+    seg_t = torch.tensor([0, kv.n], dtype=torch.int32, device="cuda")
+    out = batch._aligned_empty(1 << 20, "cuda")
+    off = torch.zeros(kv.n + 2, dtype=torch.int64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ctx = batch._ctx(0)
+    f = lib().lsmblk_encode_batch_ex
+    assert f(ctx, ctypes.byref(c), seg_t.data_ptr(), 1, 4096, 1, out.data_ptr(), 1 << 20, off.data_ptr(), kv.n + 2,
+             None, st.data_ptr(), None) != 0
+    so = torch.zeros(2, dtype=torch.int64, device="cuda")
+    assert f(ctx, ctypes.byref(c), seg_t.data_ptr(), 1, 4096, 2, out.data_ptr(), 1 << 20, off.data_ptr(), kv.n + 2,
+             so.data_ptr(), st.data_ptr(), None) != 0

@@ -1,6 +1,9 @@
 """Checks on the gfx950 ISA of the inline-asm sites of a kernel (or of every kernel with --all):
-  * no instruction reads or writes the registers of inline-asm loads between the loads and an
-    inline-asm `s_waitcnt vmcnt` (CFG reachability): the waitcnt pass does not see asm loads;
+  * no instruction reads or writes the registers an inline-asm load writes before a wait that
+    covers the load (CFG reachability): the waitcnt pass does not see asm loads.  An `s_waitcnt
+    vmcnt(N)` covers a load when at least N vector-memory instructions follow the load on the path
+    to it (returns come in issue order), so software-pipelined sites -- loads for the next step
+    still in flight across a wait for this step's -- are checked load by load;
   * no VALU write of an SGPR that an inline-asm vector-memory instruction reads comes within 5 wait
     states of it (the compiler's hazard recognizer does not look inside inline asm);
   * every inline-asm instruction is of a kind these checks cover (vector loads, `s_waitcnt`,
@@ -79,7 +82,7 @@ def check(s, kname):
             r.add(int(m.group(1)))
         return r
 
-    asm_loads, asm_waits, asm_any, unknown = [], set(), set(), []
+    asm_loads, asm_waits, asm_any, unknown = [], {}, set(), []
     inside = False
     for k, l in enumerate(body):
         if ';;#ASMSTART' in l:
@@ -97,37 +100,47 @@ def check(s, kname):
             if t.startswith('buffer_load') or t.startswith('global_load'):
                 asm_loads.append(k)
             if t.startswith('s_waitcnt') and 'vmcnt' in t:
-                asm_waits.add(k)
+                asm_waits[k] = t
+    # every vmcnt wait (asm or compiler) with its count
+    vwait = {}
+    for k, l in enumerate(body):
+        m = re.match(r'\s*s_waitcnt\b.*\bvmcnt\((\d+)\)', l)
+        if m:
+            vwait[k] = int(m.group(1))
+    vmem = re.compile(r'\s*(buffer|global|flat|scratch)_(load|store|atomic)')
     regs = set()
     for k in asm_loads:
         regs |= regs_in(body[k].split(',')[0])
     bad = len(unknown)
     for k0 in asm_loads:
+        own = regs_in(body[k0].split(',')[0])
         seen = set()
-        stack = [(blk_of[k0], k0 + 1)]
+        stack = [(blk_of[k0], k0 + 1, 0)]
         while stack:
-            bi, startk = stack.pop()
-            if (bi, startk) in seen:
+            bi, startk, cnt = stack.pop()
+            if (bi, startk, cnt) in seen:
                 continue
-            seen.add((bi, startk))
+            seen.add((bi, startk, cnt))
             stop = False
             for k in blocks[bi]:
                 if k < startk:
                     continue
                 t = body[k].strip()
-                if k in asm_waits:
-                    stop = True
+                if k in vwait and cnt >= vwait[k]:
+                    stop = True  # the load has landed
                     break
+                if vmem.match(body[k]):
+                    cnt = min(cnt + 1, 64)
                 if not t or t.startswith(';') or t.startswith('.') or k in asm_any:
                     continue
-                u = regs_in(t) & regs
+                u = regs_in(t) & own
                 if u:
                     bad += 1
                     if bad <= 20:
                         print(f"line {k}: {sorted(u)} {t[:100]}  (after asm load line {k0})")
             if not stop:
                 for sb in succs(bi):
-                    stack.append((sb, blocks[sb][0]))
+                    stack.append((sb, blocks[sb][0], cnt))
     # gfx9 hazard: a VALU write of an SGPR that a VMEM instruction reads needs 5 wait states; the
     # compiler's hazard recognizer may not look inside inline asm
     def sregs(t):
