@@ -76,10 +76,9 @@ def parse(argv=None):
                    help="diagnostics: in --dry-run, this rank raises inside compact_dist (the N>1 extra's path)")
     p.add_argument("--dry-run-fail-rank", type=int, default=None,
                    help="launcher self-test: this rank exits with status 3 before joining the group")
-    p.add_argument("--encode-mode", default="packed", choices=["slots", "packed", "slots-unfused"],
-                   help="re-encode output: per-segment slots (LSMBLK_ENCODE_SEG_SLOTS, the plan walk fused "
-                        "with emit), all segments packed (lsmblk_encode_batch), or slots through the separate "
-                        "plan walk + emit launches (A/B)")
+    p.add_argument("--encode-mode", default="packed", choices=["packed", "slots", "slots-fused"],
+                   help="re-encode output: all segments packed (lsmblk_encode_batch), per-segment slots "
+                        "(LSMBLK_ENCODE_SEG_SLOTS), or slots through the fused walk + emit launch (A/B)")
     p.add_argument("--decode-two-pass", action="store_true",
                    help="diagnostics (A/B): count + tile scan + decode (three launches) instead of the lagged decode")
     p.add_argument("--decode-lag", type=int, default=None,
@@ -224,7 +223,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     ctx = batch._ctx(local, stream)
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
     check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
-    check(lib().lsmblk_debug_set(ctx, 8, 1 if args.encode_mode == "slots-unfused" else 0))
+    check(lib().lsmblk_debug_set(ctx, 8, 1 if args.encode_mode == "slots-fused" or args.trace_fused else 0))
     if args.decode_lag is not None:
         check(lib().lsmblk_debug_set(ctx, 4, args.decode_lag))
 
@@ -355,9 +354,9 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
                    "blocks_per_gpu": nblk, "entries_per_gpu": n, "encoded_bytes_per_gpu": E,
                    "decoded_bytes_per_gpu": D, "block_size": bs, "segments_per_gpu": len(seg) - 1,
                    "parallelism": f"block-sharded x{world} (no data-path collective)",
-                   "encode_output": {"slots": "per-segment slots (LSMBLK_ENCODE_SEG_SLOTS; walk fused with emit)",
-                                     "packed": "segments packed (lsmblk_encode_batch)",
-                                     "slots-unfused": "per-segment slots, separate walk + emit launches"}[args.encode_mode],
+                   "encode_output": {"packed": "segments packed (lsmblk_encode_batch)",
+                                     "slots": "per-segment slots (LSMBLK_ENCODE_SEG_SLOTS)",
+                                     "slots-fused": "per-segment slots, fused walk + emit launch"}[args.encode_mode],
                    "rccl_world": world, "roundtrip_bit_exact": bool(ok_all),
                    "oracle_checked_blocks": int(checked_all)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

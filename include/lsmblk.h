@@ -172,8 +172,9 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
 #define LSMBLK_DEBUG_ROT_POISON 7 /* diagnostics builds only (fault injection): 1 = the SST rotation's block-chain levels
                                      get links that do not advance (J(s) = s, S(s) = 0) over a third of the
                                      stream; the rotation must report LSMBLK_E_INTERNAL, never loop */
-#define LSMBLK_DEBUG_ENCODE_UNFUSED 8 /* 1: LSMBLK_ENCODE_SEG_SLOTS through the separate plan walk and emit
-                                         launches instead of the fused one (A/B) */
+#define LSMBLK_DEBUG_ENCODE_FUSED 8 /* 1: LSMBLK_ENCODE_SEG_SLOTS with block_size <= 4096 through one launch
+                                       that walks and emits at once (encode_fused_kernel; measured slower
+                                       than the plan walk + emit launches) */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* The trace of the last lagged decode with LSMBLK_DEBUG_COUNTERS on (n <= 16 + 8 * 32768 words;
  * synchronizes).  Words 16 + 8 t + k, 100 MHz s_memrealtime stamps of 64-block tile t: k = 0 tile
@@ -230,9 +231,8 @@ int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint3
  *   slot(s) = (key_off[seg_start[s]] - key_off[seg_start[0]]) + (val_off[seg_start[s]] -
  *             val_off[seg_start[0]]) + 18 * (seg_start[s] - seg_start[0]),
  * an upper bound of the encoded size of the segments before s, so out_cap >= key bytes + value
- * bytes + 18 * n always suffices.  No segment's placement then waits for another segment's block
- * walk: with block_size <= 4096 the walk and the block writes run in one launch.  The block bytes
- * are the same as lsmblk_encode_batch's.  seg_out (u64[2 * nseg], required): [2 s] = slot(s),
+ * bytes + 18 * n always suffices, and every SST's place is known before the encode runs.  The
+ * block bytes are the same as lsmblk_encode_batch's.  seg_out (u64[2 * nseg], required): [2 s] = slot(s),
  * [2 s + 1] = segment s's encoded bytes.  blk_off[b] = where block b starts; a block ends where the
  * next starts unless it is its segment's last (then at seg_out[2 s] + seg_out[2 s + 1]);
  * blk_off[nblk] = the end of the last segment.  stats[1] = the encoded bytes (their sum). */

@@ -2473,8 +2473,11 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
 }
 
 // ================================================================ encode: fused walk + emit
-// LSMBLK_ENCODE_SEG_SLOTS (per-segment output) with blocks no larger than emit's LDS image: the
-// plan walk and emit run in one launch.  Segment g's blocks go back to back to its own slot,
+// LSMBLK_ENCODE_SEG_SLOTS (per-segment output) with blocks no larger than emit's LDS image, under
+// LSMBLK_DEBUG_ENCODE_FUSED: the plan walk and emit run in one launch.  Measured (DESIGN.md section
+// 8): correct, but 2.16-2.18 ms against 2.08 for the two launches at U -- the walkers finish at 1.2
+// ms and the emitters almost never wait for a record, yet emit slows by the walk's instructions,
+// which need the same SIMD issue slots (both are issue-bound).  Segment g's blocks go back to back to its own slot,
 //   slot(g) = (key_off[s_g] - key_off[s_0]) + (val_off[s_g] - val_off[s_0]) + 18 (s_g - s_0),
 // the bytes of every earlier segment's keys and values plus 18 per entry: an upper bound of those
 // segments' encoded size (an entry costs 2 + 2 + 8 + 2 header bytes + its 2-byte offset slot + its
@@ -2597,13 +2600,22 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
   const uint64_t want1 = (uint64_t(f.p.tag) << 2) | 1, want2 = (uint64_t(f.p.tag) << 2) | 2;
   uint32_t err = 0;
   const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
-  // record of block x of walker w: lanes 0-3 its granules, lane 4 the walker's block count
-  auto rec_issue = [&](uint32_t x, uint32_t pm) -> uint64_t {
-    uint64_t g = 0;
-    if (x < cap) {
-      if (l < 4) g = gload(f.rec + 4ull * (rb + x) + l, pm);
-      else if (l == 4) g = gload(f.wdone + w, pm);
-    }
+  // The record of block x of walker w: lanes 0-3 its granules, the others the walker's block count
+  // (agent-coherent sc1 loads of uncached memory, as gload).  Every record load is inline asm: the
+  // in-loop prefetch (the block after next) is landed by the landing's explicit vmcnt(0), the
+  // others by their own wait.  Issued as compiler loads, their destinations stayed "pending" for
+  // the waitcnt pass into the block's LDS loops, which then began with vmcnt(0) -- draining the
+  // next block's staging loads (2.5 ms against emit_kernel's 1.7).
+  auto rec_issue_asm = [&](uint32_t x) -> uint64_t {
+    const uint64_t* p = x < cap && l < 4 ? f.rec + 4ull * (rb + x) + l : f.wdone + w;
+    uint64_t g;
+    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(g) : "v"(p));
+    return g;
+  };
+  auto rec_poll = [&](uint32_t x) -> uint64_t {
+    uint64_t g = rec_issue_asm(x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(g));
     return g;
   };
   uint64_t* const dbg = kDiag ? f.p.dbg : nullptr;  // (diagnostics: record-wait ticks, bench.py --trace-fused)
@@ -2631,7 +2643,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
       if ((okm & 0x10) && x >= uint32_t(lane64(g, 4) >> 16)) return 0;
       if (spins > kSpinLimit) return -1;
       __builtin_amdgcn_s_sleep(1);
-      g = rec_issue(x, f.p.poll);
+      g = rec_poll(x);
     }
   };
   auto meta2 = [&](EmitMeta& m) {
@@ -2671,7 +2683,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
   // emit_big_kernel.  Waits for each record (before the loop, and after a flagged block).
   auto find_fast = [&](uint32_t& x, EmitMeta& m) -> bool {
     for (;; x += r) {
-      const int st = rec_resolve(rec_issue(x, 0), x, m);
+      const int st = rec_resolve(rec_poll(x), x, m);
       if (st <= 0) {
         if (st < 0) err |= LSMBLK_ERR_TIMEOUT;
         return false;
@@ -2688,7 +2700,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
   }
   issue(cur);
   uint32_t in = it + r;        // the next block: its record loads in flight
-  uint64_t pg = rec_issue(in, 0);
+  uint64_t pg = rec_issue_asm(in);
   for (;;) {
     const uint32_t s = cur.s, n = cur.n;
     const uint64_t O = cur.O, size = cur.size;
@@ -2707,6 +2719,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
         if (l + 64 * i < nv) *reinterpret_cast<u32x4*>(L.img + (l + 64 * i) * 16) = vq[i];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): the staging and the next record
+    asm volatile("" : "+v"(pg));         // (landed: defined here for the compiler)
     EmitMeta nxt;
     const int st = rec_resolve(pg, in, nxt);
     bool has_next = st > 0;
@@ -2738,7 +2751,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
       if (has_next) {
         issue(nxt);
         in += r;
-        pg = rec_issue(in, 0);
+        pg = rec_issue_asm(in);
       }
     }
     wave_sync();
@@ -3842,8 +3855,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
   } else if (key == LSMBLK_DEBUG_DECODE_LAG && value >= 2 * kTile && value <= (1u << 24)) {
     c->dec_lag = value;
     c->dec_lag_bytes = 0;  // exactly this lag (experiments)
-  } else if (key == LSMBLK_DEBUG_ENCODE_UNFUSED) {
-    c->fuse_off = value != 0;
+  } else if (key == LSMBLK_DEBUG_ENCODE_FUSED) {
+    c->fuse_on = value != 0;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->timing) c->klog_n = 0;  // the log restarts with the timing
     c->timing = value != 0;
@@ -4092,8 +4105,9 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   }
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  // the fused walk + emit: per-segment slots, blocks no larger than emit's LDS image
-  const bool fused = slots && block_size <= 4096 && !c->fuse_off;
+  // the fused walk + emit (A/B only: the walk's instructions compete with emit's for the same
+  // issue slots): per-segment slots, blocks no larger than emit's LDS image
+  const bool fused = slots && block_size <= 4096 && c->fuse_on;
   uint32_t walk_wgs = 0, nwalk = 0;
   if (fused) {
     walk_wgs = uint32_t(std::min<uint64_t>(uint64_t(cus), (uint64_t(nseg) + 1) / 2));

@@ -52,24 +52,24 @@ def seg_slots(kv: O.KV, seg):
 
 
 def slot_check(kv: O.KV, seg, block_size, ref_blocks, ref_off):
-    """LSMBLK_ENCODE_SEG_SLOTS through the fused walk + emit launch and through plan_walk + emit
-    (LSMBLK_DEBUG_ENCODE_UNFUSED): every segment at its slot, the segments packed == the oracle's
+    """LSMBLK_ENCODE_SEG_SLOTS through plan_walk + emit and through the fused walk + emit launch
+    (LSMBLK_DEBUG_ENCODE_FUSED): every segment at its slot, the segments packed == the oracle's
     blocks and offsets."""
-    from lsm_amd._lib import LSMBLK_DEBUG_ENCODE_UNFUSED, lib
+    from lsm_amd._lib import LSMBLK_DEBUG_ENCODE_FUSED, lib
     ctx = batch._ctx(0)
-    for unfused in (0, 1):
-        assert lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_UNFUSED, unfused) == 0
+    for fused in (0, 1):
+        assert lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_FUSED, fused) == 0
         try:
             out, off, so = batch.encode_kv_slots(to_dev(kv), seg, block_size)
         finally:
-            lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_UNFUSED, 0)
+            lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_FUSED, 0)
         np.testing.assert_array_equal(so[:, 0].cpu().numpy(), seg_slots(kv, seg))
         blocks, poff = batch.slots_to_packed(out, off, so)
         np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), ref_off)
         got = blocks.cpu().numpy()
         assert len(got) == len(ref_blocks)
         mism = np.flatnonzero(got != ref_blocks)
-        assert mism.size == 0, f"slots (unfused={unfused}): first mismatching byte {mism[:8]} of {len(got)}"
+        assert mism.size == 0, f"slots (fused={fused}): first mismatching byte {mism[:8]} of {len(got)}"
 
 
 def roundtrip_check(kv: O.KV, seg, block_size, shift=0):
@@ -708,7 +708,10 @@ def test_slot_encode_large_matches_packed_and_writes_only_its_segments(cfg, n, s
     out_cap, blk_cap = batch.encode_bound(d, kb, vb)
     nseg = len(seg) - 1
     seg_t = torch.from_numpy(np.asarray(seg, np.uint32).view(np.int32)).cuda()
-    for rep in range(2):
+    from lsm_amd._lib import LSMBLK_DEBUG_ENCODE_FUSED, lib
+    ctx = batch._ctx(0)
+    for rep in range(4):  # (plan walk + emit twice, then the fused launch twice: epochs advance)
+        assert lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_FUSED, rep // 2) == 0
         out = batch._aligned_empty(out_cap, "cuda")
         out.fill_(0xA5)
         off = torch.zeros(blk_cap, dtype=torch.int64, device="cuda")
@@ -727,6 +730,7 @@ def test_slot_encode_large_matches_packed_and_writes_only_its_segments(cfg, n, s
         for a, b in so2.cpu().tolist():
             untouched[a:a + b] = False
         assert bool((out[untouched] == 0xA5).all())
+    lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_FUSED, 0)
 
 
 def test_slot_encode_refuses_missing_seg_out_and_bad_flags():
