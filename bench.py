@@ -223,7 +223,8 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     ctx = batch._ctx(local, stream)
     check(lib().lsmblk_ctx_reserve(ctx, nblk + 1, n + 1, len(seg)))
     check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
-    check(lib().lsmblk_debug_set(ctx, 8, 1 if args.encode_mode == "slots-fused" or args.trace_fused else 0))
+    if args.encode_mode == "slots-fused" or args.trace_fused:
+        check(lib().lsmblk_debug_set(ctx, 8, 1))
     if args.decode_lag is not None:
         check(lib().lsmblk_debug_set(ctx, 4, args.decode_lag))
 

@@ -140,6 +140,8 @@ def lib():
             raise RuntimeError(f"liblsmblk.so not built ({so}); run __graft_entry__.build()")
         L = ctypes.CDLL(so)
         for name, res, args in SIGNATURES:
+            if so != _build.SO and not hasattr(L, name):
+                continue  # (an A/B build from an earlier revision: its missing symbols stay unbound)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
