@@ -79,6 +79,8 @@ def parse(argv=None):
     p.add_argument("--encode-mode", default="packed", choices=["packed", "slots", "slots-fused"],
                    help="re-encode output: all segments packed (lsmblk_encode_batch), per-segment slots "
                         "(LSMBLK_ENCODE_SEG_SLOTS), or slots through the fused walk + emit launch (A/B)")
+    p.add_argument("--plan-pipe", type=int, default=None, choices=[0, 1],
+                   help="A/B: the plan walk's helper pipelined over batches (1, the default) or not (0)")
     p.add_argument("--decode-two-pass", action="store_true",
                    help="diagnostics (A/B): count + tile scan + decode (three launches) instead of the lagged decode")
     p.add_argument("--decode-lag", type=int, default=None,
@@ -225,6 +227,8 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     check(lib().lsmblk_debug_set(ctx, 3, 1 if args.decode_two_pass else 0))
     if args.encode_mode == "slots-fused" or args.trace_fused:
         check(lib().lsmblk_debug_set(ctx, 8, 1))
+    if args.plan_pipe is not None:
+        check(lib().lsmblk_debug_set(ctx, 9, args.plan_pipe))
     if args.decode_lag is not None:
         check(lib().lsmblk_debug_set(ctx, 4, args.decode_lag))
 

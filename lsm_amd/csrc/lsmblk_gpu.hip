@@ -1301,6 +1301,7 @@ struct PlanArgs {
   // blocks' sizes (a segment's last block does not end where the next one starts)
   uint64_t* seg_out;
   uint32_t* blk_sz;
+  uint32_t pipe_helper;    // the helper's loads pipelined over chunks (plan_produce_pipe)
 };
 
 __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
@@ -1635,22 +1636,27 @@ __device__ __forceinline__ void walk_segment(const PlanArgs& a, const PlanKeys& 
   }
 }
 
-// plan_produce for the fused walk + emit launch, software-pipelined over chunks: a chunk's 8 key
-// loads go out, then the next chunk's 20 entry-offset loads, and only then does the chunk wait for
-// its keys (vmcnt(20)) -- one memory round trip per chunk instead of two.  (Beside emit's stream the
-// round trips are long: the unpipelined helper held its walker to ~2.5 us per window.)  Both sets
-// are issued by inline asm so that the compiler neither sinks the key loads into the per-entry
-// branch (it did) nor waits for the offsets there; registers loaded by asm are landed by explicit
-// waits and then redefined for the compiler.
+// plan_produce, software-pipelined over batches of kPipeB entries per lane (64 kPipeB entries): a
+// batch's key loads go out, then the next batch's entry-offset loads (5 per entry), and only then
+// does the batch wait for its keys (vmcnt(5 kPipeB)) -- one memory round trip per batch instead of
+// two.  Both sets are issued by inline asm so that the compiler neither sinks the key loads into
+// the per-entry branch (it did) nor waits for the offsets there; registers loaded by asm are
+// landed by explicit waits and then redefined for the compiler.  (The fused walk + emit launch's
+// helper: beside emit's stream the round trips are long, and the unpipelined helper held its
+// walker to ~2.5 us per window.  The standalone walk: M's short segments wait on its round trips.)
+// Two entries per lane per batch keep the plan walk at 3 workgroups (24 waves) per CU.
+constexpr uint32_t kPipeB = 2;
+constexpr uint32_t kPipeE = 64 * kPipeB;  // entries per batch
+static_assert(kRing % kPipeE == 0 && kRing >= 2 * kPipeE, "ring holds whole batches");
 struct ProdOffs {
-  uint32_t kp[kProdBatch], kn[kProdBatch], pp[kProdBatch], v0[kProdBatch], v1[kProdBatch];
+  uint32_t kp[kPipeB], kn[kPipeB], pp[kPipeB], v0[kPipeB], v1[kPipeB];
 };
-// the 5 offset loads of entry lane l's i-th entry of chunk [c, cend) (indices clamped: always issued)
+// the 5 offset loads of entry lane l's i-th entry of batch [c, cend) (indices clamped: always issued)
 __device__ __forceinline__ void prod_offs_issue(const rsrc_t& RKO, const rsrc_t& RVO, uint32_t c, uint32_t cend,
                                                 ProdOffs& P) {
   const uint32_t l = lane_id();
 #pragma unroll
-  for (uint32_t i = 0; i < kProdBatch; ++i) {
+  for (uint32_t i = 0; i < kPipeB; ++i) {
     uint32_t e = c + 64 * i + l;
     e = e < cend ? e : cend - 1;
     const uint32_t oe = 4 * e, op = 4 * (e > 0 ? e - 1 : 0u);
@@ -1667,26 +1673,30 @@ __device__ __forceinline__ void prod_offs_issue(const rsrc_t& RKO, const rsrc_t&
 __device__ __forceinline__ void prod_offs_land(ProdOffs& P) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-  for (uint32_t i = 0; i < kProdBatch; ++i)
+  for (uint32_t i = 0; i < kPipeB; ++i)
     asm volatile("" : "+v"(P.kp[i]), "+v"(P.kn[i]), "+v"(P.pp[i]), "+v"(P.v0[i]), "+v"(P.v1[i]));
 }
 __device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t s0, uint32_t s1, uint32_t* CR,
-                                  uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t& err) {
-  static_assert(kChunk == 64 * kProdBatch && kProdBatch == 4, "one load batch of 4 entries per lane per chunk");
+                                  uint32_t* CA, uint32_t* prod, const uint32_t* cons, uint32_t& err,
+                                  uint64_t* tr = nullptr) {
+  static_assert(kPipeB == 2, "the vmcnt below counts 5 kPipeB offset loads");
   const uint32_t l = lane_id();
   const uint32_t klim = K.glead + uni(a.key_off[a.n]);
+  uint64_t waited = 0;
+  if (tr && l == 0) tr[4] = __builtin_amdgcn_s_memrealtime();
   if (s0 >= s1) return;
   const uint32_t nb4 = uint32_t(min(uint64_t(a.n + 1) * 4, uint64_t(0xFFFFFFF0u)));
   const rsrc_t RKO = make_rsrc(a.key_off, nb4), RVO = make_rsrc(a.val_off, nb4);
   ProdOffs P;
   asm volatile("s_nop 4" ::: "memory");  // (VALU-written descriptor SGPRs before a VMEM read of them, inside asm)
-  prod_offs_issue(RKO, RVO, s0, s1 - s0 < kChunk ? s1 : s0 + kChunk, P);
+  prod_offs_issue(RKO, RVO, s0, s1 - s0 < kPipeE ? s1 : s0 + kPipeE, P);
   prod_offs_land(P);
-  for (uint32_t c = s0; c < s1; c += kChunk) {
-    const uint32_t cend = s1 - c < kChunk ? s1 : c + kChunk;
-    if (c - s0 + kChunk > kRing) {  // ring space: the walker's window must have passed c + kChunk - kRing
-      const uint32_t need = c - s0 + kChunk - kRing;
+  for (uint32_t c = s0; c < s1; c += kPipeE) {
+    const uint32_t cend = s1 - c < kPipeE ? s1 : c + kPipeE;
+    if (c - s0 + kPipeE > kRing) {  // ring space: the walker's window must have passed c + kPipeE - kRing
+      const uint32_t need = c - s0 + kPipeE - kRing;
       uint32_t spins = 0;
+      const uint64_t w0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
       while (__hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
         if (++spins > kSpinMax) {
           err |= LSMBLK_ERR_TIMEOUT;
@@ -1694,11 +1704,12 @@ __device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (tr) waited += __builtin_amdgcn_s_memrealtime() - w0;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
-    u32x4 xk[kProdBatch], xp[kProdBatch];
+    u32x4 xk[kPipeB], xp[kPipeB];
 #pragma unroll
-    for (uint32_t i = 0; i < kProdBatch; ++i) {
+    for (uint32_t i = 0; i < kPipeB; ++i) {
       const uint32_t ok = K.glead + P.kp[i], op = K.glead + P.pp[i];
       asm volatile(
           "buffer_load_dwordx4 %0, %2, %4, 0 offen\n\t"
@@ -1706,15 +1717,15 @@ __device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t
           : "=&v"(xk[i]), "=&v"(xp[i])
           : "v"(ok), "v"(op), "s"(K.gk));
     }
-    // the next chunk's offsets (after the last chunk: its own again -- always 20 loads)
-    const uint32_t cn = c + kChunk < s1 ? c + kChunk : c;
+    // the next batch's offsets (after the last batch: its own again -- always 5 kPipeB loads)
+    const uint32_t cn = c + kPipeE < s1 ? c + kPipeE : c;
     ProdOffs Pn;
-    prod_offs_issue(RKO, RVO, cn, s1 - cn < kChunk ? s1 : cn + kChunk, Pn);
-    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // this chunk's keys (issued before the 20)
+    prod_offs_issue(RKO, RVO, cn, s1 - cn < kPipeE ? s1 : cn + kPipeE, Pn);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // this batch's keys (issued before the 10)
 #pragma unroll
-    for (uint32_t i = 0; i < kProdBatch; ++i) asm volatile("" : "+v"(xk[i]), "+v"(xp[i]));
+    for (uint32_t i = 0; i < kPipeB; ++i) asm volatile("" : "+v"(xk[i]), "+v"(xp[i]));
 #pragma unroll
-    for (uint32_t i = 0; i < kProdBatch; ++i) {
+    for (uint32_t i = 0; i < kPipeB; ++i) {
       const uint32_t e = c + 64 * i + l;
       if (e >= cend) continue;
       const uint32_t kp = P.kp[i], pp = P.pp[i], kl = P.kn[i] - kp, x = (e - s0) & (kRing - 1);
@@ -1764,6 +1775,10 @@ __device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t
     prod_offs_land(Pn);
     P = Pn;
   }
+  if (tr && l == 0) {
+    tr[5] = __builtin_amdgcn_s_memrealtime();
+    tr[6] = waited;
+  }
 }
 
 // (fused: three workgroups of 8 waves per CU, so that up to 3 K segments walk at once)
@@ -1799,7 +1814,8 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
   const PlanKeys K = plan_keys(a);
   uint64_t* const tr = kDiag && a.dbg && g < kDbgTiles ? a.dbg + 16 + 8 * uint64_t(g) : nullptr;  // (diagnostics)
   if (wv >= 4) {
-    plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
+    if (a.pipe_helper) plan_produce_pipe(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
+    else plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
     const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
                           (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
     raise_err(a.stats, werr);
@@ -3857,6 +3873,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->dec_lag_bytes = 0;  // exactly this lag (experiments)
   } else if (key == LSMBLK_DEBUG_ENCODE_FUSED) {
     c->fuse_on = value != 0;
+  } else if (key == LSMBLK_DEBUG_PLAN_PIPE) {
+    c->plan_pipe = value != 0;
   } else if (key == LSMBLK_DEBUG_KERNEL_TIMING) {
     if (value && !c->timing) c->klog_n = 0;  // the log restarts with the timing
     c->timing = value != 0;
@@ -4150,6 +4168,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.dbg = c->dbg_on ? c->dbg : nullptr;
   p.seg_out = slots ? seg_out : nullptr;
   p.blk_sz = slots ? c->blk_sz : nullptr;
+  p.pipe_helper = c->plan_pipe ? 1u : 0u;
   EmitArgs e;
   e.keys = in->keys;
   e.key_off = in->key_off;
