@@ -176,7 +176,7 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
                                        that walks and emits at once (encode_fused_kernel; measured slower
                                        than the plan walk + emit launches) */
 #define LSMBLK_DEBUG_PLAN_PIPE 9 /* 0: the plan walk's helper waits for each chunk's offsets, then its keys
-                                    (two round trips per chunk); 1 (default): pipelined over chunks */
+                                    (two round trips per chunk, the default); 1: pipelined over batches */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* The trace of the last lagged decode with LSMBLK_DEBUG_COUNTERS on (n <= 16 + 8 * 32768 words;
  * synchronizes).  Words 16 + 8 t + k, 100 MHz s_memrealtime stamps of 64-block tile t: k = 0 tile

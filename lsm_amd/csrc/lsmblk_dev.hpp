@@ -588,7 +588,7 @@ struct lsmblk_ctx {
   uint8_t* fbig = nullptr;
   uint64_t fbig_cap = 0;
   bool fuse_on = false;          // diagnostics: slot output through encode_fused_kernel (A/B)
-  bool plan_pipe = true;         // the plan walk's helper pipelined over chunks (LSMBLK_DEBUG_PLAN_PIPE, A/B)
+  bool plan_pipe = false;        // the plan walk's helper pipelined over chunks (LSMBLK_DEBUG_PLAN_PIPE, A/B)
   uint64_t* lag_gran = nullptr;  // lagged decode granules (uncached): 3 aggregate + 3 base per block,
   uint64_t lag_blk_cap = 0;      //   then 3 aggregate + 3 inclusive per 64-block tile; blocks covered
   uint32_t rot_poison = 0;       // diagnostics builds only: LSMBLK_DEBUG_ROT_POISON
