@@ -3794,6 +3794,7 @@ int lsmblk_ctx_create(int device, lsmblk_ctx** out) {
   if (!c) return LSMBLK_E_NOMEM;
   c->device = device;
   if (const char* e = getenv("LSMBLK_POLL_MODE")) c->poll = uint32_t(atoi(e));
+  if (const char* e = getenv("LSMBLK_PLAN_PIPE")) c->plan_pipe = atoi(e) != 0;  // (A/B: LSMBLK_DEBUG_PLAN_PIPE)
   DeviceGuard dg(device);
   if (!dg.ok || hipMalloc(&c->counters, 2048) != hipSuccess) {
     delete c;
