@@ -380,6 +380,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     result["read_path_verify"] = read_path_verify(blocks, blk_off, nblk, out_kv, n, K, V, st_dec, dev, stream)
     result["framing_meta"] = framing_meta(pk_blocks, pk_off, nblk, seg_t, st_enc, dev, stream)
     result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
+    result["encode_slots"] = encode_slots(out_kv, seg_t, len(seg) - 1, bs, blocks, blk_off, dev, stream)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
     if not args.no_pcie and world == 1:
@@ -1091,6 +1092,38 @@ def framing_meta(blocks, blk_off, nblk, seg_t, st_enc, dev, stream, reps=5):
             "meta_bytes": total, "block_bytes_read": E, "sections": nseg,
             "gib_s_of_blocks": round(E / (ms * 1e-3) / GiB, 2), "checked_sections": 16 if ok else 0,
             "ok": bool(ok)}
+
+
+def encode_slots(kv, seg_t, nseg, bs, blocks, blk_off, dev, stream, reps=5):
+    """Re-encode with per-segment slots (LSMBLK_ENCODE_SEG_SLOTS: every SST's data section at a place
+    known before the call, include/lsmblk.h) beside the packed headline encode: encode ms (HIP
+    events over reps calls), and the slots packed == the input blocks.  Not part of `value`."""
+    K, V = kv.byte_sizes()
+    n = kv.n
+    out_cap, blk_cap = K + V + 18 * n + 16, blk_off.numel() + 1
+    out = batch._aligned_empty(out_cap, dev)
+    off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    so = torch.zeros(2 * nseg, dtype=torch.int64, device=dev)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def run():
+        batch.encode_into(kv, seg_t, nseg, bs, out, out_cap, off, blk_cap, st, stream=stream, seg_out=so)
+    run()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        run()
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    s = st.cpu().tolist()
+    nblk = blk_off.numel() - 1
+    ok = s[3] == 0 and s[0] == nblk
+    if ok:
+        pb, po = batch.slots_to_packed(out, off[:nblk + 1], so)
+        ok = torch.equal(pb, blocks) and torch.equal(po, blk_off)
+    return {"call": "lsmblk_encode_batch_ex(LSMBLK_ENCODE_SEG_SLOTS)", "ms": round(ms, 4), "segments": nseg,
+            "packed_equal_input": bool(ok)}
 
 
 def compaction_filter(kv, n, K, V, dev, stream, reps=5):
