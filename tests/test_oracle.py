@@ -272,3 +272,42 @@ def test_compaction_filter_closed_form_equals_reference_loop(seed):
     # watermark above every ts: one version per key survives, bottom tombstones vanish
     kept = pyref.compact_filter_loop(ents, 10**6, True)
     assert len({k for k, _, _ in kept}) == len(kept) and all(v for _, _, v in kept)
+
+
+@pytest.mark.parametrize("case", ["uniform", "zipf", "mixed", "one_entry_blocks", "tiny_blocks"])
+def test_slot_bound_holds_for_every_segment(case):
+    """LSMBLK_ENCODE_SEG_SLOTS (include/lsmblk.h) places segment s at slot(s) = the keys and
+    values of the segments before it + 18 bytes per entry.  That is an upper bound of those
+    segments' encoded size -- per entry 2 + 2 + 8 + 2 header bytes and a 2-byte offset slot, per
+    block a 2-byte count and at least one entry, and the key minus its shared prefix -- so no
+    segment runs into the next one's slot.  Checked on the oracle's packing, including the
+    extreme where it is tight (every entry its own block, no shared prefix)."""
+    if case == "one_entry_blocks":  # block_size below any entry: one entry per block, prefix 0
+        kv = O.KV.from_entries([(b"%08d" % (i * 7919 % 100003), i, b"v" * (i % 5)) for i in sorted(range(300))])
+        seg, bs = [0, 100, 100, 250, 300], 8
+    elif case == "tiny_blocks":
+        kv = O.KV(*synth.gen_uniform(2000, seed=4))
+        seg, bs = [0, 700, 1500, kv.n], 64
+    else:
+        gen = {"uniform": synth.gen_uniform, "zipf": synth.GENERATORS["Z"], "mixed": synth.GENERATORS["M"]}[case]
+        kv = O.KV(*gen(4000, seed=9))
+        seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 32 << 10)
+        bs = 65536 if case == "mixed" else 4096
+    seg = np.asarray(seg, dtype=np.int64)
+    ko, vo = kv.key_off.astype(np.int64), kv.val_off.astype(np.int64)
+    slots = (ko[seg] - ko[seg[0]]) + (vo[seg] - vo[seg[0]]) + 18 * (seg - seg[0])
+    tight = False
+    for s in range(len(seg) - 1):
+        sub = O.KV(kv.keys[ko[seg[s]]:ko[seg[s + 1]]], (kv.key_off[seg[s]:seg[s + 1] + 1] - kv.key_off[seg[s]]),
+                   kv.vals[vo[seg[s]]:vo[seg[s + 1]]], (kv.val_off[seg[s]:seg[s + 1] + 1] - kv.val_off[seg[s]]),
+                   kv.ts[seg[s]:seg[s + 1]])
+        n = sub.n
+        if n == 0:
+            assert slots[s + 1] == slots[s]
+            continue
+        rc, blocks, off = O.encode_segments(sub, [0, n], bs)
+        assert rc == 0
+        assert len(blocks) <= slots[s + 1] - slots[s], (case, s)
+        tight = tight or len(blocks) == slots[s + 1] - slots[s]
+    if case in ("one_entry_blocks", "tiny_blocks"):
+        assert tight  # (entries over the block size: one per block, nothing shared with a first key)
