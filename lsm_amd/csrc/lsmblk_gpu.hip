@@ -1985,6 +1985,11 @@ struct EmitMeta {
   uint32_t kb0, kb1, vb0, vb1;
 };
 
+// The plan's error flags that leave its block tables unusable: emit then writes nothing (a
+// refused segment table gave blocks whose end entry precedes their start, which emit_big walked
+// as ~2^32 entries).  CAPACITY is not one: every block that fits is still written.
+constexpr uint64_t kPlanFatal = LSMBLK_ERR_SEGMENTS | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_INTERNAL | LSMBLK_ERR_EMPTY_KEY;
+
 // One fast-path block of emit (wave-uniform): entries [s, s + n), output [O, O + size), its keys
 // staged at kimg[klead], its values at img[vlead], fl = its first key's length.
 struct EmitBlk {
@@ -2173,7 +2178,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   __shared__ EmitLds lds[kEmitWaves];
   EmitLds& L = lds[threadIdx.x >> 6];  // (a VGPR LDS base: readfirstlane here costs the kernel 4 spilled VGPRs)
   const uint32_t l = lane_id();
-  const uint64_t nblk = uni64(a.stats[0]);
+  const uint64_t nblk = uni64(a.stats[3]) & kPlanFatal ? 0 : uni64(a.stats[0]);
   const uint64_t nwaves = uint64_t(gridDim.x) * kEmitWaves;
   uint32_t err = 0;
   const uintptr_t kaddr = reinterpret_cast<uintptr_t>(a.keys), vaddr = reinterpret_cast<uintptr_t>(a.vals);
@@ -2317,7 +2322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
 // blocks j, j + nw, j + 2 nw, ... 64 at a time (a flag per lane, then a ballot).
 __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   const EmitArgs a = resolve(a0);
-  const uint64_t nblk = uni64(a.stats[0]);
+  const uint64_t nblk = uni64(a.stats[3]) & kPlanFatal ? 0 : uni64(a.stats[0]);
   const uint64_t lim = nblk < a.blk_cap ? nblk : (a.blk_cap ? a.blk_cap - 1 : 0);
   const uint64_t nw = uint64_t(gridDim.x) * 4;
   const uint32_t l = lane_id();

@@ -750,3 +750,84 @@ def test_slot_encode_refuses_missing_seg_out_and_bad_flags():
     so = torch.zeros(2, dtype=torch.int64, device="cuda")
     assert f(ctx, ctypes.byref(c), seg_t.data_ptr(), 1, 4096, 2, out.data_ptr(), 1 << 20, off.data_ptr(), kv.n + 2,
              so.data_ptr(), st.data_ptr(), None) != 0
+
+
+def _slot_encode_raw(kv_dev, seg, bs, out_cap=None, fused=0):
+    """One lsmblk_encode_batch_ex(SEG_SLOTS) call -> (status, stats, out, blk_off, seg_out)."""
+    from lsm_amd._lib import LSMBLK_DEBUG_ENCODE_FUSED, lib
+    ctx = batch._ctx(0)
+    nseg = len(seg) - 1
+    kb, vb = kv_dev.byte_sizes()
+    cap, blk_cap = batch.encode_bound(kv_dev, kb, vb)
+    out_cap = cap if out_cap is None else out_cap
+    out = batch._aligned_empty(max(out_cap, 16), "cuda")
+    off = torch.zeros(blk_cap, dtype=torch.int64, device="cuda")
+    so = torch.full((max(2 * nseg, 1),), -1, dtype=torch.int64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    seg_t = torch.from_numpy(np.asarray(seg, np.int64).astype(np.uint32).view(np.int32)).cuda()
+    assert lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_FUSED, fused) == 0
+    try:
+        batch.encode_into(kv_dev, seg_t, nseg, bs, out, out_cap, off, blk_cap, st, seg_out=so)
+        torch.cuda.synchronize()
+    finally:
+        lib().lsmblk_debug_set(ctx, LSMBLK_DEBUG_ENCODE_FUSED, 0)
+    return batch._status(st), st.cpu().tolist(), out, off, so
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_slot_encode_empty_stream_and_empty_segments(fused):
+    """No entries: every segment empty, slot 0, zero blocks, blk_off[0] = 0 -- as the packed
+    encode with the same segment table."""
+    kv = O.KV.from_entries([])
+    d = to_dev(kv)
+    for seg in ([0, 0], [0, 0, 0, 0]):
+        status, st, out, off, so = _slot_encode_raw(d, seg, 4096, fused=fused)
+        assert status == 0 and st[0] == 0 and st[1] == 0
+        assert so.cpu().tolist()[:2 * (len(seg) - 1)] == [0, 0] * (len(seg) - 1)
+        assert int(off[0].item()) == 0
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_slot_encode_refuses_bad_segment_tables(fused):
+    """A segment table that does not start at 0, decreases, or ends past / before n fails with
+    LSMBLK_E_INVAL (the walkers' SEGMENTS flag) -- no fault, no hang: emit writes nothing over
+    tables the plan refused (a decreasing table once gave a block whose end entry preceded its
+    start, which emit_big walked as ~2^32 entries) -- and the context then encodes a good table
+    correctly.  The packed encode is held to the same."""
+    from lsm_amd._lib import LSMBLK_E_INVAL
+    kv = O.KV(*synth.gen_uniform(3000, seed=12))
+    d = to_dev(kv)
+    n = kv.n
+    for seg in ([5, n], [0, 2000, 1000, n], [0, 1000, n - 1], [0, 1000, n + 7]):
+        status, *_ = _slot_encode_raw(d, seg, 4096, fused=fused)
+        assert status == LSMBLK_E_INVAL, seg
+        if not fused:  # the packed encode
+            kb, vb = d.byte_sizes()
+            cap, blk_cap = batch.encode_bound(d, kb, vb)
+            out = batch._aligned_empty(cap, "cuda")
+            off = torch.zeros(blk_cap, dtype=torch.int64, device="cuda")
+            st = torch.zeros(4, dtype=torch.int64, device="cuda")
+            seg_t = torch.from_numpy(np.asarray(seg, np.int64).astype(np.uint32).view(np.int32)).cuda()
+            batch.encode_into(d, seg_t, len(seg) - 1, 4096, out, cap, off, blk_cap, st)
+            torch.cuda.synchronize()
+            assert batch._status(st) == LSMBLK_E_INVAL, seg
+    seg = [0, 1000, 2000, n]
+    rc, ref_blocks, ref_off = O.encode_segments(kv, seg, 4096)
+    status, st, out, off, so = _slot_encode_raw(d, seg, 4096, fused=fused)
+    assert status == 0
+    pb, po = batch.slots_to_packed(out, off[:st[0] + 1], so)
+    assert np.array_equal(pb.cpu().numpy(), ref_blocks)
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_slot_encode_capacity_below_the_bound_reported(fused):
+    """out_cap below the segments' slots: LSMBLK_E_CAPACITY, nothing written past out_cap."""
+    from lsm_amd._lib import LSMBLK_E_CAPACITY
+    kv = O.KV(*synth.gen_uniform(4000, seed=13))
+    d = to_dev(kv)
+    seg = [0, 1500, 3000, kv.n]
+    kb, vb = d.byte_sizes()
+    cap, _ = batch.encode_bound(d, kb, vb)
+    small = cap // 2 & ~15
+    status, st, out, off, so = _slot_encode_raw(d, seg, 4096, out_cap=small, fused=fused)
+    assert status == LSMBLK_E_CAPACITY
