@@ -831,3 +831,31 @@ def test_slot_encode_capacity_below_the_bound_reported(fused):
     small = cap // 2 & ~15
     status, st, out, off, so = _slot_encode_raw(d, seg, 4096, out_cap=small, fused=fused)
     assert status == LSMBLK_E_CAPACITY
+
+
+@pytest.mark.parametrize("mode", ["packed", "slots", "fused"])
+def test_encode_refuses_an_empty_key(mode):
+    """An empty key (BlockBuilder::add asserts `!key.is_empty()`, src/block/builder.rs:55) fails
+    the call with LSMBLK_E_INVAL -- the walkers' EMPTY_KEY flag -- and emit writes nothing: the
+    output buffer keeps its fill bytes."""
+    from lsm_amd._lib import LSMBLK_E_INVAL
+    ents = [(b"k%05d" % i, i, b"v" * 40) for i in range(600)]
+    ents[300] = (b"", 300, b"v" * 40)
+    d = to_dev(O.KV.from_entries(ents))
+    seg = [0, 250, 600]
+    if mode == "packed":
+        kb, vb = d.byte_sizes()
+        cap, blk_cap = batch.encode_bound(d, kb, vb)
+        out = batch._aligned_empty(cap, "cuda")
+        out.fill_(0xA5)
+        off = torch.zeros(blk_cap, dtype=torch.int64, device="cuda")
+        st = torch.zeros(4, dtype=torch.int64, device="cuda")
+        seg_t = torch.tensor(seg, dtype=torch.int32, device="cuda")
+        batch.encode_into(d, seg_t, len(seg) - 1, 4096, out, cap, off, blk_cap, st)
+        torch.cuda.synchronize()
+        status = batch._status(st)
+    else:
+        status, st, out, off, so = _slot_encode_raw(d, seg, 4096, fused=int(mode == "fused"))
+    assert status == LSMBLK_E_INVAL
+    if mode == "packed":
+        assert bool((out == 0xA5).all())
