@@ -666,7 +666,12 @@ int grow(T** p, uint64_t* cap, uint64_t need, uint64_t per, unsigned flags = 0) 
     *cap = 0;
     return LSMBLK_E_NOMEM;
   }
-  if (hipMemset(*p, 0, nc * per * sizeof(T)) != hipSuccess) return LSMBLK_E_HIP;
+  // hipMemset runs on the null stream, which does not order with the caller's non-blocking stream:
+  // unwaited, the fill could land after the call's own kernels had written the buffer (it wiped a
+  // fresh context's SST-rotation levels -- the round-4 hang).  So the fill
+  // completes before grow returns, before any kernel of the call is launched.
+  if (hipMemset(*p, 0, nc * per * sizeof(T)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return LSMBLK_E_HIP;
   *cap = nc;
   return LSMBLK_OK;
 }

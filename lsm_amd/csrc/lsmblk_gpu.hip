@@ -4402,7 +4402,11 @@ int ensure_crc_tabs(lsmblk_ctx* c) {
     c->crc_tabs = nullptr;
     return LSMBLK_E_NOMEM;
   }
-  return hipMemcpy(c->crc_tabs, &h, sizeof(CrcAllTabs), hipMemcpyHostToDevice) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+  // (a null-stream copy: completed before the first CRC kernel on the caller's stream can read it)
+  return hipMemcpy(c->crc_tabs, &h, sizeof(CrcAllTabs), hipMemcpyHostToDevice) == hipSuccess &&
+                 hipDeviceSynchronize() == hipSuccess
+             ? LSMBLK_OK
+             : LSMBLK_E_HIP;
 }
 
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,

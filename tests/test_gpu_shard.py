@@ -214,6 +214,37 @@ def test_ranges_on_distinct_streams_compact_dist_single_rank():
         dist.destroy_process_group()
 
 
+def test_fresh_contexts_on_distinct_streams_repeatedly():
+    """The round-4 hang, found: a context's first call grew its workspace and
+    zeroed it with hipMemset on the null stream, which does not order with the caller's
+    non-blocking stream -- the fill could land after the rotation had written its levels there,
+    leaving links that never advance (round 4: rot_f_kernel spun forever; round 5, with the
+    lifting bounded: LSMBLK_E_INTERNAL on ~70 % of these runs).  Fresh ranges (fresh contexts) on
+    fresh streams, eight times over, every time equal to the single-stream compaction."""
+    import os
+    import socket
+    import torch.distributed as dist
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(22)
+        kv, rs = case(78, versions=3, nkeys=6000)
+        d = to_dev(kv)
+        bs, target = 4096, 24 << 10
+        opts = batch.compact_opts(0, False, block_size=bs, target_sst_size=target)
+        splitters = pick_splitters(kv, rng, 3)
+        for _ in range(8):
+            res = shard.compact_dist(_shards_on_own_streams(d, rs, opts, splitters))
+            check_against_single_stream(kv, rs, res, 0, False, bs, target)
+    finally:
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------- two-level merge (TwoMergeIterator) by key range
 from lsm_amd._lib import LSMBLK_MERGE_TWO_LEVEL as TWO  # noqa: E402
 
