@@ -2309,10 +2309,10 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if (hipMemsetAsync(stats, 0, LSMBLK_COMPACT_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (hipMemsetAsync(blk_off, 0, 8, st) != hipSuccess) return LSMBLK_E_HIP;
   // The rotation needs only the kept entries' metadata (and their keys, read in the merge input
-  // through kidx), so the kept stream's key and value bytes are gathered after it.  (Running the
-  // rotation on a second stream beside that gather measured 12.05 -> 11.50 ms on config C, but the
-  // GPU test suite then hung in a later multi-stream test -- a cross-stream wait with four hardware
-  // queues shared by more streams -- so everything stays on the caller's stream.)
+  // through kidx), so the kept stream's key and value bytes are gathered on `st` while the
+  // rotation runs on the context's second stream; the encode waits for both.  (Reverted in round 4
+  // after a GPU-suite hang; re-landed once that hang's cause was found in grow(), DESIGN.md
+  // section 10.)
   MergePlan MP{};
   GatherArgs G{};
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
@@ -2336,8 +2336,10 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   r.akey_off = in->key_off;
   r.an = n;
   r.poison = c->rot_poison;
-  if ((rc = rotation_locked(c, r, st))) return rc;
+  if ((rc = lsmblk_impl::fork_aux(c, st))) return rc;
+  if ((rc = rotation_locked(c, r, c->aux))) return rc;
   if ((rc = mwrite_bytes(G, n, st))) return rc;
+  if ((rc = lsmblk_impl::join_aux(c, st))) return rc;
   lsmblk_kv_stream ks = *kept;
   ks.n = n;  // bound; the encode reads the kept count from fst[0]
   if ((rc = lsmblk_impl::encode_locked(c, &ks, R.dn, sst_start, r.nsst, sst_cap - 1, o->block_size, out, out_cap,

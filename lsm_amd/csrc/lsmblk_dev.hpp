@@ -632,6 +632,10 @@ struct lsmblk_ctx {
   // CRC-verified decode (lsmblk_decode_batch_ex): per-block CRCs
   uint32_t* vcrc = nullptr;
   uint64_t vcrc_cap = 0;
+  // lsmblk_compact_batch: a second stream for the SST rotation beside the kept stream's byte
+  // gather, and the fork / join events (created on first use)
+  hipStream_t aux = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // SST files (lsmblk_sst.hip)
   uint8_t* sws = nullptr;
   uint64_t sws_cap = 0;
@@ -767,6 +771,10 @@ int segment_blocks_locked(lsmblk_ctx* c, const uint32_t* seg_start, uint32_t nse
 // crc_kernel<false> for a few long ranges (sections: a wave per range, its 4 KiB chunks one after
 // another, keeps more waves busy than a 16-lane row per range).
 int ensure_crc_tabs(lsmblk_ctx* c);
+// The context's second stream and its fork / join events (created on first use): work launched
+// on c->aux after fork_aux(c, st) runs beside st; join_aux(c, st) makes st wait for it.
+int fork_aux(lsmblk_ctx* c, hipStream_t st);
+int join_aux(lsmblk_ctx* c, hipStream_t st);
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg = nullptr, bool sections = false);
 // lsmblk_block_meta_batch with the context lock held.

@@ -3813,6 +3813,9 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   if (!c) return;
   DeviceGuard dg(c->device, c);
   (void)hipDeviceSynchronize();
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipFree(c->counters);
   (void)hipFree(c->dec_agg);
   (void)hipFree(c->tile_sum);
@@ -4390,6 +4393,21 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
 }  // extern "C"
 
 namespace lsmblk_impl {
+int fork_aux(lsmblk_ctx* c, hipStream_t st) {
+  if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return LSMBLK_E_HIP;
+  if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
+  if (!c->join_ev && hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
+  if (hipEventRecord(c->fork_ev, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess)
+    return LSMBLK_E_HIP;
+  return LSMBLK_OK;
+}
+
+int join_aux(lsmblk_ctx* c, hipStream_t st) {
+  if (hipEventRecord(c->join_ev, c->aux) != hipSuccess || hipStreamWaitEvent(st, c->join_ev, 0) != hipSuccess)
+    return LSMBLK_E_HIP;
+  return LSMBLK_OK;
+}
+
 int ensure_crc_tabs(lsmblk_ctx* c) {
   if (c->crc_tabs) return LSMBLK_OK;
   static CrcAllTabs h;  // (built once per process: the stream tables take ~40 M bit steps)
