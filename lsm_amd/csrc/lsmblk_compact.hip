@@ -1969,12 +1969,28 @@ __global__ void gate_kernel(const uint64_t* fst, uint64_t* dn) {
   if (threadIdx.x == 0) *dn = fst[3] ? 0ull : fst[0];
 }
 
-uint32_t rot_levels(uint64_t target) {
+#ifndef LSMBLK_ROT_HOPS
+#define LSMBLK_ROT_HOPS 16
+#endif
+// Top-level hops a lift makes for an SST of full blocks (0: no cap, every level).
+constexpr uint64_t kRotHops = LSMBLK_ROT_HOPS;
+
+uint32_t rot_levels(uint64_t target, uint32_t block_size) {
   // a block and its CRC take >= 23 bytes (4 + 1 + 8 + 2 + 2 + 2 + 4), so an SST reaches the
   // target within ceil(target / 23) blocks: 2^(levels-1) hops cover it
   const uint64_t j = target / 23 + 2;
   uint32_t k = 1;
   while (k < kRotMaxLevels && (1ull << (k - 1)) < j) ++k;
+  // Every lift repeats its top level while it fits (rot_f_kernel, lift_target, lift_before), so
+  // the levels above the one whose hop covers 1 / kRotHops of an SST of full blocks are not
+  // built: each doubling level is a pass over every entry, each extra hop one gather per entry.
+  // (Small blocks among them only add hops, never change a result.)
+  if (kRotHops && block_size) {
+    const uint64_t jb = target / block_size / kRotHops + 1;
+    uint32_t c = 1;
+    while (c < k && (1ull << (c - 1)) < jb) ++c;
+    k = c;
+  }
   return k;
 }
 
@@ -1985,11 +2001,12 @@ struct RotPlan {
 };
 
 // flevels > 0: the shard layout (F^(2^k) levels instead of the chain ping-pong, carry state).
-RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, uint32_t flevels = 0) {
+RotPlan plan_rot(uint8_t* base, uint64_t off, uint64_t n_max, uint64_t target, uint32_t block_size,
+                 uint32_t flevels = 0) {
   RotPlan P{};
   Carve cv{base, off};
   const uint64_t N1 = n_max + 1;
-  const uint32_t L = rot_levels(target);
+  const uint32_t L = rot_levels(target, block_size);
   P.r.n_max = n_max;
   P.r.target = target;
   P.r.levels = L;
@@ -2099,7 +2116,7 @@ uint32_t shard_flevels(uint32_t sst_cap) {
 
 // The rotation arguments of the last lsmblk_shard_rotation_prepare on this context.
 RotArgs shard_args(lsmblk_ctx* c, const lsmblk_kv_stream* ext) {
-  const RotPlan P = plan_rot(c->rws, 0, c->shard_n, c->shard_target, shard_flevels(c->shard_sst_cap));
+  const RotPlan P = plan_rot(c->rws, 0, c->shard_n, c->shard_target, c->shard_block_size, shard_flevels(c->shard_sst_cap));
   RotArgs r = P.r;
   r.dn = P.dn;
   r.m = c->shard_m;
@@ -2172,7 +2189,7 @@ int lsmblk_shard_rotation_prepare_ex(lsmblk_ctx* c, const lsmblk_kv_stream* ext,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   c->shard_ready = false;
   const uint32_t fl = shard_flevels(sst_cap);
-  const RotPlan P0 = plan_rot(nullptr, 0, ext->n, target_sst_size, fl);
+  const RotPlan P0 = plan_rot(nullptr, 0, ext->n, target_sst_size, block_size, fl);
   int rc = grow(&c->rws, &c->rws_cap, P0.bytes, 1);
   if (rc) return rc;
   c->shard_n = ext->n;
@@ -2262,10 +2279,10 @@ int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_
   DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  RotPlan P = plan_rot(nullptr, 0, in->n, target_sst_size);
+  RotPlan P = plan_rot(nullptr, 0, in->n, target_sst_size, block_size);
   int rc = ensure_ws(c, P.bytes);
   if (rc) return rc;
-  P = plan_rot(c->cws, 0, in->n, target_sst_size);
+  P = plan_rot(c->cws, 0, in->n, target_sst_size, block_size);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   LSM_LAUNCH(set_u64_kernel, dim3(1), dim3(64), 0, st, P.dn, uint64_t(in->n));
   RotArgs r = P.r;
@@ -2300,7 +2317,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   const uint64_t n = in->n;
   // workspace: merge + gather, then rotation, then the stage stats
   MergePlan M = plan_merge(nullptr, n, nrun);
-  RotPlan R = plan_rot(nullptr, M.bytes, n, o->target_sst_size);
+  RotPlan R = plan_rot(nullptr, M.bytes, n, o->target_sst_size, o->block_size);
   const uint64_t stats_off = (R.bytes + 255) & ~uint64_t(255);
   if ((rc = ensure_ws(c, stats_off + 4 * 64))) return rc;
   uint64_t* sts = reinterpret_cast<uint64_t*>(c->cws + stats_off);
@@ -2318,7 +2335,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   if ((rc = merge_gather_locked(c, in, run_start, nrun, 1, o->watermark, o->bottom_level, o->prefixes, o->prefix_off,
                                 o->nprefix, nullptr, kept, fst, st, &MP, two, LSMBLK_TWO_END_IN_RANGE, nullptr, &G)))
     return rc;
-  R = plan_rot(c->cws, M.bytes, n, o->target_sst_size);
+  R = plan_rot(c->cws, M.bytes, n, o->target_sst_size, o->block_size);
   LSM_LAUNCH(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
   RotArgs r = R.r;
   r.keys = kept->keys;
