@@ -4393,18 +4393,10 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
 }  // extern "C"
 
 namespace lsmblk_impl {
-#ifndef LSMBLK_AUX_PRIO
-#define LSMBLK_AUX_PRIO 1
-#endif
 int fork_aux(lsmblk_ctx* c, hipStream_t st) {
-  // The work forked onto the second stream is the longer branch (the compaction's SST rotation
-  // beside the kept bytes' gather), so its stream takes the highest priority: its waves are
-  // dispatched first and the gather fills the rest of the machine.
-  if (!c->aux) {
-    int least = 0, greatest = 0;
-    if (!LSMBLK_AUX_PRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-    if (hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, greatest) != hipSuccess) return LSMBLK_E_HIP;
-  }
+  // (normal priority: a highest-priority second stream slowed every later kernel of the process
+  // once several streams were in use)
+  if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) return LSMBLK_E_HIP;
   if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
   if (!c->join_ev && hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) return LSMBLK_E_HIP;
   if (hipEventRecord(c->fork_ev, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess)
