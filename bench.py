@@ -1218,10 +1218,16 @@ def measured_traffic(cfg, kernel, launches=1.0, default_size=True):
     c = tj.get("configs", {}).get(cfg)
     if c is None:
         return None, f"no config {cfg} pass in profiles/traffic.json"
-    if kernel in c.get("bytes_per_launch", {}):
-        return int(c["bytes_per_launch"][kernel]), None
-    if kernel in c.get("kernels", {}):
-        return int(c["kernels"][kernel]["bytes_per_dispatch"] * launches), None
+    # Kernel names are compared without spaces: the kernel log names a template instance as written
+    # in the source (`mwrite_kernel<false,true>`), rocprofv3's demangler with a space after each
+    # comma (`mwrite_kernel<false, true>`) -- VERDICT round 5: config C's traffic was null for it.
+    norm = (lambda k: "".join(str(k).split()))
+    bpl = {norm(k): v for k, v in c.get("bytes_per_launch", {}).items()}
+    kern = {norm(k): v for k, v in c.get("kernels", {}).items()}
+    if norm(kernel) in bpl:
+        return int(bpl[norm(kernel)]), None
+    if norm(kernel) in kern:
+        return int(kern[norm(kernel)]["bytes_per_dispatch"] * launches), None
     return None, f"kernel {kernel} not in the config {cfg} passes"
 
 

@@ -177,6 +177,10 @@ int lsmblk_ctx_reserve(lsmblk_ctx* ctx, uint64_t max_blocks, uint64_t max_entrie
                                        than the plan walk + emit launches) */
 #define LSMBLK_DEBUG_PLAN_PIPE 9 /* 0: the plan walk's helper waits for each chunk's offsets, then its keys
                                     (two round trips per chunk, the default); 1: pipelined over batches */
+#define LSMBLK_DEBUG_EMIT_POISON 10 /* diagnostics builds only (fault injection): 1 = after the plan walk,
+                                       every fifth block's first entry is set past its end entry (a
+                                       block table with e < s, and e > n at the end); emit must report
+                                       LSMBLK_E_INTERNAL and read none of those entries */
 int lsmblk_debug_set(lsmblk_ctx* ctx, int key, uint32_t value);
 /* The trace of the last lagged decode with LSMBLK_DEBUG_COUNTERS on (n <= 16 + 8 * 32768 words;
  * synchronizes).  Words 16 + 8 t + k, 100 MHz s_memrealtime stamps of 64-block tile t: k = 0 tile

@@ -1172,8 +1172,7 @@ __global__ __launch_bounds__(256) void mwrite_kernel(GatherArgs a) {
 __global__ void merge_empty_kernel(uint64_t* mstats, uint32_t* okey_off, uint32_t* oval_off, uint64_t entry_cap,
                                    uint64_t* stats) {
   if (threadIdx.x == 0) {
-    mstats[0] = 0;
-    mstats[1] = 0;
+    mstats[0] = mstats[1] = mstats[3] = mstats[5] = 0;  // (workspace: no stale error word for gate_kernel)
     if (entry_cap + 1 > 0 && okey_off) {
       okey_off[0] = 0;
       oval_off[0] = 0;
@@ -1858,9 +1857,9 @@ MergePlan plan_merge(uint8_t* base, uint64_t n, uint32_t nrun) {
   return P;
 }
 
-int ensure_ws(lsmblk_ctx* c, uint64_t bytes) {
+int ensure_ws(lsmblk_ctx* c, uint64_t bytes, hipStream_t st) {
   if (bytes <= c->cws_cap) return LSMBLK_OK;
-  return grow(&c->cws, &c->cws_cap, bytes, 1);
+  return grow(st, &c->cws, &c->cws_cap, bytes, 1);
 }
 
 // merge + (rules | keep all) + gather into `out`; stats as lsmblk_compact_filter_batch's.
@@ -1871,7 +1870,7 @@ int merge_gather_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32_
                         uint8_t* ksame_out = nullptr, GatherArgs* defer = nullptr) {
   const uint64_t n = in->n;
   MergePlan P = plan_merge(nullptr, n, nrun);
-  int rc = ensure_ws(c, P.bytes);
+  int rc = ensure_ws(c, P.bytes, st);
   if (rc) return rc;
   P = plan_merge(c->cws, n, nrun);
   if (plan_out) *plan_out = P;
@@ -1965,8 +1964,12 @@ __global__ void set_u64_kernel(uint64_t* p, uint64_t v) {
 }
 
 // The kept-entry count the rotation and the encode see: 0 after any merge / rules error.
-__global__ void gate_kernel(const uint64_t* fst, uint64_t* dn) {
-  if (threadIdx.x == 0) *dn = fst[3] ? 0ull : fst[0];
+// The rotation's entry count: the kept entries, or 0 after an error of the rules / gather (fst[3]) or
+// of the merge itself (merr = its mstats[3]: an unsorted run is reported there only).  With 0 the
+// rotation on the second stream reads nothing -- in particular never the kept keys that the byte
+// gather on the caller's stream is still writing.
+__global__ void gate_kernel(const uint64_t* fst, const uint64_t* merr, uint64_t* dn) {
+  if (threadIdx.x == 0) *dn = (fst[3] | *merr) ? 0ull : fst[0];
 }
 
 #ifndef LSMBLK_ROT_HOPS
@@ -2190,7 +2193,7 @@ int lsmblk_shard_rotation_prepare_ex(lsmblk_ctx* c, const lsmblk_kv_stream* ext,
   c->shard_ready = false;
   const uint32_t fl = shard_flevels(sst_cap);
   const RotPlan P0 = plan_rot(nullptr, 0, ext->n, target_sst_size, block_size, fl);
-  int rc = grow(&c->rws, &c->rws_cap, P0.bytes, 1);
+  int rc = grow(st, &c->rws, &c->rws_cap, P0.bytes, 1);
   if (rc) return rc;
   c->shard_n = ext->n;
   c->shard_m = n_own;
@@ -2280,7 +2283,7 @@ int lsmblk_sst_rotation_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint32_
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   RotPlan P = plan_rot(nullptr, 0, in->n, target_sst_size, block_size);
-  int rc = ensure_ws(c, P.bytes);
+  int rc = ensure_ws(c, P.bytes, st);
   if (rc) return rc;
   P = plan_rot(c->cws, 0, in->n, target_sst_size, block_size);
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
@@ -2319,7 +2322,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   MergePlan M = plan_merge(nullptr, n, nrun);
   RotPlan R = plan_rot(nullptr, M.bytes, n, o->target_sst_size, o->block_size);
   const uint64_t stats_off = (R.bytes + 255) & ~uint64_t(255);
-  if ((rc = ensure_ws(c, stats_off + 4 * 64))) return rc;
+  if ((rc = ensure_ws(c, stats_off + 4 * 64, st))) return rc;
   uint64_t* sts = reinterpret_cast<uint64_t*>(c->cws + stats_off);
   uint64_t *fst = sts, *rst = sts + 8, *est = sts + 16;
   if (hipMemsetAsync(sts, 0, 4 * 64, st) != hipSuccess) return LSMBLK_E_HIP;
@@ -2336,7 +2339,7 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
                                 o->nprefix, nullptr, kept, fst, st, &MP, two, LSMBLK_TWO_END_IN_RANGE, nullptr, &G)))
     return rc;
   R = plan_rot(c->cws, M.bytes, n, o->target_sst_size, o->block_size);
-  LSM_LAUNCH(gate_kernel, dim3(1), dim3(64), 0, st, fst, R.dn);
+  LSM_LAUNCH(gate_kernel, dim3(1), dim3(64), 0, st, fst, (const uint64_t*)(MP.m.mstats + 3), R.dn);
   RotArgs r = R.r;
   r.keys = kept->keys;
   r.key_off = kept->key_off;
@@ -2354,9 +2357,13 @@ int lsmblk_compact_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint32
   r.an = n;
   r.poison = c->rot_poison;
   if ((rc = lsmblk_impl::fork_aux(c, st))) return rc;
-  if ((rc = rotation_locked(c, r, c->aux))) return rc;
-  if ((rc = mwrite_bytes(G, n, st))) return rc;
-  if ((rc = lsmblk_impl::join_aux(c, st))) return rc;
+  rc = rotation_locked(c, r, c->aux);
+  if (!rc) rc = mwrite_bytes(G, n, st);
+  // joined on every path once forked: after an error the caller's stream still
+  // waits for the rotation work already queued on c->aux, which writes sst_start and the workspace
+  const int jrc = lsmblk_impl::join_aux(c, st);
+  if (rc) return rc;
+  if (jrc) return jrc;
   lsmblk_kv_stream ks = *kept;
   ks.n = n;  // bound; the encode reads the kept count from fst[0]
   if ((rc = lsmblk_impl::encode_locked(c, &ks, R.dn, sst_start, r.nsst, sst_cap - 1, o->block_size, out, out_cap,

@@ -1314,9 +1314,11 @@ __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
 // First byte of segment g's slot in the per-segment output (LSMBLK_ENCODE_SEG_SLOTS): the keys and
 // values of the segments before it plus 18 bytes per entry, an upper bound of their encoded size
 // (encode_fused_kernel).
-__device__ __forceinline__ uint64_t seg_slot(const uint32_t* key_off, const uint32_t* val_off, const uint32_t* seg_start,
-                                             uint32_t g) {
-  const uint32_t b = seg_start[0], s = seg_start[g];
+// Callers pass validated entry indices b = seg_start[0] and s = seg_start[g] (b <= s <= n): the
+// table's raw entries are never used as array indices here (a table like
+// [0, 0xFFFFFFFF, n] made the walker of segment 1 read key_off[0xFFFFFFFF] after flagging it).
+__device__ __forceinline__ uint64_t seg_slot(const uint32_t* key_off, const uint32_t* val_off, uint32_t b, uint32_t s) {
+  if (s <= b) return 0;
   return uint64_t(key_off[s] - key_off[b]) + uint64_t(val_off[s] - val_off[b]) + 18ull * (s - b);
 }
 
@@ -1856,7 +1858,11 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     const uint64_t inc[2] = {excl[0] + agg[0], excl[1] + agg[1]};
     publish<2>(a.inc, g, inc, a.tag, 2, a.poll);
   }
-  const uint64_t B0 = excl[0], O0 = a.seg_out ? seg_slot(a.key_off, a.val_off, a.seg_start, g) : excl[1];
+  // slot mode: segment 0 starts at 0 (checked by its own walker, err SEGMENTS otherwise); a
+  // segment whose own bounds were refused gets slot 0 and writes nothing (emit: kPlanFatal)
+  uint64_t O0 = excl[1];
+  if (a.seg_out) O0 = (err & LSMBLK_ERR_SEGMENTS) ? 0ull : seg_slot(a.key_off, a.val_off, 0u, s0);
+  const uint64_t B0 = excl[0];
   if (a.seg_out && l == 0) {
     a.seg_out[2ull * g] = O0;
     a.seg_out[2ull * g + 1] = bytes;
@@ -1983,6 +1989,7 @@ struct EmitMeta {
   uint32_t s, e, n;
   uint64_t O, size;
   uint32_t kb0, kb1, vb0, vb1;
+  bool bad;  // the block table entry is not s <= e <= n: refused (LSMBLK_ERR_INTERNAL), never read
 };
 
 // The plan's error flags that leave its block tables unusable: emit then writes nothing (a
@@ -2188,10 +2195,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   // they wait on lgkmcnt, not behind the staging loads in flight
   cu32_t* const kfirst = kconst(a.blk_first);
   cu64_t* const koff = kconst(a.blk_off);
+  // A block whose entry range is not s <= e <= n is refused with LSMBLK_ERR_INTERNAL and none of
+  // its entries is read: its wrapped entry count would otherwise send it to emit_big_kernel's
+  // per-entry walk, ~2^32 entries of unchecked global loads (the single-block emit
+  // experiment's illegal address).  A valid plan never writes such a block.
   auto meta1 = [&](uint64_t bi, EmitMeta& m) {
     m.bi = bi;
     m.s = kfirst[bi];
     m.e = kfirst[bi + 1];
+    m.bad = m.e < m.s || uint64_t(m.e) > a.n;
+    if (m.bad) m.s = m.e = 0;  // (meta2's loads stay in bounds)
     m.n = m.e - m.s;
     m.O = koff[bi];
     m.size = a.blk_sz ? uint64_t(kconst(a.blk_sz)[bi]) : koff[bi + 1] - m.O;
@@ -2205,8 +2218,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   auto is_fast = [&](const EmitMeta& m) {
     const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
     // the staged values and the encoded block share the image (24 B of read slack)
-    return m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
+    return !m.bad && m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
            vlead + (m.vb1 - m.vb0) + 24 <= kEmitICap && uint32_t(m.O & 15) + m.size + 8 <= kEmitICap;
+  };
+  // a block off the fast path: beyond the LDS image -> flagged for emit_big_kernel; refused -> error
+  auto not_fast = [&](const EmitMeta& m) {
+    if (m.bad) err |= LSMBLK_ERR_INTERNAL;
+    else if (l == 0) a.big_flag[m.bi] = 1;
   };
   u32x4 kq[2], vq[5];
   EmitPf pf;
@@ -2242,7 +2260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       meta1(bi, m);
       meta2(m);
       if (is_fast(m)) return true;
-      if (l == 0) a.big_flag[bi] = 1;
+      not_fast(m);
     }
     return false;
   };
@@ -2305,7 +2323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       nxt.vb0 = uni(r_vb0);
       nxt.vb1 = uni(r_vb1);
       if (!is_fast(nxt)) {
-        if (l == 0) a.big_flag[nxt.bi] = 1;
+        not_fast(nxt);
         has_next = find_fast(nxt.bi + nwaves, nxt);
       }
       if (has_next) issue(nxt);
@@ -2334,22 +2352,31 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   const rsrc_t RK = make_rsrc(a.keys - kg, klim), RV = make_rsrc(a.vals - vg, vlim);
   // this wave's flagged blocks, in order
   uint64_t wbase = uint64_t(blockIdx.x) * 4 + wave_id(), cbase = 0, bits = 0;
+  // (a flagged block whose entry range is not s <= e <= n is refused with LSMBLK_ERR_INTERNAL, as in
+  // emit_kernel: a wrapped entry count would walk ~2^32 entries of unchecked global loads)
   auto next_block = [&](BigBlk& B) -> bool {
-    while (bits == 0) {
-      if (wbase >= lim) return false;
-      const uint64_t mine = wbase + nw * l;
-      bits = __ballot(mine < lim && a.big_flag[mine]);
-      cbase = wbase;
-      wbase += nw * 64;
+    for (;;) {
+      while (bits == 0) {
+        if (wbase >= lim) return false;
+        const uint64_t mine = wbase + nw * l;
+        bits = __ballot(mine < lim && a.big_flag[mine]);
+        cbase = wbase;
+        wbase += nw * 64;
+      }
+      const uint32_t i = uint32_t(__builtin_ctzll(bits));
+      bits &= bits - 1;
+      B.bi = cbase + nw * i;
+      B.s = uni(a.blk_first[B.bi]);
+      const uint32_t e = uni(a.blk_first[B.bi + 1]);
+      if (e < B.s || uint64_t(e) > a.n) {
+        err |= LSMBLK_ERR_INTERNAL;
+        continue;
+      }
+      B.n = e - B.s;
+      B.O = uni64(a.blk_off[B.bi]);
+      B.size = a.blk_sz ? uint64_t(uni(a.blk_sz[B.bi])) : uni64(a.blk_off[B.bi + 1]) - B.O;
+      return true;
     }
-    const uint32_t i = uint32_t(__builtin_ctzll(bits));
-    bits &= bits - 1;
-    B.bi = cbase + nw * i;
-    B.s = uni(a.blk_first[B.bi]);
-    B.n = uni(a.blk_first[B.bi + 1]) - B.s;
-    B.O = uni64(a.blk_off[B.bi]);
-    B.size = a.blk_sz ? uint64_t(uni(a.blk_sz[B.bi])) : uni64(a.blk_off[B.bi + 1]) - B.O;
-    return true;
   };
   auto issue_l1 = [&](const BigBlk& B, uint32_t c) -> BigL1 {
     BigL1 x{0u, 0u, 0u, 0u};
@@ -2493,6 +2520,16 @@ __global__ __launch_bounds__(256) void emit_big_kernel(EmitArgs a0) {
   raise_err(a.stats, err);
 }
 
+// Fault injection (LSMBLK_DEBUG_EMIT_POISON, diagnostics builds): after the plan walk, block b = 1,
+// 6, 11, ... gets first entry blk_first[b + 1] + 1, so block b's end precedes its start and block
+// b - 1 ends one entry later (past n when b is the last block).  Thread t writes only b = 1 + 5 t
+// and reads only b + 1, which no thread writes.
+__global__ __launch_bounds__(256) void emit_poison_kernel(uint32_t* blk_first, const uint64_t* stats) {
+  if (stats[3] & kPlanFatal) return;
+  const uint64_t nblk = stats[0], b = 1 + 5 * (uint64_t(blockIdx.x) * 256 + threadIdx.x);
+  if (b < nblk) blk_first[b] = blk_first[b + 1] + 1;
+}
+
 // ================================================================ encode: fused walk + emit
 // LSMBLK_ENCODE_SEG_SLOTS (per-segment output) with blocks no larger than emit's LDS image, under
 // LSMBLK_DEBUG_ENCODE_FUSED: the plan walk and emit run in one launch.  Measured (DESIGN.md section
@@ -2577,7 +2614,7 @@ __device__ void fuse_walk(const FuseArgs& f, uint32_t* ring) {
   if (tr && l == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
   for (uint32_t g = g0; ok && g < g1; ++g) {
     const uint32_t s0 = uni(a.seg_start[g]), s1 = uni(a.seg_start[g + 1]);
-    const uint64_t slot = seg_slot(a.key_off, a.val_off, a.seg_start, g);
+    const uint64_t slot = seg_slot(a.key_off, a.val_off, 0u, s0);  // (ok: seg_start[0] = 0, s0 <= n)
     uint32_t nb = 0;
     uint64_t bytes = 0;
     walk_segment(a, K, R, s0, s1, err, nb, bytes,
@@ -2652,6 +2689,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
         m.bi = x;
         m.s = uint32_t(lane64(g, 0) >> 16);
         m.e = uint32_t(lane64(g, 1) >> 16);
+        m.bad = false;  // (the walker's own records: s < e <= n)
         m.n = m.e - m.s;
         m.O = lane64(g, 2) >> 16;
         m.size = lane64(g, 3) >> 16;
@@ -3718,25 +3756,25 @@ namespace {
 // per block 3 aggregate + 3 base granules; per tile 3 aggregate + 3 inclusive granules
 uint64_t lag_words(uint64_t nb) { return 6 * nb + 6 * ((nb + kTile - 1) / kTile + 1); }
 
-int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t segs) {
+int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t segs, hipStream_t st) {
   int rc;
   uint64_t cap;
   if (blocks > c->dec_cap) {
-    if ((rc = grow(&c->dec_agg, &c->dec_cap, blocks, 3))) return rc;
+    if ((rc = grow(st, &c->dec_agg, &c->dec_cap, blocks, 3))) return rc;
   }
   const uint64_t tiles = (blocks + kTile - 1) / kTile;
   if (tiles > c->tile_cap) {
     cap = c->tile_cap;
-    if ((rc = grow(&c->tile_sum, &cap, tiles, 3))) return rc;
+    if ((rc = grow(st, &c->tile_sum, &cap, tiles, 3))) return rc;
     cap = c->tile_cap;
-    if ((rc = grow(&c->tile_pre, &cap, tiles, 3))) return rc;
+    if ((rc = grow(st, &c->tile_pre, &cap, tiles, 3))) return rc;
     c->tile_cap = cap;
   }
   if (blocks > c->lag_blk_cap) {
     // one arena: per block 3 aggregate + 3 base granules, then per tile 3 aggregate + 3 inclusive
     const uint64_t nb = blocks + blocks / 4 + 1024;
     cap = 0;  // (grow frees the old arena)
-    if ((rc = grow(&c->lag_gran, &cap, lag_words(nb), 1, kStatusFlags))) {
+    if ((rc = grow(st, &c->lag_gran, &cap, lag_words(nb), 1, kStatusFlags))) {
       c->lag_blk_cap = 0;
       return rc;
     }
@@ -3745,23 +3783,23 @@ int reserve_locked(lsmblk_ctx* c, uint64_t blocks, uint64_t entries, uint64_t se
   }
   if (segs > c->seg_cap) {
     cap = c->seg_cap;
-    if ((rc = grow(&c->seg_agg, &cap, segs, 2, kStatusFlags))) return rc;
+    if ((rc = grow(st, &c->seg_agg, &cap, segs, 2, kStatusFlags))) return rc;
     cap = c->seg_cap;
-    if ((rc = grow(&c->seg_inc, &cap, segs, 2, kStatusFlags))) return rc;
+    if ((rc = grow(st, &c->seg_inc, &cap, segs, 2, kStatusFlags))) return rc;
     c->seg_cap = cap;
     c->epoch = 0;
   }
   if (entries + 1 > c->rec_cap) {
     cap = c->rec_cap;
-    if ((rc = grow(&c->rec_first, &cap, entries + 1, 1))) return rc;
+    if ((rc = grow(st, &c->rec_first, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
-    if ((rc = grow(&c->blk_first, &cap, entries + 1, 1))) return rc;
+    if ((rc = grow(st, &c->blk_first, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
-    if ((rc = grow(&c->ent, &cap, entries + 1, 1))) return rc;
+    if ((rc = grow(st, &c->ent, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
-    if ((rc = grow(&c->big_list, &cap, entries + 1, 1))) return rc;
+    if ((rc = grow(st, &c->big_list, &cap, entries + 1, 1))) return rc;
     cap = c->rec_cap;
-    if ((rc = grow(&c->blk_sz, &cap, entries + 1, 1))) return rc;
+    if ((rc = grow(st, &c->blk_sz, &cap, entries + 1, 1))) return rc;
     c->rec_cap = cap;
   }
   return LSMBLK_OK;
@@ -3817,33 +3855,34 @@ void lsmblk_ctx_destroy(lsmblk_ctx* c) {
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
   if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipFree(c->counters);
-  (void)hipFree(c->dec_agg);
-  (void)hipFree(c->tile_sum);
-  (void)hipFree(c->tile_pre);
-  (void)hipFree(c->seg_agg);
-  (void)hipFree(c->seg_inc);
-  (void)hipFree(c->rec_first);
-  (void)hipFree(c->ent);
-  (void)hipFree(c->big_list);
-  (void)hipFree(c->blk_sz);
-  (void)hipFree(c->frec);
-  (void)hipFree(c->fdone);
-  (void)hipFree(c->fwnb);
-  (void)hipFree(c->fbig);
-  (void)hipFree(c->blk_first);
+  release(c->dec_agg);
+  release(c->tile_sum);
+  release(c->tile_pre);
+  release(c->seg_agg, kStatusFlags);
+  release(c->seg_inc, kStatusFlags);
+  release(c->rec_first);
+  release(c->ent);
+  release(c->big_list);
+  release(c->blk_sz);
+  release(c->frec, kStatusFlags);
+  release(c->fdone, kStatusFlags);
+  release(c->fwnb);
+  release(c->fbig);
+  release(c->blk_first);
   (void)hipFree(c->crc_tabs);
-  (void)hipFree(c->meta_rec);
-  (void)hipFree(c->meta_pos);
-  (void)hipFree(c->meta_tile);
-  (void)hipFree(c->meta_crc);
+  release(c->meta_rec);
+  release(c->meta_pos);
+  release(c->meta_tile);
+  release(c->meta_crc);
   (void)hipFree(c->meta_cstats);
-  (void)hipFree(c->filt_keep);
-  (void)hipFree(c->filt_tile);
-  (void)hipFree(c->cws);
-  (void)hipFree(c->vcrc);
-  (void)hipFree(c->sws);
-  (void)hipFree(c->rws);
-  (void)hipFree(c->lag_gran);
+  release(c->filt_keep);
+  release(c->filt_tile);
+  release(c->cws);
+  release(c->vcrc);
+  release(c->sws);
+  release(c->rws);
+  release(c->lag_gran, kStatusFlags);
+  (void)hipStreamSynchronize(nullptr);  // (the pool frees above were queued on the null stream)
   (void)hipFree(c->dbg);
   for (auto& e : c->klog) {
     if (e.e0) (void)hipEventDestroy(e.e0);
@@ -3872,6 +3911,8 @@ int lsmblk_debug_set(lsmblk_ctx* c, int key, uint32_t value) {
     c->dbg_on = value != 0;
   } else if (key == LSMBLK_DEBUG_ROT_POISON && kDiag) {  // fault injection: diagnostics builds only
     c->rot_poison = value;
+  } else if (key == LSMBLK_DEBUG_EMIT_POISON && kDiag) {  // fault injection: diagnostics builds only
+    c->emit_poison = value;
   } else if (key == LSMBLK_DEBUG_DECODE_LAG_BYTES) {
     c->dec_lag_bytes = value;
   } else if (key == LSMBLK_DEBUG_DECODE_LAG && value == 0) {  // the default
@@ -3961,7 +4002,10 @@ int lsmblk_ctx_reserve(lsmblk_ctx* c, uint64_t max_blocks, uint64_t max_entries,
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
-  return reserve_locked(c, max_blocks, max_entries, max_segments);
+  // (on the null stream, completed before returning: a later call may come on any stream)
+  const int rc = reserve_locked(c, max_blocks, max_entries, max_segments, nullptr);
+  if (rc) return rc;
+  return hipStreamSynchronize(nullptr) == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
 int lsmblk_decode_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk,
@@ -3980,7 +4024,7 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int rc = reserve_locked(c, nblk, 0, 0);
+  int rc = reserve_locked(c, nblk, 0, 0, st);
   if (rc) return rc;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nblk == 0) {
@@ -3990,8 +4034,8 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   }
   if (flags & LSMBLK_DECODE_VERIFY_CRC) {
     // read_block's checksum test (src/table.rs:226-230) over the framed ranges, then the decode
-    if ((rc = lsmblk_impl::ensure_crc_tabs(c))) return rc;
-    if ((rc = grow(&c->vcrc, &c->vcrc_cap, nblk + 1, 1))) return rc;
+    if ((rc = lsmblk_impl::ensure_crc_tabs(c, st))) return rc;
+    if ((rc = grow(st, &c->vcrc, &c->vcrc_cap, nblk + 1, 1))) return rc;
     if (!c->meta_cstats && hipMalloc(reinterpret_cast<void**>(&c->meta_cstats), LSMBLK_STATS_WORDS * 8) != hipSuccess) {
       c->meta_cstats = nullptr;
       return LSMBLK_E_NOMEM;
@@ -4121,7 +4165,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   const bool slots = (flags & LSMBLK_ENCODE_SEG_SLOTS) != 0;
   if (slots && (!seg_out || span || dn || dnseg)) return LSMBLK_E_INVAL;
   // in->n (and nseg) are upper bounds when dn (dnseg) point at the device-side values
-  int rc = reserve_locked(c, 0, in->n, nseg);
+  int rc = reserve_locked(c, 0, in->n, nseg, st);
   if (rc) return rc;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nseg == 0) {
@@ -4142,10 +4186,10 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
     nwalk = 2 * walk_wgs;
     const uint64_t recs = in->n + nwalk + 1;
     const uint64_t fc = c->frec_cap, dc = c->fdone_cap;
-    if ((rc = grow(&c->frec, &c->frec_cap, recs, 4, kStatusFlags))) return rc;
-    if ((rc = grow(&c->fdone, &c->fdone_cap, nwalk, 1, kStatusFlags))) return rc;
-    if ((rc = grow(&c->fwnb, &c->fwnb_cap, nwalk, 1))) return rc;
-    if ((rc = grow(&c->fbig, &c->fbig_cap, recs, 1))) return rc;
+    if ((rc = grow(st, &c->frec, &c->frec_cap, recs, 4, kStatusFlags))) return rc;
+    if ((rc = grow(st, &c->fdone, &c->fdone_cap, nwalk, 1, kStatusFlags))) return rc;
+    if ((rc = grow(st, &c->fwnb, &c->fwnb_cap, nwalk, 1))) return rc;
+    if ((rc = grow(st, &c->fbig, &c->fbig_cap, recs, 1))) return rc;
     if (c->frec_cap != fc || c->fdone_cap != dc) c->epoch = 0;  // fresh granules: a new epoch sequence
   }
   if ((rc = next_epoch(c, st))) return rc;
@@ -4220,6 +4264,8 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
     if (c->skip & (3u << 16)) {  // plan ablation: the block tables are wrong, emit is not launched
       return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
     }
+    if (kDiag && c->emit_poison)  // fault injection (diagnostics builds): a corrupt block table
+      LSM_LAUNCH(emit_poison_kernel, dim3(uint32_t(in->n / (5 * 256) + 1)), dim3(256), 0, st, c->blk_first, stats);
     // the big-block flags are cleared before emit (the start of emit_kernel to the end of
     // emit_big_kernel is what bench.py's roofline divides by)
     const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;  // blocks <= entries, <= blk_cap
@@ -4255,9 +4301,9 @@ int lsmblk_crc32_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device, c);
   if (!dg.ok) return LSMBLK_E_HIP;
-  int rc = lsmblk_impl::ensure_crc_tabs(c);
-  if (rc) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int rc = lsmblk_impl::ensure_crc_tabs(c, st);
+  if (rc) return rc;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   if (nblk == 0) return LSMBLK_OK;
   return lsmblk_impl::launch_crc(c, blocks, blk_off, nblk, tail, crc, stats, st);
@@ -4294,18 +4340,18 @@ namespace lsmblk_impl {
 int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                       const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off,
                       uint64_t* stats, hipStream_t st) {
-  int rc = lsmblk_impl::ensure_crc_tabs(c);
+  int rc = lsmblk_impl::ensure_crc_tabs(c, st);
   if (rc) return rc;
   const uint64_t ntiles = (nblk + kMetaTile - 1) / kMetaTile;
   if (nblk + 1 > c->meta_blk_cap) {
     uint64_t cap = c->meta_blk_cap;
-    if ((rc = grow(&c->meta_rec, &cap, nblk + 1, 1))) return rc;
+    if ((rc = grow(st, &c->meta_rec, &cap, nblk + 1, 1))) return rc;
     cap = c->meta_blk_cap;
-    if ((rc = grow(&c->meta_pos, &cap, nblk + 1, 1))) return rc;
+    if ((rc = grow(st, &c->meta_pos, &cap, nblk + 1, 1))) return rc;
     c->meta_blk_cap = cap;
   }
-  if ((rc = grow(&c->meta_tile, &c->meta_tile_cap, ntiles + 1, 2))) return rc;
-  if ((rc = grow(&c->meta_crc, &c->meta_seg_cap, nseg, 1))) return rc;
+  if ((rc = grow(st, &c->meta_tile, &c->meta_tile_cap, ntiles + 1, 2))) return rc;
+  if ((rc = grow(st, &c->meta_crc, &c->meta_seg_cap, nseg, 1))) return rc;
   if (!c->meta_cstats && hipMalloc(reinterpret_cast<void**>(&c->meta_cstats), LSMBLK_STATS_WORDS * 8) != hipSuccess) {
     c->meta_cstats = nullptr;
     return LSMBLK_E_NOMEM;
@@ -4356,9 +4402,9 @@ int lsmblk_compact_filter_batch(lsmblk_ctx* c, const lsmblk_kv_stream* in, uint6
   if (!dg.ok) return LSMBLK_E_HIP;
   const uint64_t n = in->n, ntiles = (n + kFiltTile - 1) / kFiltTile;
   int rc;
-  if ((rc = grow(&c->filt_keep, &c->filt_cap, n + 1, 1))) return rc;
-  if ((rc = grow(&c->filt_tile, &c->filt_tile_cap, ntiles + 1, 6))) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if ((rc = grow(st, &c->filt_keep, &c->filt_cap, n + 1, 1))) return rc;
+  if ((rc = grow(st, &c->filt_tile, &c->filt_tile_cap, ntiles + 1, 6))) return rc;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;
   FiltArgs a;
   a.keys = in->keys;
@@ -4410,23 +4456,26 @@ int join_aux(lsmblk_ctx* c, hipStream_t st) {
   return LSMBLK_OK;
 }
 
-int ensure_crc_tabs(lsmblk_ctx* c) {
+int ensure_crc_tabs(lsmblk_ctx* c, hipStream_t st) {
   if (c->crc_tabs) return LSMBLK_OK;
-  static CrcAllTabs h;  // (built once per process: the stream tables take ~40 M bit steps)
+  static CrcAllTabs h;  // (built once per process: the stream tables take ~40 M bit steps; never written after)
   static std::once_flag once;
   std::call_once(once, [] {
     crc_host_tables(h.t);
     crc_stream_host_tables(h.s);
   });
-  if (hipMalloc(reinterpret_cast<void**>(&c->crc_tabs), sizeof(CrcAllTabs)) != hipSuccess) {
-    c->crc_tabs = nullptr;
-    return LSMBLK_E_NOMEM;
+  void* d = nullptr;
+  if (hipMalloc(&d, sizeof(CrcAllTabs)) != hipSuccess) return LSMBLK_E_NOMEM;
+  // Copied on the call's stream and waited for there (first use only; a later call of the context
+  // may come on another stream).  On any failure the tables are freed and c->crc_tabs stays null,
+  // so no later call runs the CRC kernels over tables that were never filled.
+  if (hipMemcpyAsync(d, &h, sizeof(CrcAllTabs), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    (void)hipFree(d);
+    return LSMBLK_E_HIP;
   }
-  // (a null-stream copy: completed before the first CRC kernel on the caller's stream can read it)
-  return hipMemcpy(c->crc_tabs, &h, sizeof(CrcAllTabs), hipMemcpyHostToDevice) == hipSuccess &&
-                 hipDeviceSynchronize() == hipSuccess
-             ? LSMBLK_OK
-             : LSMBLK_E_HIP;
+  c->crc_tabs = d;
+  return LSMBLK_OK;
 }
 
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,

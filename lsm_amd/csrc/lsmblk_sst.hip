@@ -537,7 +537,7 @@ int lsmblk_sst_files_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
   if (!dg.ok) return LSMBLK_E_HIP;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;
-  if ((rc = lsmblk_impl::ensure_crc_tabs(c))) return rc;
+  if ((rc = lsmblk_impl::ensure_crc_tabs(c, st))) return rc;
   // workspace: block CRCs, BlockMeta sections, section offsets, data-section lengths, stats
   struct Ws {
     uint32_t* crc;
@@ -571,7 +571,7 @@ int lsmblk_sst_files_batch(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t*
     meta_bytes += 2ull * karena;
   }
   const uint64_t need = carve(nullptr, meta_bytes, w);
-  if (need > c->sws_cap && (rc = grow(&c->sws, &c->sws_cap, need, 1))) return rc;
+  if (need > c->sws_cap && (rc = grow(st, &c->sws, &c->sws_cap, need, 1))) return rc;
   carve(c->sws, meta_bytes, w);
   if (hipMemsetAsync(w.st, 0, 8 * 12, st) != hipSuccess) return LSMBLK_E_HIP;
   if (hipMemsetAsync(stats, 0, LSMBLK_STATS_WORDS * 8, st) != hipSuccess) return LSMBLK_E_HIP;

@@ -798,7 +798,10 @@ def test_slot_encode_refuses_bad_segment_tables(fused):
     kv = O.KV(*synth.gen_uniform(3000, seed=12))
     d = to_dev(kv)
     n = kv.n
-    for seg in ([5, n], [0, 2000, 1000, n], [0, 1000, n - 1], [0, 1000, n + 7]):
+    # (the last two: an interior / first entry far past n, which the slot of a segment must never
+    # use as an index -- ADVICE round 5)
+    for seg in ([5, n], [0, 2000, 1000, n], [0, 1000, n - 1], [0, 1000, n + 7], [0, 0xFFFFFFFF, n],
+                [0xFFFFFFF0, n]):
         status, *_ = _slot_encode_raw(d, seg, 4096, fused=fused)
         assert status == LSMBLK_E_INVAL, seg
         if not fused:  # the packed encode

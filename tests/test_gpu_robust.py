@@ -79,3 +79,63 @@ def test_corrupt_rotation_levels_report_internal_not_hang():
     assert res["compact"] == LSMBLK_E_INTERNAL, res
     assert res["shard"] == LSMBLK_E_INTERNAL, res
     assert res["rotation_after"], res
+
+
+EMIT_CHILD = r"""
+import json, sys
+import numpy as np
+import torch
+sys.path.insert(0, %(root)r)
+from lsm_amd import batch, synth
+from lsm_amd._lib import lib, LsmBlkError
+from oracle import oracle as O
+
+POISON = 10  # LSMBLK_DEBUG_EMIT_POISON
+out = {}
+kv = O.KV(*synth.gen_uniform(60000, seed=21))
+seg = [0, 20000, 40000, kv.n]
+rc, ref_blocks, ref_off = O.encode_segments(kv, seg, 4096)
+assert rc == 0
+d = batch.KVStream.from_numpy(kv.keys, kv.key_off, kv.vals, kv.val_off, kv.ts)
+
+def status(fn):
+    try:
+        fn()
+        return 0
+    except LsmBlkError as e:
+        return e.status
+
+h = batch._ctx(0)
+assert lib().lsmblk_debug_set(h, POISON, 1) == 0
+out["packed"] = status(lambda: batch.encode_kv(d, seg, 4096))
+out["slots"] = status(lambda: batch.encode_kv_slots(d, seg, 4096))
+assert lib().lsmblk_debug_set(h, POISON, 0) == 0
+blocks, off = batch.encode_kv(d, seg, 4096)
+out["packed_after"] = bool(np.array_equal(blocks.cpu().numpy(), ref_blocks) and
+                           np.array_equal(off.cpu().numpy(), np.asarray(ref_off, np.int64)))
+ob, oo, so = batch.encode_kv_slots(d, seg, 4096)
+pb, po = batch.slots_to_packed(ob, oo, so)
+out["slots_after"] = bool(np.array_equal(pb.cpu().numpy(), ref_blocks))
+torch.cuda.synchronize()
+print(json.dumps(out))
+"""
+
+
+def test_corrupt_block_table_refused_by_emit():
+    """a block table whose end entry precedes its start (or lies past n) --
+    what a raced or stale plan table looks like, and what sent the round-5 single-block emit
+    experiment's emit_big walk into ~2^32 entries of unchecked loads -- is refused by emit_kernel
+    and emit_big_kernel with LSMBLK_E_INTERNAL, none of its entries read.  The table is corrupted by
+    the diagnostics library's LSMBLK_DEBUG_EMIT_POISON after the plan walk; then the same context
+    encodes the oracle's bytes again, packed and with per-segment slots."""
+    from lsm_amd import _build
+    from lsm_amd._lib import LSMBLK_E_INTERNAL
+    _build.build(diag=True)
+    env = dict(os.environ, LSMBLK_SO_OVERRIDE=_build.DIAG_SO)
+    r = subprocess.run([sys.executable, "-c", EMIT_CHILD % {"root": ROOT}], env=env, cwd=ROOT, capture_output=True,
+                       text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["packed"] == LSMBLK_E_INTERNAL, res
+    assert res["slots"] == LSMBLK_E_INTERNAL, res
+    assert res["packed_after"] and res["slots_after"], res
