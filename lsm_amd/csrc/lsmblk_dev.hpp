@@ -323,7 +323,21 @@ __device__ __forceinline__ void store_chunk(uint8_t* dst, const uint32_t (&v)[4]
 //     and 16..31 the tail: one predicated byte store for both.
 // (Per-lane byte-masked edge stores inside the chunk loop compiled to ~15 exec-mask branches per
 // unrolled chunk, every round that held an edge: the scalar unit is the decode's busiest pipe.)
-template <uint32_t B>
+// Store policy of a whole-chunk flush store: 0 nt (keeps the line in the XCD's L2), 1 sc1
+// (write-through: the line leaves L2, MI355X_MICROARCH.md), 2 plain.
+#ifndef LSMBLK_XDEC_STORE
+#define LSMBLK_XDEC_STORE 0
+#endif
+template <int POL>
+__device__ __forceinline__ void st_chunk16(uint8_t* dst, const u32x4& q) {
+  if constexpr (POL == 1)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(q) : "memory");
+  else if constexpr (POL == 2)
+    *reinterpret_cast<u32x4*>(dst) = q;
+  else
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(dst));
+}
+template <uint32_t B, int POL = 0>
 __device__ __forceinline__ void flush_chunks(uint8_t* gdst_aligned, const uint8_t* lds, uint32_t lo, uint32_t len,
                                              uint32_t tid, uint32_t nthr) {
   if (len == 0) return;
@@ -344,8 +358,7 @@ __device__ __forceinline__ void flush_chunks(uint8_t* gdst_aligned, const uint8_
         if (c0 + nthr * j + tid < nw) q[j] = *reinterpret_cast<const u32x4*>(lds + 16 * (cf + c0 + nthr * j + tid));
 #pragma unroll
       for (uint32_t j = 0; j < B; ++j)
-        if (c0 + nthr * j + tid < nw)
-          __builtin_nontemporal_store(q[j], reinterpret_cast<u32x4*>(gdst_aligned + 16 * (cf + c0 + nthr * j + tid)));
+        if (c0 + nthr * j + tid < nw) st_chunk16<POL>(gdst_aligned + 16 * (cf + c0 + nthr * j + tid), q[j]);
     }
   }
 }

@@ -353,7 +353,7 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
 // gdst_aligned + lo, the LDS run mirroring the global 16-B alignment (flush_chunks).
 template <uint32_t B = kLB>
 __device__ __forceinline__ void flush_run(uint8_t* gdst_aligned, const uint8_t* lds, uint32_t lo, uint32_t len) {
-  flush_chunks<B>(gdst_aligned, lds, lo, len, lane_id(), 64);
+  flush_chunks<B, LSMBLK_XDEC_STORE>(gdst_aligned, lds, lo, len, lane_id(), 64);
 }
 
 // The same flush with the edge chunks byte-masked inside the chunk loop (emit: its register
