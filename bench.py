@@ -381,6 +381,8 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
     result["framing_meta"] = framing_meta(pk_blocks, pk_off, nblk, seg_t, st_enc, dev, stream)
     result["compaction_filter"] = compaction_filter(out_kv, n, K, V, dev, stream)
     result["encode_slots"] = encode_slots(out_kv, seg_t, len(seg) - 1, bs, blocks, blk_off, dev, stream)
+    result["encode_framed"] = encode_framed(out_kv, seg_t, len(seg) - 1, bs, blocks, blk_off, dev, stream,
+                                            round(enc_ms, 4))
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(blocks, blk_off, seg, bs, args.cpu_seconds)
     if not args.no_pcie and world == 1:
@@ -1124,6 +1126,55 @@ def encode_slots(kv, seg_t, nseg, bs, blocks, blk_off, dev, stream, reps=5):
         ok = torch.equal(pb, blocks) and torch.equal(po, blk_off)
     return {"call": "lsmblk_encode_batch_ex(LSMBLK_ENCODE_SEG_SLOTS)", "ms": round(ms, 4), "segments": nseg,
             "packed_equal_input": bool(ok)}
+
+
+def encode_framed(kv, seg_t, nseg, bs, blocks, blk_off, dev, stream, enc_ms, reps=5):
+    """Re-encode as SST data sections (LSMBLK_ENCODE_FRAMED: every block followed by its BE
+    crc32fast, SsTableBuilder::finish_block, reference src/table/builder.rs:112-123): encode ms (HIP
+    events over reps calls) beside the unframed encode's; checked by the verifying framed decode
+    (every CRC recomputed on the GPU and compared, tail 4), its KV stream == the step's decoded
+    one, the framed offsets == the input's + 4 per block, and 256 sampled CRCs == zlib.  Not part
+    of `value`."""
+    import zlib
+    K, V = kv.byte_sizes()
+    n = kv.n
+    out_cap, blk_cap = K + V + 22 * n + 16, blk_off.numel() + 1
+    out = batch._aligned_empty(out_cap, dev)
+    off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    st = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def run():
+        batch.encode_into(kv, seg_t, nseg, bs, out, out_cap, off, blk_cap, st, stream=stream, framed=True)
+    run()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        run()
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    s = st.cpu().tolist()
+    nblk = blk_off.numel() - 1
+    ok = s[3] == 0 and s[0] == nblk and s[1] == int(blk_off[-1].item()) + 4 * nblk
+    if ok:
+        fo = off[:nblk + 1]
+        ok = torch.equal(fo, blk_off + 4 * torch.arange(nblk + 1, dtype=torch.int64, device=dev))
+    if ok:
+        dkv = batch.decode_blocks(out[:s[1]], fo, stream=stream, tail=4, verify=True)
+        ok = dkv.n == n and all(torch.equal(getattr(dkv, f)[:m], getattr(kv, f)[:m])
+                                for f, m in (("key_off", n + 1), ("val_off", n + 1), ("ts", n), ("keys", K),
+                                             ("vals", V)))
+        del dkv
+    if ok:
+        fh, bo = fo.cpu().numpy(), blk_off.cpu().numpy()
+        for i in np.linspace(0, nblk - 1, 256).astype(np.int64).tolist():
+            blk = blocks[bo[i]:bo[i + 1]].cpu().numpy().tobytes()
+            crc = out[fh[i + 1] - 4:fh[i + 1]].cpu().numpy().tobytes()
+            ok = ok and crc == zlib.crc32(blk).to_bytes(4, "big")
+    return {"call": "lsmblk_encode_batch_ex(LSMBLK_ENCODE_FRAMED)", "ms": round(ms, 4),
+            "unframed_encode_ms": enc_ms, "framing_cost_ms": round(ms - enc_ms, 4),
+            "gib_s": round((int(blk_off[-1].item()) + 4 * nblk) / (ms * 1e-3) / 2 ** 30, 2),
+            "verified": bool(ok)}
 
 
 def compaction_filter(kv, n, K, V, dev, stream, reps=5):

@@ -243,6 +243,16 @@ int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint3
  * next starts unless it is its segment's last (then at seg_out[2 s] + seg_out[2 s + 1]);
  * blk_off[nblk] = the end of the last segment.  stats[1] = the encoded bytes (their sum). */
 #define LSMBLK_ENCODE_SEG_SLOTS 1u
+/* LSMBLK_ENCODE_FRAMED writes every block followed by its crc32fast as a big-endian u32 -- the SST
+ * data section exactly as SsTableBuilder::finish_block builds it (src/table/builder.rs:112-123:
+ * the encoded block, then put_u32(crc32(block))).  blk_off[b] = where block b starts; its CRC sits
+ * at the block's end, and (without SEG_SLOTS) blk_off[b + 1] = blk_off[b] + block size + 4, so
+ * lsmblk_decode_batch_ex(tail = 4, LSMBLK_DECODE_VERIFY_CRC) reads the output as read_block reads
+ * the file.  stats[1] counts the CRC bytes too.  With SEG_SLOTS the slot bound is 22 bytes per
+ * entry instead of 18 (4 more per block, at most one block per entry) and seg_out[2 s + 1] includes
+ * the segment's CRCs.  The CRCs are a pass over the encoded blocks (the streaming CRC kernel of
+ * lsmblk_crc32_batch) after emit. */
+#define LSMBLK_ENCODE_FRAMED 2u
 int lsmblk_encode_batch_ex(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* seg_start,
                            uint32_t nseg, uint32_t block_size, uint32_t flags, uint8_t* out,
                            uint64_t out_cap, uint64_t* blk_off, uint64_t blk_cap, uint64_t* seg_out,

@@ -25,6 +25,7 @@ LSMBLK_E_INTERNAL = -8
 LSMBLK_E_CHECKSUM = -9
 LSMBLK_DECODE_VERIFY_CRC = 1
 LSMBLK_ENCODE_SEG_SLOTS = 1
+LSMBLK_ENCODE_FRAMED = 2
 LSMBLK_DEBUG_ENCODE_FUSED = 8
 LSMBLK_SHARD_LAST = 1
 LSMBLK_MERGE_RUNS = 0

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from ._lib import (CompactOptsC, KVStreamC, KeyRangeC, LSMBLK_DECODE_VERIFY_CRC, LSMBLK_E_CAPACITY,
-                   LSMBLK_ENCODE_SEG_SLOTS, LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
+                   LSMBLK_ENCODE_FRAMED, LSMBLK_ENCODE_SEG_SLOTS, LSMBLK_MERGE_RUNS, LSMBLK_MERGE_TWO_LEVEL, LSMBLK_SHARD_LAST, LsmBlkError, check, lib)
 
 STATS_WORDS = 4
 _ctx_lock = threading.Lock()
@@ -292,16 +292,17 @@ def decode_blocks(blocks: torch.Tensor, blk_off: torch.Tensor, stream=None, tail
     raise LsmBlkError(LSMBLK_E_CAPACITY, "decode_blocks")
 
 
-def encode_bound(kv: KVStream, key_bytes: int, val_bytes: int):
-    """Exact worst-case output sizes: (bytes, blk_off entries)."""
-    return key_bytes + val_bytes + 18 * kv.n + 16, kv.n + 2
+def encode_bound(kv: KVStream, key_bytes: int, val_bytes: int, framed: bool = False):
+    """Exact worst-case output sizes: (bytes, blk_off entries); framed: + 4 CRC bytes per block."""
+    return key_bytes + val_bytes + (22 if framed else 18) * kv.n + 16, kv.n + 2
 
 
 def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: int, out, out_cap,
-                blk_off, blk_cap, stats, stream=None, seg_out=None):
+                blk_off, blk_cap, stats, stream=None, seg_out=None, framed=False):
     """Asynchronous encode into preallocated buffers (no host sync).  With seg_out (int64[2 nseg])
     the output is per-segment slots (LSMBLK_ENCODE_SEG_SLOTS, include/lsmblk.h): every segment's
-    blocks at its own slot, seg_out[s] = (slot, bytes); slots_to_packed packs them."""
+    blocks at its own slot, seg_out[s] = (slot, bytes); slots_to_packed packs them.  framed: every
+    block followed by its big-endian crc32 -- the SST data section (LSMBLK_ENCODE_FRAMED)."""
     dev = _dev_index(seg_start)
     kv.check(dev, "kv")
     _need(seg_start, torch.int32, "seg_start", dev, nseg + 1)
@@ -309,15 +310,44 @@ def encode_into(kv: KVStream, seg_start: torch.Tensor, nseg: int, block_size: in
     _need(blk_off, torch.int64, "blk_off", dev, blk_cap)
     _need(stats, torch.int64, "stats", dev, STATS_WORDS)
     c = kv._c()
-    if seg_out is None:
+    if seg_out is None and not framed:
         _native("lsmblk_encode_batch", dev, stream, ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
                 _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, stats.data_ptr(),
                 _stream_ptr(stream, dev), what="lsmblk_encode_batch")
         return
-    _need(seg_out, torch.int64, "seg_out", dev, 2 * nseg)
+    if seg_out is not None:
+        _need(seg_out, torch.int64, "seg_out", dev, 2 * nseg)
+    flags = (LSMBLK_ENCODE_SEG_SLOTS if seg_out is not None else 0) | (LSMBLK_ENCODE_FRAMED if framed else 0)
     _native("lsmblk_encode_batch_ex", dev, stream, ctypes.byref(c), seg_start.data_ptr(), nseg, block_size,
-            LSMBLK_ENCODE_SEG_SLOTS, _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, seg_out.data_ptr(),
+            flags, _ptr(out), out_cap, blk_off.data_ptr(), blk_cap, _ptr(seg_out),
             stats.data_ptr(), _stream_ptr(stream, dev), what="lsmblk_encode_batch_ex")
+
+
+def encode_kv_framed(kv: KVStream, seg_start, block_size: int, stream=None, slots: bool = False):
+    """The SST data sections of kv's segments (LSMBLK_ENCODE_FRAMED): every block followed by its
+    big-endian crc32fast, as SsTableBuilder::finish_block writes them (reference
+    src/table/builder.rs:112-123).  -> (out u8 tensor, blk_off int64 tensor[nblk+1]) -- packed:
+    blk_off[b+1] - blk_off[b] = block b's size + 4, the layout lsmblk_decode_batch_ex(tail=4)
+    reads; with slots=True also seg_out int64 tensor[nseg, 2] (every segment at its slot)."""
+    dev = torch.device("cuda", _dev_index(kv.key_off))
+    seg_start = _u32_table(seg_start, dev)
+    nseg = seg_start.numel() - 1
+    kb, vb = kv.byte_sizes()
+    out_cap, blk_cap = encode_bound(kv, kb, vb, framed=True)
+    out = _aligned_empty(out_cap, dev)
+    blk_off = torch.zeros(blk_cap, dtype=torch.int64, device=dev)
+    seg_out = torch.zeros(max(2 * nseg, 1), dtype=torch.int64, device=dev) if slots else None
+    stats = torch.zeros(STATS_WORDS, dtype=torch.int64, device=dev)
+    encode_into(kv, seg_start, nseg, block_size, out, out_cap, blk_off, blk_cap, stats, stream, seg_out=seg_out,
+                framed=True)
+    torch.cuda.synchronize(dev)
+    st = _status(stats)
+    if st:
+        raise LsmBlkError(st, "encode_kv_framed")
+    nblk, nbytes = stats[0].item(), stats[1].item()
+    if slots:
+        return out, blk_off[:nblk + 1], seg_out[:2 * nseg].view(-1, 2)
+    return out[:nbytes], blk_off[:nblk + 1]
 
 
 def encode_kv_slots(kv: KVStream, seg_start, block_size: int, stream=None):

@@ -813,6 +813,10 @@ int fork_aux(lsmblk_ctx* c, hipStream_t st);
 int join_aux(lsmblk_ctx* c, hipStream_t st);
 int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                uint32_t* crc, uint64_t* stats, hipStream_t st, uint32_t* agg = nullptr, bool sections = false);
+// LSMBLK_ENCODE_FRAMED: every block's CRC written big-endian after it (the encode's block table;
+// its count read on the device from stats[0], nothing after an encode error).
+int launch_crc_frames(lsmblk_ctx* c, uint8_t* out, const uint64_t* blk_off, const uint32_t* blk_sz,
+                      uint64_t nblk_max, uint64_t* stats, hipStream_t st);
 // lsmblk_block_meta_batch with the context lock held.
 int block_meta_locked(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, uint64_t nblk, uint32_t tail,
                       const uint32_t* seg_blk, uint32_t nseg, uint8_t* meta, uint64_t meta_cap, uint64_t* meta_off,

@@ -1302,6 +1302,7 @@ struct PlanArgs {
   uint64_t* seg_out;
   uint32_t* blk_sz;
   uint32_t pipe_helper;    // the helper's loads pipelined over chunks (plan_produce_pipe)
+  uint32_t frame;          // LSMBLK_ENCODE_FRAMED: 4 bytes (the block's CRC) after every block, else 0
 };
 
 __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
@@ -1317,9 +1318,11 @@ __device__ __forceinline__ PlanArgs resolve(const PlanArgs& a0) {
 // Callers pass validated entry indices b = seg_start[0] and s = seg_start[g] (b <= s <= n): the
 // table's raw entries are never used as array indices here (a table like
 // [0, 0xFFFFFFFF, n] made the walker of segment 1 read key_off[0xFFFFFFFF] after flagging it).
-__device__ __forceinline__ uint64_t seg_slot(const uint32_t* key_off, const uint32_t* val_off, uint32_t b, uint32_t s) {
+// Framed output (LSMBLK_ENCODE_FRAMED) adds 4 bytes per block, at most one block per entry: 22 per entry.
+__device__ __forceinline__ uint64_t seg_slot(const uint32_t* key_off, const uint32_t* val_off, uint32_t b, uint32_t s,
+                                             uint32_t frame = 0) {
   if (s <= b) return 0;
-  return uint64_t(key_off[s] - key_off[b]) + uint64_t(val_off[s] - val_off[b]) + 18ull * (s - b);
+  return uint64_t(key_off[s] - key_off[b]) + uint64_t(val_off[s] - val_off[b]) + (18ull + frame) * (s - b);
 }
 
 constexpr uint32_t kAlcpUnsorted = 0x80000000u;
@@ -1843,6 +1846,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     // blocks | HW_ID (wave, SIMD, CU, SE) << 32 | XCC_ID << 56: where the walker ran
     tr[7] = nb | (uint64_t(__builtin_amdgcn_s_getreg(0xF804)) << 32) | (uint64_t(__builtin_amdgcn_s_getreg(0x1814) & 0xF) << 56);
   }
+  bytes += uint64_t(a.frame) * nb;  // (framed: every block's CRC after it, written by the CRC pass)
   // make this wave's record stores visible to its own later loads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1861,7 +1865,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
   // slot mode: segment 0 starts at 0 (checked by its own walker, err SEGMENTS otherwise); a
   // segment whose own bounds were refused gets slot 0 and writes nothing (emit: kPlanFatal)
   uint64_t O0 = excl[1];
-  if (a.seg_out) O0 = (err & LSMBLK_ERR_SEGMENTS) ? 0ull : seg_slot(a.key_off, a.val_off, 0u, s0);
+  if (a.seg_out) O0 = (err & LSMBLK_ERR_SEGMENTS) ? 0ull : seg_slot(a.key_off, a.val_off, 0u, s0, a.frame);
   const uint64_t B0 = excl[0];
   if (a.seg_out && l == 0) {
     a.seg_out[2ull * g] = O0;
@@ -1875,12 +1879,13 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
       first = a.rec_first[s0 + i];
       sz = a.sz[s0 + i];
     }
-    const uint64_t incl = wave_incl_scan<uint64_t>(sz);
+    const uint64_t ext = i < nb ? uint64_t(sz) + a.frame : 0ull;  // the block and its frame
+    const uint64_t incl = wave_incl_scan<uint64_t>(ext);
     if (i < nb) {
       const uint64_t bi = B0 + i;
       a.blk_first[bi] = first;
       if (a.blk_sz) a.blk_sz[bi] = sz;
-      if (bi < a.blk_cap) a.blk_off[bi] = oc + incl - sz;
+      if (bi < a.blk_cap) a.blk_off[bi] = oc + incl - ext;
     }
     oc += __shfl(incl, 63, 64);
   }
@@ -3155,6 +3160,12 @@ struct CrcStreamArgs {
   uint32_t* crc;
   const CrcStreamTabs* tabs;
   uint64_t* stats;
+  // framed encode (LSMBLK_ENCODE_FRAMED): the encode's own blocks, nblk read from the device (the
+  // encode's stats[0]; none after any encode error), block b = [blk_off[b], + sz[b]), and its CRC
+  // written big-endian right after it (finish_block, src/table/builder.rs:118-122) instead of to crc
+  uint8_t* frame_out;
+  const uint32_t* sz;
+  const uint64_t* dnblk;
 };
 
 __global__ __launch_bounds__(1024) void crc_stream_kernel(CrcStreamArgs a) {
@@ -3164,9 +3175,10 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(CrcStreamArgs a) {
   for (uint32_t i = t; i < sizeof(CrcStreamTabs) / 16; i += 64 * kCsWaves)
     reinterpret_cast<u32x4*>(&S)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
   for (uint32_t e = t; e < 4 * 256 * 32; e += 64 * kCsWaves) rep[e] = (&a.tabs->a256[0][0])[e >> 5];
-  if (blockIdx.x == 0 && t == 0) {
-    a.stats[0] = a.nblk;
-    a.stats[1] = a.nblk ? a.blk_off[a.nblk] - a.blk_off[0] : 0;
+  const uint64_t nblk = a.dnblk ? (a.stats[3] ? 0ull : *a.dnblk) : a.nblk;
+  if (blockIdx.x == 0 && t == 0 && !a.frame_out) {
+    a.stats[0] = nblk;
+    a.stats[1] = nblk ? a.blk_off[nblk] - a.blk_off[0] : 0;
   }
   __syncthreads();
   const uint8_t* const R8 = reinterpret_cast<const uint8_t*>(rep);
@@ -3180,15 +3192,15 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(CrcStreamArgs a) {
     return xor3(a0, a1, a2) ^ a3;
   };
   uint32_t err = 0;
-  const uint64_t ngrp = (a.nblk + 3) / 4, nw = uint64_t(gridDim.x) * kCsWaves;
+  const uint64_t ngrp = (nblk + 3) / 4, nw = uint64_t(gridDim.x) * kCsWaves;
   // lanes 0..4: blk_off[4 G + lane], the group's block offsets (loaded one group ahead)
   auto offs = [&](uint64_t G) -> uint64_t {
-    return G < ngrp && l <= 4 && 4 * G + l <= a.nblk ? a.blk_off[4 * G + l] : 0ull;
+    return G < ngrp && l <= 4 && 4 * G + l <= nblk ? a.blk_off[4 * G + l] : 0ull;
   };
   uint64_t G = uni64(uint64_t(blockIdx.x) * kCsWaves + w);
   uint64_t onext = offs(G);
   for (; G < ngrp; G += nw) {
-    const uint64_t b0 = G * 4, nb = a.nblk - b0 < 4 ? a.nblk - b0 : 4;  // blocks of this wave
+    const uint64_t b0 = G * 4, nb = nblk - b0 < 4 ? nblk - b0 : 4;  // blocks of this wave
     uint64_t Sx[5];
 #pragma unroll
     for (uint32_t k = 0; k < 5; ++k) Sx[k] = lane64(onext, k);
@@ -3196,9 +3208,10 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(CrcStreamArgs a) {
     const bool have = g < nb;
     const uint64_t s = g == 0 ? Sx[0] : g == 1 ? Sx[1] : g == 2 ? Sx[2] : Sx[3];
     const uint64_t e = g == 0 ? Sx[1] : g == 1 ? Sx[2] : g == 2 ? Sx[3] : Sx[4];
-    const bool valid = have && e >= s + a.tail && e - s <= 0x7FFFFFF0ull;
+    const uint32_t fsz = a.sz && have ? a.sz[b0 + g] : 0u;  // (framed: the block's size from the plan)
+    const bool valid = have && (a.sz ? fsz <= 0x7FFFFFF0u : e >= s + a.tail && e - s <= 0x7FFFFFF0ull);
     if (have && !valid) err |= LSMBLK_ERR_MALFORMED;
-    const uint32_t L = valid ? uint32_t(e - s) - a.tail : 0u;
+    const uint32_t L = !valid ? 0u : a.sz ? fsz : uint32_t(e - s) - a.tail;
     const uint32_t T = (0u - L) & 15u, nch = (L + T + 4095) >> 12, P = (nch << 12) - L - T;
     const uint64_t S0 = Sx[0], Se = Sx[nb];
     // one descriptor over the wave's blocks when they lie inside [S0, Se) (adjacent ranges do)
@@ -3276,7 +3289,12 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(CrcStreamArgs a) {
     }
     if (have && lq == 0) {
       const uint32_t r = crc_apply(S.unzt[T], acc);
-      a.crc[b0 + g] = L ? ~r : 0u;
+      const uint32_t v = L ? ~r : 0u;
+      if (a.crc) a.crc[b0 + g] = v;
+      if (a.frame_out && valid) {  // big-endian, as put_u32 writes it
+        uint8_t* f = a.frame_out + s + L;
+        f[0] = uint8_t(v >> 24), f[1] = uint8_t(v >> 16), f[2] = uint8_t(v >> 8), f[3] = uint8_t(v);
+      }
     }
   }
 #pragma unroll
@@ -4145,7 +4163,7 @@ int lsmblk_encode_batch_ex(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint
                            uint64_t blk_cap, uint64_t* seg_out, uint64_t* stats, void* stream) {
   if (!c || !in || !seg_start || !blk_off || !stats || !aligned16(out)) return LSMBLK_E_INVAL;
   if (in->n >= 0xFFFFFFFFull || !in->key_off || !in->val_off) return LSMBLK_E_INVAL;
-  if (block_size == 0 || (flags & ~uint32_t(LSMBLK_ENCODE_SEG_SLOTS))) return LSMBLK_E_INVAL;
+  if (block_size == 0 || (flags & ~uint32_t(LSMBLK_ENCODE_SEG_SLOTS | LSMBLK_ENCODE_FRAMED))) return LSMBLK_E_INVAL;
   if ((flags & LSMBLK_ENCODE_SEG_SLOTS) && !seg_out) return LSMBLK_E_INVAL;
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device, c);
@@ -4163,7 +4181,9 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
                   uint64_t* seg_out) {
   const KLogRange lr(c, &c->enc_log0, &c->enc_log1);
   const bool slots = (flags & LSMBLK_ENCODE_SEG_SLOTS) != 0;
+  const bool framed = (flags & LSMBLK_ENCODE_FRAMED) != 0;
   if (slots && (!seg_out || span || dn || dnseg)) return LSMBLK_E_INVAL;
+  if (framed && (span || dn || dnseg)) return LSMBLK_E_INVAL;
   // in->n (and nseg) are upper bounds when dn (dnseg) point at the device-side values
   int rc = reserve_locked(c, 0, in->n, nseg, st);
   if (rc) return rc;
@@ -4178,7 +4198,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
   // the fused walk + emit (A/B only: the walk's instructions compete with emit's for the same
   // issue slots): per-segment slots, blocks no larger than emit's LDS image
-  const bool fused = slots && block_size <= 4096 && c->fuse_on;
+  const bool fused = slots && !framed && block_size <= 4096 && c->fuse_on;
   uint32_t walk_wgs = 0, nwalk = 0;
   if (fused) {
     walk_wgs = uint32_t(std::min<uint64_t>(uint64_t(cus), (uint64_t(nseg) + 1) / 2));
@@ -4192,6 +4212,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
     if ((rc = grow(st, &c->fbig, &c->fbig_cap, recs, 1))) return rc;
     if (c->frec_cap != fc || c->fdone_cap != dc) c->epoch = 0;  // fresh granules: a new epoch sequence
   }
+  if (framed && (rc = ensure_crc_tabs(c, st))) return rc;
   if ((rc = next_epoch(c, st))) return rc;
   if (hipMemsetAsync(c->counters, 0, 2048, st) != hipSuccess) return LSMBLK_E_HIP;
   PlanArgs p;
@@ -4220,8 +4241,9 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   p.skip = c->skip;
   p.dbg = c->dbg_on ? c->dbg : nullptr;
   p.seg_out = slots ? seg_out : nullptr;
-  p.blk_sz = slots ? c->blk_sz : nullptr;
+  p.blk_sz = slots || framed ? c->blk_sz : nullptr;
   p.pipe_helper = c->plan_pipe ? 1u : 0u;
+  p.frame = framed ? 4u : 0u;
   EmitArgs e;
   e.keys = in->keys;
   e.key_off = in->key_off;
@@ -4236,7 +4258,7 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   e.n = in->n;
   e.stats = stats;
   e.big_flag = reinterpret_cast<uint8_t*>(c->big_list);
-  e.blk_sz = slots ? c->blk_sz : nullptr;
+  e.blk_sz = slots || framed ? c->blk_sz : nullptr;
   e.skip = c->skip;
   e.dn = dn;
   if (fused) {
@@ -4282,6 +4304,10 @@ int encode_locked(lsmblk_ctx* c, const lsmblk_kv_stream* in, const uint64_t* dn,
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&big_cu, emit_big_kernel, 256, 0) != hipSuccess || big_cu < 1)
     big_cu = 4;
   LSM_LAUNCH_SLOT(4, emit_big_kernel, dim3(uint32_t(cus) * uint32_t(big_cu)), dim3(256), 0, st, e);
+  if (framed) {  // every block's CRC after it: the SST data section (src/table/builder.rs:112-123)
+    const uint64_t nblk_max = blk_cap < in->n + 1 ? blk_cap : in->n + 1;
+    if ((rc = launch_crc_frames(c, out, blk_off, c->blk_sz, nblk_max, stats, st))) return rc;
+  }
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 
@@ -4501,6 +4527,9 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
     b.crc = crc;
     b.tabs = &static_cast<const CrcAllTabs*>(c->crc_tabs)->s;
     b.stats = stats;
+    b.frame_out = nullptr;
+    b.sz = nullptr;
+    b.dnblk = nullptr;
     const uint64_t want = (nblk + 4 * kCsWaves - 1) / (4 * kCsWaves);
     const uint32_t grid = uint32_t(want < uint64_t(cus) ? (want ? want : 1) : uint64_t(cus));
     LSM_LAUNCH(crc_stream_kernel, dim3(grid), dim3(64 * kCsWaves), 0, st, b);
@@ -4516,6 +4545,29 @@ int launch_crc(lsmblk_ctx* c, const uint8_t* blocks, const uint64_t* blk_off, ui
   const dim3 grid(uint32_t(want < cap ? want : cap));
   if (agg) LSM_LAUNCH(crc_kernel<true>, grid, dim3(256), 0, st, a);
   else LSM_LAUNCH(crc_kernel<false>, grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
+}
+
+// The CRCs of a framed encode's blocks, written after each block (LSMBLK_ENCODE_FRAMED): the
+// streaming CRC pass over the encode's own block table, its block count read on the device.
+int launch_crc_frames(lsmblk_ctx* c, uint8_t* out, const uint64_t* blk_off, const uint32_t* blk_sz,
+                      uint64_t nblk_max, uint64_t* stats, hipStream_t st) {
+  CrcStreamArgs b;
+  b.blocks = out;
+  b.blk_off = blk_off;
+  b.nblk = nblk_max;
+  b.tail = 4;
+  b.crc = nullptr;
+  b.tabs = &static_cast<const CrcAllTabs*>(c->crc_tabs)->s;
+  b.stats = stats;
+  b.frame_out = out;
+  b.sz = blk_sz;
+  b.dnblk = stats;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const uint64_t want = (nblk_max + 4 * kCsWaves - 1) / (4 * kCsWaves);
+  const uint32_t grid = uint32_t(want < uint64_t(cus) ? (want ? want : 1) : uint64_t(cus));
+  LSM_LAUNCH(crc_stream_kernel, dim3(grid), dim3(64 * kCsWaves), 0, st, b);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
 }
 }  // namespace lsmblk_impl lsmblk_impl

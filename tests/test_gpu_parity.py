@@ -72,6 +72,41 @@ def slot_check(kv: O.KV, seg, block_size, ref_blocks, ref_off):
         assert mism.size == 0, f"slots (fused={fused}): first mismatching byte {mism[:8]} of {len(got)}"
 
 
+def framed_want(ref_blocks, ref_off):
+    """The SST data section of packed blocks: every block followed by its crc32fast, big-endian
+    (SsTableBuilder::finish_block, src/table/builder.rs:112-123) -> (bytes, offsets u64[nblk+1])."""
+    parts, offs, o = [], [0], 0
+    for b in range(len(ref_off) - 1):
+        blk = bytes(ref_blocks[int(ref_off[b]):int(ref_off[b + 1])])
+        parts.append(blk + zlib.crc32(blk).to_bytes(4, "big"))
+        o += len(blk) + 4
+        offs.append(o)
+    return b"".join(parts), np.asarray(offs, np.uint64)
+
+
+def framed_check(kv: O.KV, seg, block_size, ref_blocks, ref_off):
+    """LSMBLK_ENCODE_FRAMED, packed and with per-segment slots: the output is the blocks each
+    followed by its BE crc32, the verifying framed decode (tail 4) reads it back."""
+    want, want_off = framed_want(ref_blocks, ref_off)
+    d = to_dev(kv)
+    out, off = batch.encode_kv_framed(d, seg, block_size)
+    np.testing.assert_array_equal(off.cpu().numpy().view(np.uint64), want_off)
+    assert out.cpu().numpy().tobytes() == want
+    if len(ref_off) > 1:
+        dkv = batch.decode_blocks(out, off, tail=4, verify=True)
+        assert dkv.n == kv.n
+        k, ko, v, vo, ts = dkv.to_numpy()
+        np.testing.assert_array_equal(ko, kv.key_off)
+        np.testing.assert_array_equal(ts, kv.ts[:kv.n])
+    sout, soff, so = batch.encode_kv_framed(d, seg, block_size, slots=True)
+    so = so.cpu().numpy()
+    s = np.asarray(seg, dtype=np.int64)
+    ko, vo = kv.key_off.astype(np.int64), kv.val_off.astype(np.int64)
+    np.testing.assert_array_equal(so[:, 0], (ko[s[:-1]] - ko[s[0]]) + (vo[s[:-1]] - vo[s[0]]) + 22 * (s[:-1] - s[0]))
+    host = sout.cpu().numpy()
+    assert b"".join(host[a:a + n].tobytes() for a, n in so) == want
+
+
 def roundtrip_check(kv: O.KV, seg, block_size, shift=0):
     """GPU encode == oracle encode (packed, and per-segment slots); GPU decode(oracle blocks) ==
     oracle decode."""
@@ -85,6 +120,7 @@ def roundtrip_check(kv: O.KV, seg, block_size, shift=0):
     mism = np.flatnonzero(got != ref_blocks)
     assert mism.size == 0, f"first mismatching byte {mism[:8]} of {len(got)}"
     slot_check(kv, seg, block_size, ref_blocks, ref_off)
+    framed_check(kv, seg, block_size, ref_blocks, ref_off)
     rc, ref_kv = O.decode_blocks(ref_blocks, ref_off)
     assert rc == 0
     db, do = dev_blocks(ref_blocks, ref_off, shift)
@@ -748,8 +784,8 @@ def test_slot_encode_refuses_missing_seg_out_and_bad_flags():
     assert f(ctx, ctypes.byref(c), seg_t.data_ptr(), 1, 4096, 1, out.data_ptr(), 1 << 20, off.data_ptr(), kv.n + 2,
              None, st.data_ptr(), None) != 0
     so = torch.zeros(2, dtype=torch.int64, device="cuda")
-    assert f(ctx, ctypes.byref(c), seg_t.data_ptr(), 1, 4096, 2, out.data_ptr(), 1 << 20, off.data_ptr(), kv.n + 2,
-             so.data_ptr(), st.data_ptr(), None) != 0
+    assert f(ctx, ctypes.byref(c), seg_t.data_ptr(), 1, 4096, 4, out.data_ptr(), 1 << 20, off.data_ptr(), kv.n + 2,
+             so.data_ptr(), st.data_ptr(), None) != 0  # (flag 4: unknown; 2 is LSMBLK_ENCODE_FRAMED)
 
 
 def _slot_encode_raw(kv_dev, seg, bs, out_cap=None, fused=0):
@@ -862,3 +898,44 @@ def test_encode_refuses_an_empty_key(mode):
     assert status == LSMBLK_E_INVAL
     if mode == "packed":
         assert bool((out == 0xA5).all())
+
+
+def test_framed_encode_is_the_sst_builders_data_section():
+    """LSMBLK_ENCODE_FRAMED of one segment == the data section of the SST file that
+    oracle/pyref.py's line-by-line SsTableBuilder restatement writes (its bytes before
+    meta_offset, src/table/builder.rs:68-98 + 112-123), for the week1_day3 KAT entries at two
+    block sizes and a U sample; and the BlockMeta offsets of that file are the framed blk_off."""
+    from oracle import pyref
+    cases = [(week1_day3_kv(), 128), (week1_day3_kv(), 4096), (O.KV(*synth.gen_uniform(3000, seed=31)), 4096)]
+    for kv, bs in cases:
+        ents = kv.entries()
+        f = pyref.sst_file(ents, bs)
+        out, off = batch.encode_kv_framed(to_dev(kv), [0, kv.n], bs)
+        data = out.cpu().numpy().tobytes()
+        assert f[:len(data)] == data
+        metas = pyref.sst_block_metas(ents, bs)
+        assert [m[0] for m in metas] == off.cpu().numpy()[:-1].tolist()
+
+
+def test_framed_encode_u_large_equals_blocks_and_crcs():
+    """At 400 K entries: the framed encode == the packed encode with lsmblk_crc32_batch's CRCs
+    interleaved (and a sample of them == zlib), the verifying framed decode reads it back."""
+    kv = O.KV(*synth.gen_uniform(400_000, seed=33))
+    seg = synth.segments_by_bytes(kv.key_off, kv.val_off, 2 << 20)
+    d = to_dev(kv)
+    blocks, boff = batch.encode_kv(d, seg, 4096)
+    crc = batch.crc32_blocks(blocks, boff).cpu().numpy().view(np.uint32)
+    out, off = batch.encode_kv_framed(d, seg, 4096)
+    b, o = blocks.cpu().numpy(), boff.cpu().numpy()
+    fo = off.cpu().numpy()
+    nblk = len(o) - 1
+    assert len(fo) == nblk + 1 and fo[-1] == o[-1] + 4 * nblk
+    np.testing.assert_array_equal(fo[:-1], o[:-1] + 4 * np.arange(nblk))
+    f = out.cpu().numpy()
+    ends = fo[1:] - 4
+    got_crc = (f[ends[:, None] + np.arange(4)].astype(np.uint32) << np.array([24, 16, 8, 0], np.uint32)).sum(1)
+    np.testing.assert_array_equal(got_crc.astype(np.uint32), crc)
+    for i in range(0, nblk, max(1, nblk // 50)):
+        assert zlib.crc32(b[o[i]:o[i + 1]].tobytes()) == int(crc[i])
+    dkv = batch.decode_blocks(out, off, tail=4, verify=True)
+    assert dkv.n == kv.n
