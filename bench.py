@@ -90,6 +90,7 @@ def parse(argv=None):
     p.add_argument("--trace-fused", action="store_true",
                    help="diagnostics: the fused walk + emit launch's per-walker trace and emitter record waits")
     p.add_argument("--ablate-only", action="store_true", help="diagnostics: time only mask 0 and --ablate")
+    p.add_argument("--ablate-decode", action="store_true", help="diagnostics: --ablate is a decode mask")
     p.add_argument("--ablate", type=int, default=None,
                    help="diagnostics: time decode alone with this skip mask (prints a non-bench line)")
     return p.parse_args(argv)
@@ -306,9 +307,9 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
             check(lib().lsmblk_debug_set(ctx, 1, 0))
             print(json.dumps({"ablation_plan_ms_by_skip_mask": res}), flush=True)
             return None
-        if 16 <= args.ablate < 256:  # encode-side masks: per-kernel times with the mask applied
+        if (16 <= args.ablate < 256 or args.ablate == 1) and not args.ablate_decode:  # encode-side masks
             res = {}
-            for mask in (0, 16, 32, 64, 112, 128, 240):
+            for mask in (0, 1, 16, 32, 64, 112, 128, 240):
                 check(lib().lsmblk_debug_set(ctx, 1, mask))
                 step()
                 res[mask] = kernel_times(ctx, step, dev, reps=2)["emit"]
@@ -374,7 +375,7 @@ def run_blocks(args, cfg, steps, warmup, rank, world, local, dev, extra=False):
                      "step_frac": round((algo["decode"] + algo["emit"]) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "cpu_baseline": None,
     }
-    if extra:
+    if extra or not ok_all:  # (the side legs read the step's outputs; a failed round trip ends the run)
         return result
     result["framing_crc32"] = framing_crc32(blocks, blk_off, nblk, E, dev, stream)
     result["read_path_verify"] = read_path_verify(blocks, blk_off, nblk, out_kv, n, K, V, st_dec, dev, stream)

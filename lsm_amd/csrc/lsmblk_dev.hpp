@@ -241,18 +241,35 @@ __device__ __forceinline__ void raise_err(uint64_t* stats, uint32_t err) {
 // GlbImg reads global memory through a bounds-checked buffer descriptor (OOB reads = 0).
 // Decode reads the (unswizzled) LDS image with unaligned ds_read_u16/b32/b64/b128 (the gfx9
 // unaligned access mode): one instruction per field instead of one per byte.
+#ifndef LSMBLK_XALIGNED_LDS
+#define LSMBLK_XALIGNED_LDS 0
+#endif
+// 4 / 8 bytes at byte x of a 16-B-aligned LDS buffer (any alignment) from aligned dwords: the LDS
+// array serves a misaligned access with extra passes (PMC SQ_LDS_UNALIGNED_STALL), two or three
+// aligned dword reads + v_alignbyte do not stall.
+__device__ __forceinline__ uint32_t lds_dw_al(const uint8_t* base, uint32_t x) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(base, 16)) + (x >> 2);
+  return __builtin_amdgcn_alignbyte(d[1], d[0], x & 3);
+}
+__device__ __forceinline__ u32x2 lds_qw_al(const uint8_t* base, uint32_t x) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(base, 16)) + (x >> 2);
+  const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], sh = x & 3;
+  return u32x2{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh)};
+}
 struct LdsImg {
   const uint8_t* base;  // LDS image; block byte 0 is image byte lead
   uint32_t lead;
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return base[lead + i]; }
   __device__ __forceinline__ uint32_t u16(uint32_t i) const {
+    if constexpr (LSMBLK_XALIGNED_LDS) return bswap16(lds_dw_al(base, lead + i) & 0xFFFFu);
     return bswap16(*reinterpret_cast<const uint16_t*>(base + lead + i));
   }
   __device__ __forceinline__ uint32_t le32(uint32_t i) const {
+    if constexpr (LSMBLK_XALIGNED_LDS) return lds_dw_al(base, lead + i);
     return *reinterpret_cast<const uint32_t*>(base + lead + i);
   }
   __device__ __forceinline__ uint64_t u64(uint32_t i) const {
-    const u32x2 q = *reinterpret_cast<const u32x2*>(base + lead + i);
+    const u32x2 q = LSMBLK_XALIGNED_LDS ? lds_qw_al(base, lead + i) : *reinterpret_cast<const u32x2*>(base + lead + i);
     return __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
   }
 };

@@ -242,6 +242,15 @@ struct LdsSink {
   }
 };
 
+// Experiment switch (default off): the value copy of a staged (LDS) wave as 16-B-aligned output
+// chunks, each funnel-shifted from 8-B-aligned image reads.  Measured round 6 (U, lag 0): the
+// decode's unaligned-LDS stall cycles halve (8.2e8 -> 3.6e8) but bank conflicts rise 14x
+// (2.2e7 -> 3.0e8: the staged values sit at a ~128-B stride, so lanes reading the same chunk of
+// their values share banks) and VALU +46%; net 2.04 vs 2.05 ms, within noise.  Rotating each
+// lane's chunk order spreads the banks (1.2e8) but its VALU makes the kernel 2-6% slower.
+#ifndef LSMBLK_XDEC_VALN
+#define LSMBLK_XDEC_VALN 0
+#endif
 // Fast path, lane per entry: every entry lane writes its own key and value as contiguous
 // runs of 16-B pieces (the last piece overlaps the previous one), so runs of adjacent
 // entries abut and no lane needs a chunk -> entry search.
@@ -272,10 +281,31 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
     const bool kuni = !__ballot(kirr);
     const uint32_t nkmax = __builtin_amdgcn_readlane(wave_incl_max32(live ? (kl + 15) >> 4 : 0u), 63);
     const uint32_t nvmax = __builtin_amdgcn_readlane(wave_incl_max32(live && vl >= 16 ? (vl + 15) >> 4 : 0u), 63);
+    // Aligned value path (values composed in the LDS output image, at most 64 entries, every value
+    // >= 16 B): lane k writes the 16-B-aligned image chunks that start inside its value, each built
+    // from 8-B-aligned reads of the staged image and a byte funnel shift; the chunk that runs past
+    // the value's end takes the rest from the next value (lane k + 1).  The misaligned 16-B LDS reads
+    // and writes of the piece copies below cost the LDS array extra passes (PMC SQ_LDS_UNALIGNED_STALL;
+    // the same accesses moved to aligned addresses, a timing probe: decode 2.14 -> 1.96 ms at U).
+    const uint32_t vS = sb + s + 10, vD = out.vb + vout;  // the value's image / output-image bytes
+    bool valn = false;
+    uint32_t vm = 0, vmmax = 0, vS1 = 0, vD1 = 0;
+    if constexpr (std::is_same_v<Sink, LdsSink>) {
+      // (lane 0 also writes the chunk holding the run's first byte, read from vS - (vD & 15) on)
+      valn = LSMBLK_XDEC_VALN && it == 0 && n <= 64 && !__ballot(live && (vl < 16 || (l == 0 && vS < (vD & 15)))) &&
+             !(skip & (4 | 32 | 64));
+      if (valn) {  // (wave-uniform)
+        const uint32_t cs = l == 0 ? (vD >> 4) : ((vD + 15) >> 4), ce = (vD + vl - 1) >> 4;
+        vm = live ? ce - cs + 1 : 0u;
+        vmmax = __builtin_amdgcn_readlane(wave_incl_max32(vm), 63);
+        vS1 = uint32_t(__shfl(int(vS), int(min(l + 1, 63u)), 64));
+        vD1 = uint32_t(__shfl(int(vD), int(min(l + 1, 63u)), 64));
+      }
+    }
     if (!live) continue;
     if (!(skip & 8)) {
       const uint64_t e = E0 + k;
-      const u32x2 q = *reinterpret_cast<const u32x2*>(img + sb + s);
+      const u32x2 q = LSMBLK_XALIGNED_LDS ? lds_qw_al(img, sb + s) : *reinterpret_cast<const u32x2*>(img + sb + s);
       a.ts[e] = __builtin_bswap64((uint64_t(q.y) << 32) | q.x);
       a.key_off[e] = uint32_t(K0 + kout);
       a.val_off[e] = uint32_t(V0 + vout);
@@ -323,21 +353,75 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
         }
       }
     }
-    if (!(skip & 4)) {
+    if (valn) {
+      uint8_t* const ob = L.out;
+      // 16 bytes of the staged image at byte x (any alignment) from the 8-B-aligned dwords d[0..5]
+      // that start at x & ~7: a dword select by bit 2, then v_alignbyte by x & 3
+      // (the dword select by mask, not `b2 ? d[j + 1] : d[j]`: the compiler turned that into a
+      // dynamically indexed array in scratch memory -- decode 3.35 ms)
+      auto funnel = [](const uint32_t (&d)[6], uint32_t x, uint32_t (&v)[4]) {
+        const uint32_t m = (x & 4) ? ~0u : 0u;
+        uint32_t y[5];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) y[j] = __builtin_amdgcn_bitop3_b32(m, d[j + 1], d[j], 0xCA);  // m ? d[j + 1] : d[j]
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_alignbyte(y[i + 1], y[i], x & 3);
+      };
+      auto rd8 = [&](uint32_t x, uint32_t& lo, uint32_t& hi) {  // (x 8-B aligned)
+        const u32x2 q = *reinterpret_cast<const u32x2*>(img + x);
+        lo = q.x, hi = q.y;
+      };
+      const uint32_t cs = l == 0 ? (vD >> 4) : ((vD + 15) >> 4);
+      const uint32_t a0 = vS + 16 * cs - vD;  // image byte of chunk cs's first byte (>= 0, see valn)
+uint32_t d[6], x8 = a0 & ~7u;
+      rd8(x8, d[0], d[1]);
+      rd8(x8 + 8, d[2], d[3]);
+      rd8(x8 + 16, d[4], d[5]);
+      for (uint32_t i = 0; i < vmmax; ++i) {
+        if (i < vm) {
+          uint32_t v[4];
+          funnel(d, a0, v);
+          const uint32_t c = cs + i, cut = vD + vl - 16 * c;  // bytes of the chunk from this value
+          if (cut < 16 && k + 1 < n) {  // the rest from the next value
+            const uint32_t a1 = vS1 + 16 * c - vD1, y8 = a1 & ~7u;
+            uint32_t e[6], w[4];
+            rd8(y8, e[0], e[1]);
+            rd8(y8 + 8, e[2], e[3]);
+            rd8(y8 + 16, e[4], e[5]);
+            funnel(e, a1, w);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+              const int32_t nb = int32_t(cut) - int32_t(4 * q);  // leading bytes of dword q from this value
+              const uint32_t msk = nb <= 0 ? 0u : nb >= 4 ? ~0u : (1u << (8 * nb)) - 1;
+              v[q] = (v[q] & msk) | (w[q] & ~msk);
+            }
+          }
+          *reinterpret_cast<u32x4*>(ob + 16 * c) = u32x4{v[0], v[1], v[2], v[3]};
+          d[0] = d[4], d[1] = d[5];
+          x8 += 16;
+          rd8(x8 + 8, d[2], d[3]);
+          rd8(x8 + 16, d[4], d[5]);
+        }
+      }
+    } else if (!(skip & 4)) {
       const uint32_t src = sb + s + 10;  // image byte of the value
       if (vl >= 16) {
         for (uint32_t i0 = 0; i0 < nvmax; i0 += kLB) {  // uniform trip count, pieces clamped
           u32x4 q[kLB];
           uint32_t o[kLB];
+          // (diagnostics builds, ablation masks 32 / 64: the same accesses moved to 16- / 4-byte
+          // aligned addresses -- timing probes of the misaligned accesses' cost, bytes wrong)
+          const uint32_t am = (skip & 32) ? 15u : (skip & 64) ? 3u : 0u;
 #pragma unroll
           for (uint32_t j = 0; j < kLB; ++j) {
             o[j] = min(16 * (i0 + j), vl - 16);
-            q[j] = *reinterpret_cast<const u32x4*>(img + src + o[j]);
+            q[j] = *reinterpret_cast<const u32x4*>(img + ((src + o[j]) & ~am));
           }
 #pragma unroll
           for (uint32_t j = 0; j < kLB; ++j) {
             const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-            out.put16(true, vout + o[j], v);
+            const uint32_t xa = (out.vb + vout + o[j]) & ~am;
+            out.put16(true, xa >= out.vb ? xa - out.vb : xa + am + 1 - out.vb, v);
           }
         }
       } else if (vl) {
@@ -2015,6 +2099,9 @@ struct EmitPf {
   uint64_t ts = 0;
 };
 
+// (diagnostics builds, ablation mask 1: emit's misaligned LDS accesses moved to aligned addresses --
+// a timing probe of their cost, the bytes are wrong)
+#define EAL(x, m) ((diag_mask(a.skip) & 1u) ? ((x) & ~uint32_t(m)) : (x))
 // Phase 1 of emit_kernel for block B (staged and landed): returns the block's data length, ncs =
 // its image chunks; eh / et = the first / last 16 bytes of the value of entries l, l + 64.
 __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, const EmitBlk& B, const EmitPf& pf,
@@ -2059,7 +2146,7 @@ __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, c
         uint32_t z = 16;
 #pragma unroll
         for (int i = 3; i >= 0; --i) {
-          const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, klead + kp + 4 * i);
+          const uint32_t x = fkw[i] ^ lds_dword_at(L.kimg, EAL(klead + kp + 4 * i, 3));
           z = x ? 4 * i + (__builtin_ctz(x) >> 3) : z;
         }
         p = z < 16 && z < m ? z : m;  // (z == 16: m unless the loop below finds a difference)
@@ -2074,8 +2161,8 @@ __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, c
         }
       }
       const uint32_t vs = vlead + vp;
-      lds_read16(L.img, vs, eh[it]);
-      lds_read16(L.img, vs + (vl > 16 ? vl - 16 : 0u), et[it]);
+      lds_read16(L.img, EAL(vs, 15), eh[it]);
+      lds_read16(L.img, EAL(vs + (vl > 16 ? vl - 16 : 0u), 15), et[it]);
     }
     const uint32_t dg = k < n ? kl + vl + 14 - p : 0;
     const uint32_t incl = wave_incl_scan<uint32_t>(dg);
@@ -2125,7 +2212,7 @@ __device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const
       }
 #pragma unroll
       for (uint32_t j = 0; j < kEB; ++j)
-        if (src[j] != ~0u) v[j] = *reinterpret_cast<const u32x4*>(L.img + src[j]);
+        if (src[j] != ~0u) v[j] = *reinterpret_cast<const u32x4*>(L.img + EAL(src[j], 15));
 #pragma unroll
       for (uint32_t j = 0; j < kEB; ++j)
         if (src[j] != ~0u) *reinterpret_cast<u32x4*>(L.img + 16 * (c0 - int32_t(64 * (j + 1)) + int32_t(l))) = v[j];
@@ -2147,23 +2234,23 @@ __device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const
       // unaligned LDS stores (the image is not swizzled): every field is one or two stores
       uint8_t* o = L.img;
       const uint32_t ox = olead + pos;
-      *reinterpret_cast<uint32_t*>(o + ox) = bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16);
+      *reinterpret_cast<uint32_t*>(o + EAL(ox, 3)) = bswap16(p & 0xFFFF) | (bswap16(sfx & 0xFFFF) << 16);
       for (uint32_t t = 0; t < sfx; t += 16) {
         const uint32_t o2 = sfx >= 16 ? min(t, sfx - 16) : 0u;
         uint32_t v[4];
-        lds_read16(L.kimg, ks + o2, v);
-        if (sfx >= 16) *reinterpret_cast<u32x4*>(o + ox + 4 + o2) = u32x4{v[0], v[1], v[2], v[3]};
+        lds_read16(L.kimg, EAL(ks + o2, 15), v);
+        if (sfx >= 16) *reinterpret_cast<u32x4*>(o + EAL(ox + 4 + o2, 15)) = u32x4{v[0], v[1], v[2], v[3]};
         else lds_st_short(o + ox + 4, sfx, v);
       }
       const uint64_t tbe = __builtin_bswap64(tsv);
-      *reinterpret_cast<u32x2*>(o + ox + 4 + sfx) = u32x2{uint32_t(tbe), uint32_t(tbe >> 32)};
-      *reinterpret_cast<uint16_t*>(o + ox + 12 + sfx) = uint16_t(bswap16(vl & 0xFFFF));
+      *reinterpret_cast<u32x2*>(o + EAL(ox + 4 + sfx, 7)) = u32x2{uint32_t(tbe), uint32_t(tbe >> 32)};
+      *reinterpret_cast<uint16_t*>(o + EAL(ox + 12 + sfx, 1)) = uint16_t(bswap16(vl & 0xFFFF));
       // value bytes outside whole chunks: a value of >= 16 bytes rewrites its first and last
       // 16 (the bytes inside whole chunks are rewritten with what the move put there)
       const uint32_t A = olead + vd;
       if (vl >= 16) {
-        *reinterpret_cast<u32x4*>(o + A) = u32x4{eh[it][0], eh[it][1], eh[it][2], eh[it][3]};
-        *reinterpret_cast<u32x4*>(o + A + vl - 16) = u32x4{et[it][0], et[it][1], et[it][2], et[it][3]};
+        *reinterpret_cast<u32x4*>(o + EAL(A, 15)) = u32x4{eh[it][0], eh[it][1], eh[it][2], eh[it][3]};
+        *reinterpret_cast<u32x4*>(o + EAL(A + vl - 16, 15)) = u32x4{et[it][0], et[it][1], et[it][2], et[it][3]};
       } else if (vl) {
         lds_st_short(o + A, vl, eh[it]);
       }
