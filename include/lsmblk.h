@@ -57,7 +57,7 @@ extern "C" {
 enum {
   LSMBLK_OK = 0,
   LSMBLK_E_INVAL = -1,     /* bad argument: empty key, empty build, bad segment table, misaligned output */
-  LSMBLK_E_MALFORMED = -2, /* a block does not parse (the reference would panic) */
+  LSMBLK_E_MALFORMED = -2, /* a block does not parse (the reference would panic); an encode input's offsets decrease */
   LSMBLK_E_CAPACITY = -3,  /* an output buffer is too small; the stats hold the required sizes */
   LSMBLK_E_NOMEM = -4,     /* host or device allocation failed */
   LSMBLK_E_HIP = -5,       /* a HIP runtime call failed */
@@ -226,7 +226,8 @@ int lsmblk_decode_batch_ex(lsmblk_ctx* ctx, const uint8_t* blocks, const uint64_
  * packing at every segment start (seg_start u32[nseg+1], seg_start[0] = 0, seg_start[nseg]
  * = in->n, non-decreasing), exactly as one SsTableBuilder per segment would.  Blocks are
  * written tightly packed to `out` (16-byte aligned, out_cap bytes); blk_off (u64, room for
- * blk_cap values) receives nblk+1 offsets. */
+ * blk_cap values) receives nblk+1 offsets.  key_off / val_off must be non-decreasing: an entry whose
+ * offsets decrease fails the call with LSMBLK_ERR_MALFORMED and nothing is written. */
 int lsmblk_encode_batch(lsmblk_ctx* ctx, const lsmblk_kv_stream* in, const uint32_t* seg_start,
                         uint32_t nseg, uint32_t block_size, uint8_t* out, uint64_t out_cap,
                         uint64_t* blk_off, uint64_t blk_cap, uint64_t* stats, void* stream);

@@ -242,14 +242,16 @@ struct LdsSink {
   }
 };
 
-// Experiment switch (default off): the value copy of a staged (LDS) wave as 16-B-aligned output
-// chunks, each funnel-shifted from 8-B-aligned image reads.  Measured round 6 (U, lag 0): the
-// decode's unaligned-LDS stall cycles halve (8.2e8 -> 3.6e8) but bank conflicts rise 14x
-// (2.2e7 -> 3.0e8: the staged values sit at a ~128-B stride, so lanes reading the same chunk of
-// their values share banks) and VALU +46%; net 2.04 vs 2.05 ms, within noise.  Rotating each
-// lane's chunk order spreads the banks (1.2e8) but its VALU makes the kernel 2-6% slower.
+// Value copies of a staged (LDS) wave as 16-B-aligned output chunks, each funnel-shifted from
+// 8-B-aligned image reads (LSMBLK_XDEC_VALN, round 6; 0 = the unaligned 16-B pieces below).
+// PMC at U (profiles/r06_pmc_lds_decode_{old,new}.txt): unaligned-LDS stall cycles 8.2e8 -> 3.6e8,
+// LDS issue waits 4.7e8 -> 1.2e8 (0.60 -> 0.20 of all instruction waits), bank conflicts 2.2e7 ->
+// 3.0e8 (the staged values sit at a ~128-B stride, so lanes reading the same chunk of their values
+// share banks), VALU +46 %; decode 2.050 against 2.060 ms (three alternating pairs, one box).
+// Rotating each lane's chunk order spreads the banks (1.2e8) but its VALU made the kernel 2-6 %
+// slower (not kept).
 #ifndef LSMBLK_XDEC_VALN
-#define LSMBLK_XDEC_VALN 0
+#define LSMBLK_XDEC_VALN 1
 #endif
 // Fast path, lane per entry: every entry lane writes its own key and value as contiguous
 // runs of 16-B pieces (the last piece overlaps the previous one), so runs of adjacent
@@ -373,7 +375,7 @@ __device__ __forceinline__ void dec_entry_runs(const DecodeArgs& a, DecLds& L, u
       };
       const uint32_t cs = l == 0 ? (vD >> 4) : ((vD + 15) >> 4);
       const uint32_t a0 = vS + 16 * cs - vD;  // image byte of chunk cs's first byte (>= 0, see valn)
-uint32_t d[6], x8 = a0 & ~7u;
+      uint32_t d[6], x8 = a0 & ~7u;
       rd8(x8, d[0], d[1]);
       rd8(x8 + 8, d[2], d[3]);
       rd8(x8 + 16, d[4], d[5]);
@@ -1517,7 +1519,11 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
       for (uint32_t i = 0; i < kProdBatch; ++i) {
         const uint32_t e = c + 64 * (h + i) + l;
         if (e >= cend) continue;
-        const uint32_t kl = kn[i] - kp[i], x = (e - s0) & (kRing - 1);
+        // offsets that decrease (a corrupt stream) are refused, and the entry is walked as a
+        // 1-byte key and an empty value so that no loop below runs over a wrapped length
+        const bool inv = kn[i] < kp[i] || v1[i] < v0[i];
+        if (inv) err |= LSMBLK_ERR_MALFORMED;
+        const uint32_t kl = inv ? 1u : kn[i] - kp[i], x = (e - s0) & (kRing - 1);
         if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
         uint32_t al = 0;
         if (e != s0 && !nokeys) {  // as plan_adj_kernel: LCP with the predecessor, bit 31 = out of order
@@ -1560,7 +1566,7 @@ __device__ void plan_produce(const PlanArgs& a, const PlanKeys& K, uint32_t s0, 
           const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
           al = (lcp < kAlcpLcp ? lcp : kAlcpLcp) | (sorted ? 0u : kAlcpUnsorted);
         }
-        CR[x] = kl + (v1[i] - v0[i]);
+        CR[x] = inv ? kl : kl + (v1[i] - v0[i]);
         CA[x] = al;
       }
     }
@@ -1647,14 +1653,14 @@ __device__ __forceinline__ void walk_segment(const PlanArgs& a, const PlanKeys& 
       if (!direct && __ballot(al & kAlcpUnsorted)) {  // an out-of-order pair inside this block
         direct = true;
         sp = a.key_off[s];
-        sl = a.key_off[s + 1] - sp;
+        sl = a.key_off[s + 1] >= sp ? a.key_off[s + 1] - sp : 0u;  // (decreasing offsets: refused by the helper)
       }
       uint32_t p = 0;
       if (!direct) {
         p = min(pmin, wave_incl_min31(al & kAlcpLcp));
         pmin = __builtin_amdgcn_readlane(p, 63);
       } else if (valid && e != s) {
-        const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
+        const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] >= kp ? a.key_off[e + 1] - kp : 0u;
         uint32_t w0, w1;
         p = key_lcp(K, sp, sl, kp, kl, w0, w1);
       }
@@ -1817,7 +1823,9 @@ __device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t
     for (uint32_t i = 0; i < kPipeB; ++i) {
       const uint32_t e = c + 64 * i + l;
       if (e >= cend) continue;
-      const uint32_t kp = P.kp[i], pp = P.pp[i], kl = P.kn[i] - kp, x = (e - s0) & (kRing - 1);
+      const bool inv = P.kn[i] < P.kp[i] || P.v1[i] < P.v0[i];  // (refused, as plan_produce)
+      if (inv) err |= LSMBLK_ERR_MALFORMED;
+      const uint32_t kp = P.kp[i], pp = P.pp[i], kl = inv ? 1u : P.kn[i] - kp, x = (e - s0) & (kRing - 1);
       if (kl == 0) err |= LSMBLK_ERR_EMPTY_KEY;
       uint32_t al = 0;
       if (e != s0) {  // LCP with the predecessor, bit 31 = out of order (as plan_produce)
@@ -1856,7 +1864,7 @@ __device__ void plan_produce_pipe(const PlanArgs& a, const PlanKeys& K, uint32_t
         const bool sorted = lcp == m ? pl <= kl : ((w0 >> sh) & 0xFF) < ((w1 >> sh) & 0xFF);
         al = (lcp < kAlcpLcp ? lcp : kAlcpLcp) | (sorted ? 0u : kAlcpUnsorted);
       }
-      CR[x] = kl + (P.v1[i] - P.v0[i]);
+      CR[x] = inv ? kl : kl + (P.v1[i] - P.v0[i]);
       CA[x] = al;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1906,6 +1914,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(4)
     if (a.pipe_helper) plan_produce_pipe(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
     else plan_produce(a, K, s0, s1, CR, CA, &hand_prod[ww], &hand_cons[ww], err, tr);
     const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
+                          (__ballot(err & LSMBLK_ERR_MALFORMED) ? LSMBLK_ERR_MALFORMED : 0u) |
                           (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
     raise_err(a.stats, werr);
     return;
@@ -2084,14 +2093,15 @@ struct EmitMeta {
 // The plan's error flags that leave its block tables unusable: emit then writes nothing (a
 // refused segment table gave blocks whose end entry precedes their start, which emit_big walked
 // as ~2^32 entries).  CAPACITY is not one: every block that fits is still written.
-constexpr uint64_t kPlanFatal = LSMBLK_ERR_SEGMENTS | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_INTERNAL | LSMBLK_ERR_EMPTY_KEY;
+constexpr uint64_t kPlanFatal =
+    LSMBLK_ERR_SEGMENTS | LSMBLK_ERR_TIMEOUT | LSMBLK_ERR_INTERNAL | LSMBLK_ERR_EMPTY_KEY | LSMBLK_ERR_MALFORMED;
 
 // One fast-path block of emit (wave-uniform): entries [s, s + n), output [O, O + size), its keys
 // staged at kimg[klead], its values at img[vlead], fl = its first key's length.
 struct EmitBlk {
   uint32_t s, n;
   uint64_t O, size;
-  uint32_t kb0, vb0, klead, vlead, olead, fl;
+  uint32_t kb0, vb0, klead, vlead, olead, fl, kb1, vb1;
 };
 // The first 64 entries' offsets and ts of a block, loaded by entry lane k one block ahead.
 struct EmitPf {
@@ -2134,11 +2144,17 @@ __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, c
         vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1];
         L.ts[k] = a.ts[s + k];
       }
-      kp = ko0 - kb0;
-      kl = ko1 - ko0;
-      vp = vo0 - vb0;
-      vl = vo1 - vo0;
-      if (k != 0 && !(diag_mask(a.skip) & 128)) {
+      // an entry outside its block's byte ranges or of negative length (offsets that decrease:
+      // the plan helper refuses such a stream, but the fused launch emits while it walks) is
+      // emptied and reported, so no loop below runs over a wrapped length
+      const bool inv = ko0 < kb0 || ko1 < ko0 || ko1 - kb0 > B.kb1 - kb0 || vo0 < vb0 || vo1 < vo0 ||
+                       vo1 - vb0 > B.vb1 - vb0;
+      if (inv) err |= LSMBLK_ERR_MALFORMED;
+      kp = inv ? 0u : ko0 - kb0;
+      kl = inv ? 0u : ko1 - ko0;
+      vp = inv ? 0u : vo0 - vb0;
+      vl = inv ? 0u : vo1 - vo0;
+      if (k != 0 && !inv && !(diag_mask(a.skip) & 128)) {
         // the first 16 bytes by selects, no branches: z = the first differing byte (16 if none);
         // bytes read past either key do not matter, p is capped at m (the key image has 16 B
         // of slack before the value image, which is LDS too)
@@ -2180,7 +2196,8 @@ __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, c
       }
     }
   }
-  if (uint64_t(dc) + 2ull * n + 2 != size) err |= LSMBLK_ERR_INTERNAL;
+  // (a block holding an emptied entry has the wrong length by construction: MALFORMED says why)
+  if (uint64_t(dc) + 2ull * n + 2 != size && !(err & LSMBLK_ERR_MALFORMED)) err |= LSMBLK_ERR_INTERNAL;
   return dc;
 }
 
@@ -2310,7 +2327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   auto is_fast = [&](const EmitMeta& m) {
     const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
     // the staged values and the encoded block share the image (24 B of read slack)
-    return !m.bad && m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
+    return !m.bad && m.n <= kEmitMaxE && m.kb1 >= m.kb0 && m.vb1 >= m.vb0 && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
            vlead + (m.vb1 - m.vb0) + 24 <= kEmitICap && uint32_t(m.O & 15) + m.size + 8 <= kEmitICap;
   };
   // a block off the fast path: beyond the LDS image -> flagged for emit_big_kernel; refused -> error
@@ -2401,7 +2418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       r_vb1 = a.val_off[nxt.e];
     }
     wave_sync();
-    const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl};
+    const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl, kb1, vb1};
     uint32_t eh[2][4], et[2][4];  // first / last 16 bytes of the value of entries l, l + 64
     uint32_t ncs;
     const uint32_t data_len = emit_phase1(a, L, B, pf, eh, et, ncs, err);
@@ -2691,6 +2708,7 @@ __device__ void fuse_walk(const FuseArgs& f, uint32_t* ring) {
   if (wv >= 2) {
     plan_produce_pipe(a, K, S0, S1, CR, CA, prod, cons, err);
     const uint32_t werr = (__ballot(err & LSMBLK_ERR_EMPTY_KEY) ? LSMBLK_ERR_EMPTY_KEY : 0u) |
+                          (__ballot(err & LSMBLK_ERR_MALFORMED) ? LSMBLK_ERR_MALFORMED : 0u) |
                           (__ballot(err & LSMBLK_ERR_TIMEOUT) ? LSMBLK_ERR_TIMEOUT : 0u);
     raise_err(a.stats, werr);
     return;
@@ -2805,7 +2823,8 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
   };
   auto is_fast = [&](const EmitMeta& m) {
     const uint32_t klead = uint32_t((kaddr + m.kb0) & 15), vlead = uint32_t((vaddr + m.vb0) & 15);
-    return m.n <= kEmitMaxE && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
+    // (decreasing bounds: not fast; the helper has refused the stream, so emit_big writes nothing)
+    return m.n <= kEmitMaxE && m.kb1 >= m.kb0 && m.vb1 >= m.vb0 && klead + (m.kb1 - m.kb0) + 8 <= kEmitKCap &&
            vlead + (m.vb1 - m.vb0) + 24 <= kEmitICap && uint32_t(m.O & 15) + m.size + 8 <= kEmitICap;
   };
   u32x4 kq[2], vq[5];
@@ -2884,7 +2903,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
       r_vb1 = a.val_off[nxt.e];
     }
     wave_sync();
-    const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl};
+    const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl, kb1, vb1};
     uint32_t eh[2][4], et[2][4];
     uint32_t ncs;
     const uint32_t data_len = emit_phase1(a, L, B, pf, eh, et, ncs, err);

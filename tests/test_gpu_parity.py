@@ -900,6 +900,39 @@ def test_encode_refuses_an_empty_key(mode):
         assert bool((out == 0xA5).all())
 
 
+@pytest.mark.parametrize("mode", ["packed", "slots", "fused"])
+@pytest.mark.parametrize("which", ["key_off", "val_off"])
+def test_encode_refuses_decreasing_offsets(mode, which):
+    """A KV stream whose key or value offsets decrease (a corrupt stream: an entry of wrapped,
+    ~4 GiB length) fails the call with LSMBLK_E_MALFORMED -- the plan helpers' flag, one of the
+    plan's fatal flags -- and nothing is written (the packed output keeps its fill bytes); the walk
+    never runs over the wrapped lengths."""
+    ents = [(b"k%05d" % i, i, b"v" * 40) for i in range(600)]
+    d = to_dev(O.KV.from_entries(ents))
+    arr = getattr(d, which)
+    arr[301] = arr[299]  # entry 300 ends before it starts
+    seg = [0, 250, 600]
+    if mode == "packed":
+        cap, blk_cap = batch.encode_bound(d, 600 * 6, 600 * 40)
+        out = batch._aligned_empty(cap, "cuda")
+        out.fill_(0xA5)
+        off = torch.zeros(blk_cap, dtype=torch.int64, device="cuda")
+        st = torch.zeros(4, dtype=torch.int64, device="cuda")
+        seg_t = torch.tensor(seg, dtype=torch.int32, device="cuda")
+        batch.encode_into(d, seg_t, len(seg) - 1, 4096, out, cap, off, blk_cap, st)
+        torch.cuda.synchronize()
+        status = batch._status(st)
+    else:
+        status, st, out, off, so = _slot_encode_raw(d, seg, 4096, fused=int(mode == "fused"))
+    if mode == "fused":  # (emits while it walks: another block's size self-check may fail first)
+        from lsm_amd._lib import LSMBLK_E_INTERNAL
+        assert status in (LSMBLK_E_MALFORMED, LSMBLK_E_INTERNAL)
+    else:
+        assert status == LSMBLK_E_MALFORMED
+    if mode == "packed":
+        assert bool((out == 0xA5).all())
+
+
 def test_framed_encode_is_the_sst_builders_data_section():
     """LSMBLK_ENCODE_FRAMED of one segment == the data section of the SST file that
     oracle/pyref.py's line-by-line SsTableBuilder restatement writes (its bytes before
