@@ -759,25 +759,6 @@ __device__ __forceinline__ int key_cmp16(const GKeys& G, const u32x4& x, uint32_
   return key_cmp(G, pa + 16, la - 16, pb + 16, lb - 16);
 }
 
-// mkeep with the merged predecessor ip's key compare already done (same: equal user keys).
-__device__ __forceinline__ bool mkeep(const GatherArgs& a, uint64_t j, uint32_t i, uint32_t ip, bool same) {
-  if (!a.rules) return true;
-  const uint64_t t = a.ts[i];
-  if (t > a.wm) return true;
-  const bool start = !(j > 0 && same);
-  if (!start && a.ts[ip] <= a.wm) return false;  // a later version at or below the watermark
-  if (a.bottom && start && a.val_off[i + 1] == a.val_off[i]) return false;  // :244-254
-  const uint32_t k0 = a.key_off[i], kl = a.key_off[i + 1] - k0;
-  for (uint32_t f = 0; f < a.npfx; ++f) {  // CompactionFilter::Prefix, :264-275
-    const uint32_t f0 = a.pfx_off[f], fl = a.pfx_off[f + 1] - f0;
-    if (fl > kl) continue;
-    bool m = true;
-    for (uint32_t x = 0; x < fl && m; ++x) m = a.pfx[f0 + x] == a.keys[k0 + x];
-    if (m) return false;
-  }
-  return true;
-}
-
 __device__ __forceinline__ bool prefix_filtered(const GatherArgs& a, uint32_t i) {
   const uint32_t k0 = a.key_off[i], kl = a.key_off[i + 1] - k0;
   for (uint32_t f = 0; f < a.npfx; ++f) {
@@ -826,42 +807,92 @@ __global__ __launch_bounds__(256) void mgroup_kernel(GatherArgs a) {
 __global__ __launch_bounds__(256) void mflag_kernel(GatherArgs a) {
   const uint64_t N = *a.nm;
   const GKeys G = gkeys(a.keys, a.key_off[a.n_max]);
+  // Every thread loads its own merged entry (input index, key position and length, first 16 key
+  // bytes, value length, ts) once and takes its merged predecessor's from the neighbouring thread
+  // through LDS (thread 0 loads its predecessor): half the gathers of loading both per thread.
+  __shared__ u32x4 s16[256];
+  __shared__ uint32_t sidx[256], sk0[256], skl[256];
+  __shared__ uint64_t sts[256];
+  const uint32_t t = threadIdx.x;
   uint32_t c = 0;
   uint64_t kb = 0, vb = 0;
-#pragma unroll
+#pragma unroll 1
   for (uint32_t sub = 0; sub < kGTile / 256; ++sub) {
-    const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + threadIdx.x;
-    if (j < N) {
-      bool k = false;
-      uint32_t same = 0;
-      // the merged order must be non-decreasing in the user key: an unsorted input run (which
-      // MergeIterator assumes away, merge_iterator.rs:135-138) is reported, never followed.  One
-      // compare with the merged predecessor gives the order and the rules' same-key test.
-      const uint32_t i = a.perm[j], ip = j > 0 ? a.perm[j - 1] : 0u;
-      bool ordered = i < a.n_max && ip < a.n_max;
-      int cmp = -1;
-      if (ordered && j > 0) {
-        const uint32_t p0 = a.key_off[ip], p1 = a.key_off[i];
-        cmp = key_cmp16(G, a.k16[ip], p0, a.key_off[ip + 1] - p0, a.k16[i], p1, a.key_off[i + 1] - p1);
-        ordered = cmp <= 0;
+    const uint64_t j = uint64_t(blockIdx.x) * kGTile + sub * 256 + t;
+    const bool live = j < N;
+    const uint32_t i = live ? a.perm[j] : kNone;
+    const bool iv = live && i < a.n_max;
+    uint32_t k0 = 0, kl = 0, vl = 0;
+    u32x4 x16{0u, 0u, 0u, 0u};
+    uint64_t tsi = 0;
+    if (iv) {
+      k0 = a.key_off[i];
+      kl = a.key_off[i + 1] - k0;
+      vl = a.val_off[i + 1] - a.val_off[i];
+      x16 = a.k16[i];
+      if (a.rules) tsi = a.ts[i];
+    }
+    __syncthreads();  // (the previous round's neighbour reads are done)
+    s16[t] = x16;
+    sidx[t] = iv ? i : kNone;
+    sk0[t] = k0;
+    skl[t] = kl;
+    sts[t] = tsi;
+    __syncthreads();
+    if (!live) continue;
+    bool k = false;
+    uint32_t same = 0;
+    // the merged order must be non-decreasing in the user key: an unsorted input run (which
+    // MergeIterator assumes away, merge_iterator.rs:135-138) is reported, never followed.  One
+    // compare with the merged predecessor gives the order and the rules' same-key test.
+    uint32_t ip = 0, p0 = 0, pl = 0;
+    u32x4 p16{0u, 0u, 0u, 0u};
+    uint64_t tsp = 0;
+    if (t > 0) {
+      ip = sidx[t - 1];
+      p16 = s16[t - 1];
+      p0 = sk0[t - 1];
+      pl = skl[t - 1];
+      tsp = sts[t - 1];
+    } else if (j > 0) {
+      ip = a.perm[j - 1];
+      if (ip < a.n_max) {
+        p0 = a.key_off[ip];
+        pl = a.key_off[ip + 1] - p0;
+        p16 = a.k16[ip];
+        if (a.rules) tsp = a.ts[ip];
       }
-      if (ordered) {
-        if (a.two && a.rules) {
-          const uint32_t g = a.keep[j];
-          k = (g & 1u) && in_range(a, i);
-          same = g & 2u;
-        } else {
-          k = in_range(a, i) && mkeep(a, j, i, ip, cmp == 0);
-        }
+    }
+    bool ordered = iv && ip < a.n_max;
+    int cmp = -1;
+    if (ordered && j > 0) {
+      cmp = key_cmp16(G, p16, p0, pl, x16, k0, kl);
+      ordered = cmp <= 0;
+    }
+    if (ordered) {
+      if (a.two && a.rules) {
+        const uint32_t g = a.keep[j];
+        k = (g & 1u) && in_range(a, i);
+        same = g & 2u;
+      } else if (!in_range(a, i)) {
+        k = false;
+      } else if (!a.rules || tsi > a.wm) {
+        k = true;  // (above the watermark every version is kept)
       } else {
-        atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)LSMBLK_ERR_MALFORMED);
+        // the rules of the closed form (filt_keep, src/compact.rs:239-276) over the preloaded fields
+        const bool start = !(j > 0 && cmp == 0);
+        if (!start && tsp <= a.wm) k = false;               // a later version at or below the watermark
+        else if (a.bottom && start && vl == 0) k = false;   // :244-254
+        else k = !(a.npfx && prefix_filtered(a, i));        // CompactionFilter::Prefix, :264-275
       }
-      a.keep[j] = (k ? 1u : 0u) | same;
-      if (k) {
-        c += 1;
-        kb += a.key_off[i + 1] - a.key_off[i];
-        vb += a.val_off[i + 1] - a.val_off[i];
-      }
+    } else {
+      atomicOr(reinterpret_cast<unsigned long long*>(a.stats + 3), (unsigned long long)LSMBLK_ERR_MALFORMED);
+    }
+    a.keep[j] = (k ? 1u : 0u) | same;
+    if (k) {
+      c += 1;
+      kb += kl;
+      vb += vl;
     }
   }
   __shared__ uint64_t ws[4][3];
@@ -1308,20 +1339,58 @@ __device__ __forceinline__ uint32_t lcp_k16(const GKeys& G, const u32x4& x, uint
 
 __global__ __launch_bounds__(256) void rot_adj_kernel(RotArgs a) {
   const uint64_t n = rot_n(a);
-  const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint64_t e = uint64_t(blockIdx.x) * 256 + t;
+  if (a.kidx) {
+    // The kept keys through the merge input (see RotArgs).  Every thread loads its own entry's
+    // input index, key length and first 16 key bytes once and takes its predecessor's from the
+    // neighbouring thread through LDS (thread 0 loads its predecessor): half the gathers of
+    // loading both per thread.  The key arena positions are loaded only for a tie on 16 bytes.
+    __shared__ u32x4 s16[256];
+    __shared__ uint32_t sidx[256], slen[256];
+    uint32_t i = 0, kl = 0, vl = 0;
+    u32x4 x16{0u, 0u, 0u, 0u};
+    if (e < n) {
+      const uint32_t kp = a.key_off[e];
+      kl = a.key_off[e + 1] - kp;
+      vl = a.val_off[e + 1] - a.val_off[e];
+      i = a.kidx[e];
+      x16 = a.k16[i];
+    }
+    s16[t] = x16;
+    sidx[t] = i;
+    slen[t] = kl;
+    __syncthreads();
+    if (e >= n) return;
+    a.rec[e] = kl + vl;
+    uint32_t al = 0;
+    if (e > 0) {
+      uint32_t ip, pl;
+      u32x4 p16;
+      if (t > 0) {
+        ip = sidx[t - 1];
+        pl = slen[t - 1];
+        p16 = s16[t - 1];
+      } else {
+        ip = a.kidx[e - 1];
+        pl = a.key_off[e] - a.key_off[e - 1];
+        p16 = a.k16[ip];
+      }
+      const GKeys K = gkeys(a.akeys, a.akey_off[a.an]);
+      const bool tie = pl > 16 && kl > 16 && p16.x == x16.x && p16.y == x16.y && p16.z == x16.z && p16.w == x16.w;
+      int ord = 0;
+      const uint32_t lcp = lcp_k16(K, p16, tie ? a.akey_off[ip] : 0u, pl, x16, tie ? a.akey_off[i] : 0u, kl, &ord);
+      const bool same = a.ksame ? a.ksame[e] != 0 : ord == 0;
+      al = (lcp < kRotLcp ? lcp : kRotLcp) | (ord > 0 ? kRotUnsorted : 0u) | (same ? kRotSame : 0u);
+    }
+    a.alcp[e] = al;
+    return;
+  }
   if (e >= n) return;
   const uint32_t kp = a.key_off[e], kl = a.key_off[e + 1] - kp;
   a.rec[e] = kl + (a.val_off[e + 1] - a.val_off[e]);
   uint32_t al = 0;
-  if (e > 0 && a.kidx) {  // the kept keys through the merge input (see RotArgs)
-    const GKeys K = gkeys(a.akeys, a.akey_off[a.an]);
-    const uint32_t i = a.kidx[e], ip = a.kidx[e - 1];
-    const uint32_t pl = kp - a.key_off[e - 1];
-    int ord = 0;
-    const uint32_t lcp = lcp_k16(K, a.k16[ip], a.akey_off[ip], pl, a.k16[i], a.akey_off[i], kl, &ord);
-    const bool same = a.ksame ? a.ksame[e] != 0 : ord == 0;
-    al = (lcp < kRotLcp ? lcp : kRotLcp) | (ord > 0 ? kRotUnsorted : 0u) | (same ? kRotSame : 0u);
-  } else if (e > 0) {
+  if (e > 0) {
     const GKeys K = gkeys(a.keys, a.key_off[n]);
     const uint32_t pp = a.key_off[e - 1], pl = kp - pp;
     int ord = 0;
@@ -1466,7 +1535,48 @@ __global__ __launch_bounds__(256) void rot_double_kernel(RotArgs a, uint32_t k) 
   or_need(a.need + k, short_chain);
 }
 
-// Highest block-chain level computed (J / S levels 0 .. top).
+// Levels k and k + 1 from level k - 1 in one pass: J_k(s) = J_{k-1}(J_{k-1}(s)) and J_{k+1}(s) =
+// J_k(J_k(s)) = J_{k-1}^4(s) -- one linear read and three dependent gathers of level k - 1 (the
+// later gathers land a few tiles ahead, mostly in L2) instead of two passes that each read,
+// gather and write a whole level.  need[k] / need[k + 1] as two rot_double_kernel passes would set
+// them (no short chain at level k means none at k + 1: the rot_top walk never reads past it).
+__global__ __launch_bounds__(256) void rot_double2_kernel(RotArgs a, uint32_t k) {
+  if (!*(volatile uint32_t*)(a.need + k - 1)) return;  // every chain done one level down
+  const uint64_t n = rot_n(a);
+  const uint64_t s0 = uint64_t(xcd_tile(blockIdx.x, gridDim.x)) * 256 * kRotPer + threadIdx.x;
+  const uint64_t N1 = a.n_max + 1;
+  const u32x2* L0 = a.JS + (k - 1) * N1;
+  auto sat = [](uint64_t v) { return v > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(v); };
+  bool short1 = false, short2 = false;
+  u32x2 v[kRotPer], w[kRotPer], y[kRotPer], z[kRotPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) {
+    const uint64_t s = s0 + 256 * i;
+    v[i] = s <= n ? L0[s] : u32x2{0u, 0u};
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) w[i] = s0 + 256 * i <= n ? L0[v[i].x] : u32x2{0u, 0u};
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) y[i] = s0 + 256 * i <= n ? L0[w[i].x] : u32x2{0u, 0u};
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) z[i] = s0 + 256 * i <= n ? L0[y[i].x] : u32x2{0u, 0u};
+#pragma unroll
+  for (uint32_t i = 0; i < kRotPer; ++i) {
+    const uint64_t s = s0 + 256 * i;
+    if (s <= n) {
+      const uint64_t s1 = uint64_t(v[i].y) + w[i].y;                // S_k(s)
+      const uint64_t s2 = s1 + uint64_t(y[i].y) + z[i].y;          // S_k(s) + S_k(J_k(s))
+      a.JS[k * N1 + s] = u32x2{w[i].x, sat(s1)};
+      a.JS[(k + 1) * N1 + s] = u32x2{z[i].x, sat(s2)};
+      short1 = short1 || (w[i].x < n && s1 < a.target);
+      short2 = short2 || (z[i].x < n && s2 < a.target);
+    }
+  }
+  or_need(a.need + k, short1);
+  or_need(a.need + k + 1, short2);
+}
+
+// Highest block-chain level computed (J / S levels 0 .. top).// Highest block-chain level computed (J / S levels 0 .. top).
 __device__ __forceinline__ uint32_t rot_top(const RotArgs& a) {
   uint32_t kc = 1;
   while (kc < a.levels && a.need[kc - 1]) ++kc;
@@ -2044,7 +2154,16 @@ int rotation_chains(const RotArgs& r, hipStream_t st) {
   LSM_LAUNCH(rot_adj_kernel, dim3(g), dim3(256), 0, st, r);
   LSM_LAUNCH(rot_next_kernel, dim3(g), dim3(256), 0, st, r);
   const uint32_t gd = uint32_t((r.n_max + 1 + 256 * kRotPer - 1) / (256 * kRotPer));
-  for (uint32_t k = 1; k < r.levels; ++k) LSM_LAUNCH(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
+  // two levels per pass while two remain (rot_double2_kernel), then the last one alone
+  for (uint32_t k = 1; k < r.levels;) {
+    if (k + 1 < r.levels) {
+      LSM_LAUNCH(rot_double2_kernel, dim3(gd), dim3(256), 0, st, r, k);
+      k += 2;
+    } else {
+      LSM_LAUNCH(rot_double_kernel, dim3(gd), dim3(256), 0, st, r, k);
+      k += 1;
+    }
+  }
   if (kDiag && r.poison) LSM_LAUNCH(rot_poison_kernel, dim3(uint32_t((r.n_max / 3 + 256) / 256)), dim3(256), 0, st, r);
   LSM_LAUNCH(rot_f_kernel, dim3(uint32_t((r.n_max + 1 + 511) / 512)), dim3(256), 0, st, r);
   return hipGetLastError() == hipSuccess ? LSMBLK_OK : LSMBLK_E_HIP;
