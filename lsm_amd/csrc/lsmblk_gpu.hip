@@ -2114,6 +2114,10 @@ struct EmitPf {
 #define EAL(x, m) ((diag_mask(a.skip) & 1u) ? ((x) & ~uint32_t(m)) : (x))
 // Phase 1 of emit_kernel for block B (staged and landed): returns the block's data length, ncs =
 // its image chunks; eh / et = the first / last 16 bytes of the value of entries l, l + 64.
+// kChk: check every entry against its block's byte ranges (the fused launch, which emits while the
+// plan's helper may still be finding a corrupt stream; emit_kernel runs only after a plan without
+// fatal flags, whose helper has checked every entry's offsets).
+template <bool kChk>
 __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, const EmitBlk& B, const EmitPf& pf,
                                                 uint32_t (&eh)[2][4], uint32_t (&et)[2][4], uint32_t& ncs, uint32_t& err) {
   const uint32_t l = lane_id();
@@ -2144,11 +2148,11 @@ __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, c
         vo0 = a.val_off[s + k]; vo1 = a.val_off[s + k + 1];
         L.ts[k] = a.ts[s + k];
       }
-      // an entry outside its block's byte ranges or of negative length (offsets that decrease:
-      // the plan helper refuses such a stream, but the fused launch emits while it walks) is
-      // emptied and reported, so no loop below runs over a wrapped length
-      const bool inv = ko0 < kb0 || ko1 < ko0 || ko1 - kb0 > B.kb1 - kb0 || vo0 < vb0 || vo1 < vo0 ||
-                       vo1 - vb0 > B.vb1 - vb0;
+      // (kChk) an entry outside its block's byte ranges or of negative length (offsets that
+      // decrease: the plan helper refuses such a stream, but the fused launch emits while it
+      // walks) is emptied and reported, so no loop below runs over a wrapped length
+      const bool inv = kChk && (ko0 < kb0 || ko1 < ko0 || ko1 - kb0 > B.kb1 - kb0 || vo0 < vb0 || vo1 < vo0 ||
+                                vo1 - vb0 > B.vb1 - vb0);
       if (inv) err |= LSMBLK_ERR_MALFORMED;
       kp = inv ? 0u : ko0 - kb0;
       kl = inv ? 0u : ko1 - ko0;
@@ -2421,7 +2425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl, kb1, vb1};
     uint32_t eh[2][4], et[2][4];  // first / last 16 bytes of the value of entries l, l + 64
     uint32_t ncs;
-    const uint32_t data_len = emit_phase1(a, L, B, pf, eh, et, ncs, err);
+    const uint32_t data_len = emit_phase1<false>(a, L, B, pf, eh, et, ncs, err);
     // the level-2 loads have landed on every path (on the !has_next path there were none):
     // without this the waitcnt pass keeps them pending past the branch below and waits for
     // the next block's whole prefetch before the chunk moves reuse their registers
@@ -2906,7 +2910,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
     const EmitBlk B{s, n, O, size, kb0, vb0, klead, vlead, olead, fl, kb1, vb1};
     uint32_t eh[2][4], et[2][4];
     uint32_t ncs;
-    const uint32_t data_len = emit_phase1(a, L, B, pf, eh, et, ncs, err);
+    const uint32_t data_len = emit_phase1<true>(a, L, B, pf, eh, et, ncs, err);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
     if (has_next) {
       nxt.kb0 = uni(r_kb0);
