@@ -71,7 +71,13 @@ __device__ __forceinline__ void dbg_trace(uint64_t* dbg, uint64_t t, uint32_t k)
 // LDS reads per lane issued together before their uses (one LDS round trip per batch instead
 // of one per read): flushes, value copies, chunk moves.
 constexpr uint32_t kLB = 2;  // decode: 2 measured 1 % faster per step than 1, 4 slower (1.64 vs 1.58 ms)
-constexpr uint32_t kEB = 1;  // emit holds the next block's prefetch: 2 and 4 spill
+#ifndef LSMBLK_XEB
+#define LSMBLK_XEB 4
+#endif
+// Chunk groups per batch in emit's value moves and flush (all of a batch's LDS reads issued before
+// its uses).  Round 2: 2 and 4 spilled beside the next block's prefetch; round 6: 124 / 128 VGPRs, no
+// spill, emit 1.715 / 1.705 / 1.698 ms at 1 / 2 / 4 (alternating, one box).
+constexpr uint32_t kEB = LSMBLK_XEB;
 
 
 // LDS per single-wave workgroup is exactly 8 KiB, so 20 blocks are resident per CU (5 waves per
