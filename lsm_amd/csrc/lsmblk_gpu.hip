@@ -2212,6 +2212,7 @@ __device__ __forceinline__ uint32_t emit_phase1(const EmitArgs& a, EmitLds& L, c
 }
 
 // Phases 2b-3 of emit_kernel, the offsets table and the flush of block B's image.
+template <uint32_t EB>
 __device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const EmitBlk& B, uint32_t data_len,
                                             uint32_t ncs, const uint32_t (&eh)[2][4], const uint32_t (&et)[2][4]) {
   const uint32_t l = lane_id();
@@ -2219,7 +2220,7 @@ __device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const
   const uint64_t O = B.O, size = B.size;
   // Phase 2a (ascending): image chunk -> source byte of a chunk lying wholly inside one
   // value, else ~0 (the last entry whose value starts at or before the chunk by max-scan).
-  // kEB chunk groups per batch: every LDS read of the batch is issued before its uses.
+  // EB chunk groups per batch: every LDS read of the batch is issued before its uses.
   // (EMIT_DIRECT_CENT: the entry lanes wrote the map in phase 1)
   wave_sync();
   // Phase 2b (descending): move whole-value chunks to their place in the encoded block.
@@ -2229,19 +2230,19 @@ __device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const
   // unread.
   if (!(diag_mask(a.skip) & 32)) {
     const int32_t top = int32_t((ncs + 63) & ~63u);
-    for (int32_t c0 = top; c0 > 0; c0 -= int32_t(64 * kEB)) {
-      uint32_t src[kEB];
-      u32x4 v[kEB];
+    for (int32_t c0 = top; c0 > 0; c0 -= int32_t(64 * EB)) {
+      uint32_t src[EB];
+      u32x4 v[EB];
 #pragma unroll
-      for (uint32_t j = 0; j < kEB; ++j) {
+      for (uint32_t j = 0; j < EB; ++j) {
         const int32_t c = c0 - int32_t(64 * (j + 1)) + int32_t(l);
         src[j] = (c0 >= int32_t(64 * (j + 1)) && uint32_t(c) < ncs) ? L.cent[c] : ~0u;
       }
 #pragma unroll
-      for (uint32_t j = 0; j < kEB; ++j)
+      for (uint32_t j = 0; j < EB; ++j)
         if (src[j] != ~0u) v[j] = *reinterpret_cast<const u32x4*>(L.img + EAL(src[j], 15));
 #pragma unroll
-      for (uint32_t j = 0; j < kEB; ++j)
+      for (uint32_t j = 0; j < EB; ++j)
         if (src[j] != ~0u) *reinterpret_cast<u32x4*>(L.img + 16 * (c0 - int32_t(64 * (j + 1)) + int32_t(l))) = v[j];
     }
   }
@@ -2291,7 +2292,7 @@ __device__ __forceinline__ void emit_finish(const EmitArgs& a, EmitLds& L, const
   wave_sync();
   // flush the image: 16-B chunks; only the two end chunks can be partial
   // (a block past out_cap writes nothing: the plan pass has raised CAPACITY)
-  if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run_masked<kEB>(a.out + (O - olead), L.img, olead, uint32_t(size));
+  if (!(diag_mask(a.skip) & 64) && O + size <= a.out_cap) flush_run_masked<EB>(a.out + (O - olead), L.img, olead, uint32_t(size));
   wave_sync();
 }
 
@@ -2448,7 +2449,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       if (has_next) issue(nxt);
     }
     wave_sync();
-    emit_finish(a, L, B, data_len, ncs, eh, et);
+    emit_finish<kEB>(a, L, B, data_len, ncs, eh, et);
     if (!has_next) break;
     cur = nxt;
   }
@@ -2935,7 +2936,7 @@ __device__ void fuse_emit(const FuseArgs& f, EmitLds& L) {
       }
     }
     wave_sync();
-    emit_finish(a, L, B, data_len, ncs, eh, et);
+    emit_finish<1>(a, L, B, data_len, ncs, eh, et);  // (one chunk group: four spill beside the fused launch's walk state)
     if (!has_next) break;
     cur = nxt;
   }
